@@ -1,0 +1,326 @@
+"""
+Generate golden vectors by running the upstream Pyxu reference's own NumPy code path.
+
+Run in the build container only (needs ``/root/reference``):
+
+    python tests/golden/make_goldens.py
+
+Each case is written to ``tests/golden/<name>.npz`` with its inputs, parameters and the
+reference's outputs.  Nothing from the reference is copied: only data.  Stencil-family goldens are
+additionally checked against ``scipy.ndimage`` (the reference's own ground truth in
+``src/pyxu_tests/operator/linop/test_stencil.py:144-189``) before being written.
+"""
+import os
+import sys
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle", "refshim"))
+import boot  # noqa: E402,F401  (makes /root/reference/src importable)
+
+warnings.simplefilter("ignore")
+
+import scipy.ndimage as snd  # noqa: E402
+
+import pyxu.abc as pxa  # noqa: E402
+import pyxu.operator as pxo  # noqa: E402
+import pyxu.opt.solver as pxsl  # noqa: E402
+import pyxu.opt.stop as pxst  # noqa: E402
+import pyxu.runtime as pxrt  # noqa: E402
+
+WIDTHS = {"f32": pxrt.Width.SINGLE, "f64": pxrt.Width.DOUBLE}
+
+
+def save(name, **data):
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in data.items()})
+    print(f"wrote {name}.npz ({os.path.getsize(path)} B)")
+
+
+def phantom(shape, rng):
+    """Piecewise-constant rectangles in [0, 1]."""
+    x = np.zeros(shape)
+    for _ in range(6):
+        lo = [rng.integers(0, n // 2) for n in shape]
+        hi = [l + rng.integers(n // 8 + 1, n // 2 + 1) for l, n in zip(lo, shape)]
+        x[tuple(slice(l, h) for l, h in zip(lo, hi))] = rng.uniform(0.2, 1.0)
+    return x
+
+
+# ----------------------------------------------------------------------------- per-op goldens
+def gen_stencil():
+    rng = np.random.default_rng(0)
+    cases = [
+        # (arg_shape, separable, kernel shapes, modes)
+        ((17,), False, [(5,)], ["constant", "wrap", "reflect", "symmetric", "edge"]),
+        ((9, 11), True, [(3,), (4,)], ["constant", "wrap", "reflect", "symmetric", "edge", ("constant", "edge")]),
+        ((9, 11), False, [(3, 4)], ["constant", "wrap", "reflect", "symmetric", "edge"]),
+        ((6, 7, 8), True, [(3,), (1,), (5,)], ["constant", "symmetric"]),
+        ((6, 7, 8), False, [(2, 3, 2)], ["constant", "wrap"]),
+    ]
+    for w, width in WIDTHS.items():
+        dt = width.value
+        for ci, (arg_shape, sep, kshapes, modes) in enumerate(cases):
+            for mi, mode in enumerate(modes):
+                kern = [rng.standard_normal(ks) for ks in kshapes]
+                kern = [k.astype(dt) for k in kern]
+                if sep:
+                    center = [int(rng.integers(0, ks[0])) for ks in kshapes]
+                    kspec = kern
+                else:
+                    center = [int(rng.integers(0, n)) for n in kshapes[0]]
+                    kspec = kern[0]
+                x = rng.standard_normal((2, 3, int(np.prod(arg_shape)))).astype(dt)
+                z = rng.standard_normal((2, 3, int(np.prod(arg_shape)))).astype(dt)
+                with pxrt.Precision(width):
+                    op = pxo.Stencil(arg_shape=arg_shape, kernel=kspec, center=center, mode=mode)
+                    y = op.apply(x)
+                    a = op.adjoint(z)
+                    L = float(op.lipschitz)
+                # ground truth (reference test strategy): scipy.ndimage on the padded input
+                if mode == "constant":
+                    full = kern[0] if not sep else np.multiply.outer(*kern[:2]) if len(kern) == 2 else \
+                        np.multiply.outer(np.multiply.outer(kern[0], kern[1]), kern[2])
+                    origin = [c - (n // 2) for c, n in zip(center, full.shape)]
+                    ref = snd.correlate(x.reshape(6, *arg_shape).astype(np.float64), full.reshape(1, *full.shape).astype(np.float64),
+                                        mode="constant", origin=[0] + origin).reshape(x.shape)
+                    tol = 1e-4 if w == "f32" else 1e-10
+                    assert np.allclose(y, ref, atol=tol * max(1, np.abs(ref).max())), (arg_shape, mode)
+                save(
+                    f"stencil_{w}_c{ci}_m{mi}",
+                    arg_shape=np.array(arg_shape),
+                    separable=sep,
+                    n_kernels=len(kern),
+                    **{f"kernel{i}": k for i, k in enumerate(kern)},
+                    center=np.array(center),
+                    mode=np.array(mode if isinstance(mode, str) else list(mode)),
+                    x=x, y=y, z=z, adj=a, lipschitz=L,
+                )
+
+
+def gen_convolve_gaussian():
+    rng = np.random.default_rng(1)
+    for w, width in WIDTHS.items():
+        dt = width.value
+        for sigma in (1.0, 2.0):
+            arg_shape = (40, 37)
+            x = rng.standard_normal((2, int(np.prod(arg_shape)))).astype(dt)
+            z = rng.standard_normal((2, int(np.prod(arg_shape)))).astype(dt)
+            with pxrt.Precision(width):
+                op = pxo.Gaussian(arg_shape=arg_shape, sigma=sigma, truncate=3.0)
+                y, a = op.apply(x), op.adjoint(z)
+                taps = op._st_fw[0]._kernel.reshape(-1)
+            ref = snd.gaussian_filter(x.reshape(2, *arg_shape).astype(np.float64), sigma=(0, sigma, sigma), mode="constant", truncate=3.0)
+            assert np.allclose(y.reshape(ref.shape), ref, atol=1e-5 if w == "f32" else 1e-12)
+            save(f"gaussian_{w}_s{int(sigma)}", arg_shape=np.array(arg_shape), sigma=sigma, truncate=3.0, taps=taps, x=x, y=y, z=z, adj=a)
+        # Convolve (flipped correlation) with a non-symmetric separable kernel
+        arg_shape = (12, 15)
+        k0, k1 = rng.standard_normal(4).astype(dt), rng.standard_normal(3).astype(dt)
+        x = rng.standard_normal((int(np.prod(arg_shape)),)).astype(dt)
+        z = rng.standard_normal((int(np.prod(arg_shape)),)).astype(dt)
+        with pxrt.Precision(width):
+            op = pxo.Convolve(arg_shape=arg_shape, kernel=[k0, k1], center=(1, 2), mode="constant")
+            y, a = op.apply(x), op.adjoint(z)
+        save(f"convolve_{w}", arg_shape=np.array(arg_shape), kernel0=k0, kernel1=k1, center=np.array([1, 2]), x=x, y=y, z=z, adj=a)
+
+
+def gen_gradient():
+    rng = np.random.default_rng(2)
+    cases = [
+        dict(arg_shape=(13, 17)),
+        dict(arg_shape=(6, 7, 9)),
+        dict(arg_shape=(6, 7, 9), directions=(1, 2)),
+        dict(arg_shape=(13, 17), scheme="central", accuracy=2),
+        dict(arg_shape=(13, 17), scheme="backward", sampling=0.5),
+        dict(arg_shape=(13, 17), mode="symmetric"),
+    ]
+    for w, width in WIDTHS.items():
+        dt = width.value
+        for ci, kw in enumerate(cases):
+            arg_shape = kw["arg_shape"]
+            N = int(np.prod(arg_shape))
+            nd = len(kw.get("directions", arg_shape))
+            x = rng.standard_normal((3, N)).astype(dt)
+            z = rng.standard_normal((3, nd * N)).astype(dt)
+            kw2 = {k: v for k, v in kw.items() if k in ("scheme", "accuracy", "sampling")}
+            with pxrt.Precision(width):
+                op = pxo.Gradient(arg_shape=arg_shape, directions=kw.get("directions"), mode=kw.get("mode", "constant"), **kw2)
+                y, a = op.apply(x), op.adjoint(z)
+                L = float(op.lipschitz)
+            save(
+                f"gradient_{w}_c{ci}",
+                arg_shape=np.array(arg_shape),
+                directions=np.array(kw.get("directions", tuple(range(len(arg_shape))))),
+                scheme=kw.get("scheme", "forward"),
+                accuracy=kw.get("accuracy", 1),
+                sampling=kw.get("sampling", 1.0),
+                mode=kw.get("mode", "constant"),
+                x=x, y=y, z=z, adj=a, lipschitz=L,
+            )
+
+
+def gen_norms():
+    rng = np.random.default_rng(3)
+    for w, width in WIDTHS.items():
+        dt = width.value
+        arg_shape = (2, 7, 5)
+        N = int(np.prod(arg_shape))
+        x = (2 * rng.standard_normal((4, N))).astype(dt)
+        with pxrt.Precision(width):
+            l1 = pxo.L1Norm(dim=N)
+            l21 = pxo.L21Norm(arg_shape=arg_shape, l2_axis=(0,))
+            sl2 = pxo.SquaredL2Norm(dim=N)
+            po = pxo.PositiveOrthant(dim=N)
+            lam = 0.7
+            out = dict(
+                x=x,
+                l1_apply=l1.apply(x), l1_prox=l1.prox(x, 0.8), l1_fprox=(lam * l1).fenchel_prox(x, 1.3),
+                l21_apply=l21.apply(x), l21_prox=l21.prox(x, 0.8), l21_fprox=(lam * l21).fenchel_prox(x, 1.3),
+                l21_moreau_grad=l21.moreau_envelope(0.3).grad(x),
+                l21_moreau_apply=l21.moreau_envelope(0.3).apply(x),
+                sl2_apply=sl2.apply(x), sl2_grad=sl2.grad(x), sl2_prox=sl2.prox(x, 0.8),
+                po_prox=po.prox(x, 0.8),
+                arg_shape=np.array(arg_shape), lam=lam,
+            )
+        save(f"norms_{w}", **out)
+
+
+def gen_dense():
+    rng = np.random.default_rng(4)
+    for w, width in WIDTHS.items():
+        dt = width.value
+        A = rng.standard_normal((64, 256)).astype(dt)
+        x = rng.standard_normal((3, 256)).astype(dt)
+        z = rng.standard_normal((3, 64)).astype(dt)
+        with pxrt.Precision(width):
+            op = pxa.LinOp.from_array(A)
+            y, a = op.apply(x), op.adjoint(z)
+        save(f"dense_{w}", A=A, x=x, y=y, z=z, adj=a)
+
+
+# ----------------------------------------------------------------------------- trajectory goldens
+def _deblur_problem(width, arg_shape, sigma, rng, noise=0.01):
+    dt = width.value
+    x_gt = phantom(arg_shape, rng)
+    with pxrt.Precision(width):
+        H = pxo.Gaussian(arg_shape=arg_shape, sigma=sigma, truncate=3.0)
+        y = H.apply(x_gt.reshape(-1).astype(dt))
+    y = (y + noise * rng.standard_normal(y.shape)).astype(dt)
+    return H, y
+
+
+def gen_pgd():
+    for w, width in WIDTHS.items():
+        dt = width.value
+        rng = np.random.default_rng(10)
+        sh = (32, 36)
+        N = int(np.prod(sh))
+        H, y = _deblur_problem(width, sh, 2.0, rng)
+        for variant in ("l1", "tv", "tv_l1g"):
+            x0 = np.zeros(N, dtype=dt)
+            lam, mu = 0.01, 0.01
+            with pxrt.Precision(width):
+                f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H
+                if variant == "l1":
+                    g = lam * pxo.L1Norm(dim=N)
+                    L = 1.0
+                else:
+                    G = pxo.Gradient(arg_shape=sh)
+                    tv = lam * pxo.L21Norm(arg_shape=(2, *sh)).moreau_envelope(mu) * G
+                    f = f + tv
+                    g = pxo.PositiveOrthant(dim=N) if variant == "tv" else lam * pxo.L1Norm(dim=N)
+                    L = 1.0 + lam / mu * 8.0
+                f.diff_lipschitz = L
+                res = {}
+                for n_it in (1, 10, 100):
+                    slvr = pxsl.PGD(f=f, g=g, show_progress=False)
+                    slvr.fit(x0=x0, stop_crit=pxst.MaxIter(n_it) | pxst.RelError(eps=1e-30))
+                    res[f"x_{n_it}"] = slvr.solution()
+                    res[f"hist_{n_it}"] = slvr.stats()[1]["RelError[x]"]
+            save(f"pgd_{variant}_{w}", arg_shape=np.array(sh), y=y, x0=x0, lam=lam, mu=mu, sigma=2.0, diff_lipschitz=L,
+                 **res)
+    # stacked x0 (2, N), one y (vectorisation over stacking dims)
+    width = WIDTHS["f32"]
+    dt = width.value
+    rng = np.random.default_rng(11)
+    sh = (24, 20)
+    N = int(np.prod(sh))
+    H, y = _deblur_problem(width, sh, 1.0, rng)
+    x0 = rng.uniform(0, 1, (2, N)).astype(dt)
+    with pxrt.Precision(width):
+        f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H
+        f.diff_lipschitz = 1.0
+        g = 0.02 * pxo.L1Norm(dim=N)
+        slvr = pxsl.PGD(f=f, g=g, show_progress=False)
+        slvr.fit(x0=x0, stop_crit=pxst.MaxIter(20))
+        xs = slvr.solution()
+    save("pgd_stacked_f32", arg_shape=np.array(sh), y=y, x0=x0, lam=0.02, sigma=1.0, x_20=xs)
+
+
+def gen_pds():
+    for w, width in WIDTHS.items():
+        dt = width.value
+        for dims, tv in (((24, 28), "iso"), ((10, 11, 12), "aniso")):
+            rng = np.random.default_rng(20 + len(dims))
+            N = int(np.prod(dims))
+            D = len(dims)
+            H, y = _deblur_problem(width, dims, 2.0, rng)
+            lam = 0.02
+            x0 = np.zeros(N, dtype=dt)
+            with pxrt.Precision(width):
+                f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H
+                f.diff_lipschitz = 1.0
+                K = pxo.Gradient(arg_shape=dims)
+                h = lam * (pxo.L21Norm(arg_shape=(D, *dims)) if tv == "iso" else pxo.L1Norm(dim=D * N))
+                res = {}
+                for name, klass in (("pd3o", pxsl.PD3O), ("cv", pxsl.CondatVu)):
+                    for n_it in (1, 10, 100):
+                        slvr = klass(f=f, g=None, h=h, K=K, show_progress=False)
+                        slvr.fit(x0=x0, stop_crit=pxst.MaxIter(n_it))
+                        data, hist = slvr.stats()
+                        res[f"{name}_x_{n_it}"] = data["x"]
+                        res[f"{name}_z_{n_it}"] = data["z"]
+                    res[f"{name}_tau"] = slvr._mstate["tau"]
+                    res[f"{name}_sigma"] = slvr._mstate["sigma"]
+                    res[f"{name}_rho"] = slvr._mstate["rho"]
+                res["K_lipschitz"] = float(K.lipschitz)
+            save(f"pds_{tv}{D}d_{w}", arg_shape=np.array(dims), y=y, x0=x0, lam=lam, sigma=2.0, diff_lipschitz=1.0, **res)
+
+
+def gen_admm():
+    for w, width in WIDTHS.items():
+        dt = width.value
+        rng = np.random.default_rng(30)
+        M, N = 48, 160
+        A = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(dt)
+        xs = np.zeros(N)
+        xs[rng.choice(N, 8, replace=False)] = rng.standard_normal(8)
+        y = (A @ xs + 0.01 * rng.standard_normal(M)).astype(dt)
+        lam = 0.05
+        x0 = np.zeros(N, dtype=dt)
+        with pxrt.Precision(width):
+            K = pxa.LinOp.from_array(A)
+            f = 0.5 * pxo.SquaredL2Norm(dim=M).asloss(y) * K
+            h = lam * pxo.L1Norm(dim=N)
+            res = {}
+            for n_it in (1, 5, 30):
+                slvr = pxsl.ADMM(f=f, h=h, show_progress=False)
+                slvr.fit(x0=x0, tau=1.0, stop_crit=pxst.MaxIter(n_it))
+                data, _ = slvr.stats()
+                res[f"x_{n_it}"] = data["x"]
+                res[f"u_{n_it}"] = data["u"]
+                res[f"z_{n_it}"] = data["z"]
+        save(f"admm_{w}", A=A, y=y, x0=x0, lam=lam, tau=1.0, **res)
+
+
+if __name__ == "__main__":
+    gen_stencil()
+    gen_convolve_gaussian()
+    gen_gradient()
+    gen_norms()
+    gen_dense()
+    gen_pgd()
+    gen_pds()
+    gen_admm()
