@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""
+Benchmark: PGD solver iterations/s on TV-regularised deblurring (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 2048 x 2048 image, H = Gaussian(sigma=2) blur (13 taps/axis,
+zero boundary), f = 1/2||H x - y||^2 + lam * env_mu(L21) o Gradient, g = PositiveOrthant,
+lam = mu = 0.01, fp32, synthetic piecewise-constant phantom + 1% noise.
+One "step" = one PGD iteration (Solver._step: stop check every `stop_rate` iterations + m_step)
+driven through the pyxu_amd Solver API in MANUAL mode.
+
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): every rank solves its own image
+(independent problems shard with no data-path collective) -> weak scaling; value = total
+image-iterations/s over all ranks = ranks * K / max_rank(elapsed).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+
+
+def phantom(shape, rng):
+    x = np.zeros(shape, dtype=np.float32)
+    for _ in range(12):
+        lo = [int(rng.integers(0, n // 2)) for n in shape]
+        hi = [l + int(rng.integers(n // 8 + 1, n // 2 + 1)) for l, n in zip(lo, shape)]
+        x[tuple(slice(l, h) for l, h in zip(lo, hi))] = rng.uniform(0.2, 1.0)
+    return x
+
+
+def build_problem(n0, n1, seed, lam=0.01, mu=0.01, sigma=2.0):
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd.util import to_device
+
+    sh = (n0, n1)
+    N = n0 * n1
+    rng = np.random.default_rng(seed)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        H = pxo.Gaussian(arg_shape=sh, sigma=sigma, truncate=3.0)
+        x_gt = to_device(phantom(sh, rng).reshape(-1))
+        y = H.apply(x_gt)
+        noise = to_device((0.01 * rng.standard_normal(N)).astype(np.float32))
+        from pyxu_amd import _dev
+
+        y = _dev.axpby(1.0, y, 1.0, noise)
+        G = pxo.Gradient(arg_shape=sh)
+        f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H + lam * pxo.L21Norm(arg_shape=(2, *sh)).moreau_envelope(mu) * G
+        f.diff_lipschitz = 1.0 + (lam / mu) * 8.0  # ||H||^2 + lam/mu ||Grad||^2, set analytically (§8(d))
+        g = pxo.PositiveOrthant(dim=N)
+    return f, g, y
+
+
+def cpu_baseline(n0, n1, seed, iters, lam=0.01, mu=0.01, sigma=2.0):
+    """Oracle (NumPy port of the reference path) on the host: same problem, `iters` PGD iterations."""
+    import oracle as orc
+
+    sh = (n0, n1)
+    N = n0 * n1
+    rng = np.random.default_rng(seed)
+    taps, c = orc.gaussian_taps(sigma, 3.0, np.float32)
+    blur = dict(arg_shape=sh, kernel=[taps, taps], center=[c, c])
+    x_gt = phantom(sh, rng).reshape(-1)
+    y = orc.stencil_apply(x_gt, sh, [taps, taps], [c, c])
+    y = (y + (0.01 * rng.standard_normal(N)).astype(np.float32)).astype(np.float32)
+    grad = lambda v: orc.deblur_tv_grad(v, blur, y, lam, mu, dict(arg_shape=sh))
+    prox = lambda z, t: orc.positive_orthant_prox(z)
+    tau = np.float32(1 / np.float32(1.0 + (lam / mu) * 8.0))
+    x0 = np.zeros(N, dtype=np.float32)
+    orc.pgd(x0, grad, prox, tau, 1)  # warm-up (page-in, allocator)
+    t0 = time.perf_counter()
+    orc.pgd(x0, grad, prox, tau, iters)
+    dt = time.perf_counter() - t0
+    return iters / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n", type=int, default=2048, help="image side (configs[1]: 2048)")
+    ap.add_argument("--stop-rate", type=int, default=50, help="stop-criterion evaluation rate (reference default 1)")
+    ap.add_argument("--cpu-iters", type=int, default=4, help="oracle iterations for the CPU baseline (0 = skip)")
+    ap.add_argument("--generic", action="store_true", help="disable the fused m_step (rule-by-rule HIP path)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import pyxu_amd
+    import pyxu_amd.abc as pxa
+    import pyxu_amd.opt.solver as pxs
+    import pyxu_amd.opt.stop as pxst
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd import _dev
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+    if not pyxu_amd.native_loaded():
+        raise RuntimeError("libpyxu_amd.so not loaded")
+
+    n0 = n1 = args.n
+    N = n0 * n1
+    f, g, y = build_problem(n0, n1, seed=1234 + rank)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        slvr = pxs.PGD(f=f, g=g, show_progress=False, stop_rate=args.stop_rate)
+        stop = pxst.MaxIter(10**9) | pxst.RelError(eps=1e-30)
+        slvr.fit(x0=_dev.zeros((N,), y), stop_crit=stop, mode=pxa.Mode.MANUAL, fused=not args.generic)
+        fused = slvr._plan is not None
+        gen = slvr.steps()
+        for _ in range(args.warmup):
+            next(gen)
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            next(gen)
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+
+        # ---- dominant-kernel duration: HIP events on the launch stream, kernel-only replay of the
+        # same fused step (same buffers, same parameters) back to back.
+        stream = torch.cuda.current_stream()
+        kern_ms = None
+        alg_bytes = None
+        if fused:
+            p = slvr._plan
+            x, xp = slvr._mstate["x"], slvr._mstate["x_prev"]
+            out = _dev.empty_like(x)
+            reps = 50
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            tau = slvr._mstate["tau"]
+            for _ in range(5):
+                _dev.pgd_tv2d_step(x, xp, p["y"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
+                                   p["h0"], p["h1"], p["lam"], p["mu"], 0.9, tau, p["prox"], 0.0)
+            ev0.record(stream)
+            for _ in range(reps):
+                _dev.pgd_tv2d_step(x, xp, p["y"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
+                                   p["h0"], p["h1"], p["lam"], p["mu"], 0.9, tau, p["prox"], 0.0)
+            ev1.record(stream)
+            ev1.synchronize()
+            kern_ms = ev0.elapsed_time(ev1) / reps
+            alg_bytes = 4 * 4 * N * p["stack"]  # x, x_prev, y read + x_new write, fp32, once each
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    if rank == 0:
+        value = world * args.steps / elapsed_max
+        roof = None
+        if kern_ms is not None:
+            achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "pgd_tv2d_kernel",
+                    "kernel_ms": round(kern_ms, 5), "bytes_per_launch": alg_bytes}
+        cpu = None
+        if args.cpu_iters > 0 and world == 1:
+            v, dt = cpu_baseline(n0, n1, seed=1234, iters=args.cpu_iters)
+            cpu = {"value": round(v, 4), "unit": "iterations/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle NumPy PGD, same {n0}x{n1} TV-deblur problem, {args.cpu_iters} iterations in {dt:.1f} s"}
+        line = {
+            "metric": "solver iterations/s (PGD, TV-regularised deblur)",
+            "value": round(value, 2),
+            "unit": "image-iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed_max / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (piecewise-constant phantom, Gaussian blur, 1% noise)",
+            "config": {"workload": f"PGD {n0}x{n1} Gaussian(sigma=2) deblur + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
+                       "image": [n0, n1], "images_per_gpu": 1, "stop_rate": args.stop_rate,
+                       "stop_crit": "MaxIter | RelError", "fused_m_step": fused, "parallelism": f"independent-images x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,245 @@
+/*
+ * pyxu_amd — C-ABI of the MI355X (gfx950) proximal-splitting backend.
+ *
+ * This is the drop-in boundary for Pyxu's proximal-splitting hot path.
+ * Every entry point is a plain `extern "C"` function over raw device pointers and sizes:
+ *   - returns 0 on success, a HIP error code (>0) or a PXA_ERR_* code (<0) on failure
+ *     (pxa_error_string() gives a message); no exception crosses the ABI;
+ *   - the caller owns every buffer (device pointers, e.g. torch-ROCm `data_ptr()`), the library never
+ *     allocates persistent device memory; scratch space is passed in explicitly;
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); launches are asynchronous;
+ *   - functions are stateless and re-entrant (safe from Pyxu's solver worker thread,
+ *     reference src/pyxu/abc/solver.py:710-718) and graph-capturable (no alloc/sync inside);
+ *   - arrays are C-contiguous, laid out exactly as the reference's NDArrays: a leading stack of
+ *     independent problems followed by the row-major flattening of `arg_shape`
+ *     (reference src/pyxu/operator/linop/stencil/stencil.py:441-461).
+ *
+ * dtype codes: PXA_F32 (float) and PXA_F64 (double), mirroring pyxu.runtime.Width
+ * (reference src/pyxu/runtime/_runtime.py:25-45).
+ *
+ * Reference interfaces replaced are cited per function (paths under /root/reference/src/pyxu).
+ */
+#ifndef PYXU_AMD_H
+#define PYXU_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PXA_F32 0
+#define PXA_F64 1
+
+#define PXA_OK 0
+#define PXA_ERR_ARG (-1)         /* invalid argument (shape, count, null pointer, ...) */
+#define PXA_ERR_DTYPE (-2)       /* unsupported dtype code */
+#define PXA_ERR_UNSUPPORTED (-3) /* valid request outside this build's supported envelope */
+
+#define PXA_MAX_DIM 4    /* spatial rank supported by stencil / gradient kernels */
+#define PXA_MAX_TAPS 64  /* taps per separable-axis pass (kernel-argument resident) */
+
+/* Boundary modes of Pad (operator/linop/pad.py:145-160). */
+#define PXA_MODE_CONSTANT 0
+#define PXA_MODE_WRAP 1
+#define PXA_MODE_REFLECT 2
+#define PXA_MODE_SYMMETRIC 3
+#define PXA_MODE_EDGE 4
+
+/* Row reductions (pxa_row_reduce). */
+#define PXA_RED_SUMSQ 0  /* sum x^2            : SquaredL2Norm.apply, norm(ord=2)^2   (norm.py:91-94) */
+#define PXA_RED_DIFFSQ 1 /* sum (x-y)^2        : RelError numerator (opt/stop.py:365-371) */
+#define PXA_RED_DOT 2    /* sum x*y            : CG alpha denominator (opt/solver/cg.py:130) */
+#define PXA_RED_ABS 3    /* sum |x|            : L1Norm.apply (norm.py:42-45) */
+#define PXA_RED_MAXABS 4 /* max |x|            : LInfinityNorm / norm(ord=inf) */
+#define PXA_RED_SUM 5    /* sum x              : Sum / QuadraticFunc.apply (operator.py:1255-1262) */
+#define PXA_RED_NEGCNT 6 /* count(x < 0)       : PositiveOrthant.apply (func/indicator.py:198-202) */
+
+/* ---------------------------------------------------------------------------------------------
+ * Library information
+ * ------------------------------------------------------------------------------------------- */
+const char* pxa_version(void);
+const char* pxa_error_string(int code);
+/* Number of exported compute entry points (for the loader's self-check). */
+int pxa_abi_version(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Element-wise kernels: the arithmetic glue of the operator algebra
+ * (abc/arithmetic.py ScaleRule :167-218, ArgShiftRule :580-652, AddRule :843-943) and the solver
+ * updates (opt/solver/pgd.py:173-191, opt/solver/pds.py:429-442, :747-761, :1631-1638).
+ * `out` may alias any input.
+ * ------------------------------------------------------------------------------------------- */
+
+/* out = a*x + b*y      (y may be NULL: out = a*x). */
+int pxa_axpby(int dtype, int64_t n, double a, const void* x, double b, const void* y, void* out, void* stream);
+
+/* out[i] = a*x[i] + b*y[i % ny]: y broadcast over the leading stack dims (ArgShiftRule.apply/prox/grad,
+ * arithmetic.py:580-652; AddRule range broadcasting :843-849). */
+int pxa_axpby_bcast(int dtype, int64_t n, double a, const void* x, double b, const void* y, int64_t ny, void* out,
+                    void* stream);
+
+/* out = a*x + b*y + c*z. */
+int pxa_lincomb3(int dtype, int64_t n, double a, const void* x, double b, const void* y, double c, const void* z,
+                 void* out, void* stream);
+
+ /* out = (x - y) * a + x   (PGD momentum step y_k, opt/solver/pgd.py:179-181). */
+int pxa_extrapolate(int dtype, int64_t n, double a, const void* x, const void* y, void* out, void* stream);
+
+/* out = x / d          (SquaredL2Norm.prox: y /= 2*tau+1, norm.py:100-104; moreau grad x /= mu). */
+int pxa_div(int dtype, int64_t n, const void* x, double d, void* out, void* stream);
+
+/* out = x + s           with s a broadcast scalar (ArgShiftRule with scalar shift, arithmetic.py:580-584). */
+int pxa_add_scalar(int dtype, int64_t n, const void* x, double s, void* out, void* stream);
+
+/* out[i] = v. */
+int pxa_fill(int dtype, int64_t n, double v, void* out, void* stream);
+
+/* out = x * y (element-wise product; QuadraticFunc.apply, operator.py:1255). */
+int pxa_mul(int dtype, int64_t n, const void* x, const void* y, void* out, void* stream);
+
+/* out = clip(x, lo, hi); has_hi=0 means no upper bound.  PositiveOrthant.prox (func/indicator.py:204-206). */
+int pxa_clip(int dtype, int64_t n, const void* x, double lo, double hi, int has_hi, void* out, void* stream);
+
+/* L1Norm.prox (operator/func/norm.py:47-52): out = fmax(0, |x| - tau) * sign(x). */
+int pxa_prox_l1(int dtype, int64_t n, const void* x, double tau, void* out, void* stream);
+
+/* L21Norm.prox (norm.py:352-364) with x viewed as (outer, group, inner) and the l2 norm taken over
+ * `group` at each (outer, inner):  out = x * (1 - tau / fmax(||x||_2, tau)). */
+int pxa_prox_l21(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, double tau, void* out,
+                 void* stream);
+
+/* ProxFunc.fenchel_prox of lam*L1Norm (operator.py:905-944 Moreau form, arithmetic.py:182-183):
+ *   out = x - sigma * prox_{lam*|.|_1 / sigma}(x / sigma). */
+int pxa_fenchel_prox_l1(int dtype, int64_t n, const void* x, double sigma, double lam, void* out, void* stream);
+
+/* ProxFunc.fenchel_prox of lam*L21Norm, same (outer, group, inner) view as pxa_prox_l21. */
+int pxa_fenchel_prox_l21(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, double sigma,
+                         double lam, void* out, void* stream);
+
+/* Gradient of scale * moreau_envelope(mu) of L1 / L21 (operator.py:1053-1058, arithmetic.py:209-213):
+ *   out = scale * (x - prox_{mu f}(x)) / mu. */
+int pxa_moreau_grad_l1(int dtype, int64_t n, const void* x, double mu, double scale, void* out, void* stream);
+int pxa_moreau_grad_l21(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, double mu,
+                        double scale, void* out, void* stream);
+
+/* Per-(outer, inner) l2 norm over `group` (L21Norm.apply inner part, norm.py:338-350), written to
+ * `out` (outer*inner elements, dtype). */
+int pxa_group_norm(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, void* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Row reductions (opt/stop.py RelError/AbsError :353-382, :250-266; math/linalg.py norm :14-22;
+ * opt/solver/cg.py:125-153).  x (and y) are (rows, n); out is a DEVICE array of `rows` doubles.
+ * Accumulation is in double, in a fixed order (deterministic run to run).
+ * `work` must hold pxa_row_reduce_workspace_bytes(rows, n) bytes of device memory.
+ * ------------------------------------------------------------------------------------------- */
+size_t pxa_row_reduce_workspace_bytes(int64_t rows, int64_t n);
+int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, const void* y, double* out, void* work,
+                   void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Stencils (operator/linop/stencil/stencil.py:356-627, _stencil.py:232-476; pad.py; select.py).
+ *
+ * All stencil entry points act on `stack` independent arrays of spatial shape `shape[0..ndim)`;
+ * array s starts at x + s*x_stack_stride (elements) and y + s*y_stack_stride.
+ * Output: y = corr(x) + beta*y  (beta = 0 overwrites; beta = 1 accumulates, as vstack adjoints do,
+ * blocks.py:838-860).
+ * Taps are given in the reference's code-generation order (itertools.product over the kernel,
+ * _stencil.py:284-305) after its constant folding: taps with isclose(k, 0) removed, taps with
+ * isclose(k, 1) replaced by exactly 1.
+ *
+ * zero_partial = 0 : zero-padding semantics, out[i] = sum_q k_q x[i + off_q] with x = 0 outside;
+ *                    this is Trim o S o Pad for mode="constant" (stencil.py:441-450) in one pass.
+ * zero_partial = 1 : numba @stencil semantics on an already-padded array: out[i] = 0 wherever one
+ *                    offset leaves the array (_stencil.py:238-244, :337-383).
+ * ------------------------------------------------------------------------------------------- */
+
+/* One separable-axis pass: taps along `axis` only; offsets[q] = q - center (relative index). */
+int pxa_stencil_axis(int dtype, int64_t stack, int ndim, const int64_t* shape, int axis, int ntaps,
+                     const int32_t* offsets, const double* coefs, int zero_partial, const void* x,
+                     int64_t x_stack_stride, void* y, int64_t y_stack_stride, double beta, void* stream);
+
+/* Fused separable filter over every axis with a non-trivial kernel (axis order 0..ndim-1, as
+ * Stencil._stencil_chain applies them).  Per axis a: ntaps[a] taps at offsets/coefs
+ * [a*PXA_MAX_TAPS ..).  ntaps[a] == 0 marks an identity axis.  Constant mode (zero_partial=0) only.
+ * `work` must hold pxa_stencil_sep_workspace_bytes(...) bytes (intermediate field) or be NULL when
+ * at most one axis is non-trivial. */
+size_t pxa_stencil_sep_workspace_bytes(int dtype, int64_t stack, int ndim, const int64_t* shape,
+                                       const int* ntaps);
+int pxa_stencil_sep(int dtype, int64_t stack, int ndim, const int64_t* shape, const int* ntaps,
+                    const int32_t* offsets, const double* coefs, const void* x, int64_t x_stack_stride, void* y,
+                    int64_t y_stack_stride, double beta, void* work, void* stream);
+
+/* Non-separable N-D stencil.  Taps live in DEVICE memory: offsets_dev (ntaps x ndim int32, relative
+ * offsets) and coefs_dev (ntaps, dtype). */
+int pxa_stencil_nd(int dtype, int64_t stack, int ndim, const int64_t* shape, int ntaps, const int32_t* offsets_dev,
+                   const void* coefs_dev, int zero_partial, const void* x, int64_t x_stack_stride, void* y,
+                   int64_t y_stack_stride, double beta, void* stream);
+
+/* Pad.apply (pad.py:235-306): y (stack, shape + lo + hi) from x (stack, shape); modes per axis. */
+int pxa_pad(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* pad_lo, const int64_t* pad_hi,
+            const int* modes, const void* x, void* y, void* stream);
+
+/* Pad.adjoint (pad.py:307-372): y (stack, shape) from x (stack, padded shape).  `work` holds one
+ * padded-size scratch field (stack * prod(shape + lo + hi) elements). */
+int pxa_pad_adjoint(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* pad_lo,
+                    const int64_t* pad_hi, const int* modes, const void* x, void* y, void* work, void* stream);
+
+/* Trim.apply / SubSample (select.py:120-142, :205-251) when embed=0: y = x[lo : n - hi] per axis.
+ * Trim.adjoint (select.py:144-167) when embed=1: y (padded) = 0 except the core, which receives x. */
+int pxa_trim(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* lo, const int64_t* hi,
+             int embed, const void* x, void* y, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Gradient (operator/linop/diff.py Gradient :1113-1265 = vstack of 2-tap finite-difference
+ * Stencils, blocks.py:660-679, :838-860) in ONE pass over x (apply) or z (adjoint),
+ * constant (zero) boundary.  Direction d (0 <= d < ndir) differentiates spatial axis dirs[d] with
+ * taps (off0[d], coef0[d]) and (off1[d], coef1[d]) in code-generation order.
+ * apply  : g (stack, ndir, N) direction-major, g[s,d,i] = c0 x[i+o0 e] + c1 x[i+o1 e]
+ * adjoint: x (stack, N), x[s,i] = sum_d ( c1' z_d[i-o1 e] + c0' z_d[i-o0 e] )   (flipped order)
+ * ------------------------------------------------------------------------------------------- */
+int pxa_gradient2(int dtype, int64_t stack, int ndim, const int64_t* shape, int ndir, const int* dirs,
+                  const int* off0, const double* coef0, const int* off1, const double* coef1, const void* x, void* g,
+                  void* stream);
+int pxa_gradient2_adjoint(int dtype, int64_t stack, int ndim, const int64_t* shape, int ndir, const int* dirs,
+                          const int* off0, const double* coef0, const int* off1, const double* coef1, const void* z,
+                          void* x, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Dense LinOp (operator/linop/base.py _ExplicitLinOp._matmat :407-419, apply/adjoint :421-427):
+ *   trans = 0 : Y (B x M) = X (B x N) A^T      (A.dot(x) per stacked row)
+ *   trans = 1 : Y (B x N) = X (B x M) A        (A^T.dot(z) per stacked row)
+ * A is (M x N) row-major.  `work` must hold pxa_dense_workspace_bytes(...) bytes.
+ * ------------------------------------------------------------------------------------------- */
+size_t pxa_dense_workspace_bytes(int dtype, int trans, int64_t M, int64_t N, int64_t B);
+int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, const void* A, const void* X, void* Y,
+                     void* work, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused solver steps (the whole m_step of a recognised problem in one launch).
+ *
+ * PGD on  F(x) = 1/2||H x - y||^2 + lam * env_mu(L21 o Grad)(x),  G = PositiveOrthant | l1w*L1 | 0
+ * (opt/solver/pgd.py:173-191 with the arithmetic of AddRule/ChainRule/ScaleRule/ArgShiftRule):
+ *   yk   = x + a (x - x_prev)
+ *   grad = H^T (H yk - y) + Grad^T( lam * (v - prox_{mu L21}(v)) / mu ),  v = Grad yk
+ *   x_new = prox_{tau G}( yk - tau * grad )
+ * H is a separable zero-boundary (mode="constant") correlation over 2 spatial axes (taps0 on axis
+ * 0, taps1 on axis 1, offsets/coefs in code-generation order); Grad the forward-difference
+ * Gradient (diff.py default scheme) with spacing h0, h1.  `stack` independent images, each
+ * (n0, n1), contiguous; image s uses data image (s % y_images) of y (1 = one y shared by a stack of
+ * initial points, stack = batch-as-axis images with their own data).  x_new must not alias x or x_prev.  If `partials` is not NULL, each
+ * workgroup writes (sum (x_new-x)^2, sum x^2) for RelError into partials[2*blk..] (double) —
+ * pxa_pgd_tv2d_partials_count() gives the number of workgroups.
+ * prox codes: 0 none, 1 positive orthant, 2 l1 with weight prox_w.
+ * ------------------------------------------------------------------------------------------- */
+int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
+int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
+                      const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
+                      double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
+                      const void* x_prev, const void* y, void* x_new, double* partials, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PYXU_AMD_H */

@@ -1,0 +1,370 @@
+"""
+Device-array kernels: thin Python entry points over the C-ABI (``include/pyxu_amd.h``).
+
+Every function takes/returns torch-ROCm tensors resident on the current device, launches on
+``torch.cuda.current_stream()`` and raises on any non-zero status.  Host arrays are rejected with
+a TypeError: this package has no CPU compute path.
+"""
+import ctypes as ct
+
+import numpy as np
+
+from pyxu_amd._lib import check, f64_array, i32_array, i64_array, int_array, lib
+
+__all__ = []  # internal module
+
+RED_SUMSQ, RED_DIFFSQ, RED_DOT, RED_ABS, RED_MAXABS, RED_SUM, RED_NEGCNT = range(7)
+MODES = {"constant": 0, "wrap": 1, "reflect": 2, "symmetric": 3, "edge": 4}
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def dtcode(t) -> int:
+    torch = _torch()
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.float64:
+        return 1
+    raise TypeError(f"pyxu_amd: unsupported dtype {t.dtype} (float32/float64 only).")
+
+
+def require(t, name="arr"):
+    """Validate a device operand: CUDA (ROCm) tensor, float32/64, contiguous."""
+    if not (type(t).__module__.startswith("torch") and hasattr(t, "is_cuda")):
+        raise TypeError(
+            f"pyxu_amd: `{name}` must be an MI355X device tensor (got {type(t).__name__}); "
+            "move host data with pyxu_amd.util.to_device()."
+        )
+    if not t.is_cuda:
+        raise TypeError(f"pyxu_amd: `{name}` lives on {t.device}; pyxu_amd computes on the MI355X only.")
+    dtcode(t)
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def ptr(t) -> int:
+    return t.data_ptr()
+
+
+def stream():
+    return ct.c_void_p(_torch().cuda.current_stream().cuda_stream)
+
+
+def empty(shape, like):
+    return _torch().empty(shape, dtype=like.dtype, device=like.device)
+
+
+def empty_like(t):
+    return _torch().empty_like(t, memory_format=_torch().contiguous_format)
+
+
+def copy(x):
+    x = require(x)
+    return x.clone(memory_format=_torch().contiguous_format)
+
+
+def scalar_dt(x):
+    return np.float32 if dtcode(x) == 0 else np.float64
+
+
+# ------------------------------------------------------------------ element-wise
+def axpby(a, x, b=0.0, y=None, out=None):
+    """out = a*x + b*y."""
+    x = require(x, "x")
+    if y is not None:
+        y = require(y, "y")
+        assert y.numel() == x.numel() and y.dtype == x.dtype
+    out = empty_like(x) if out is None else out
+    check(
+        lib.pxa_axpby(dtcode(x), x.numel(), float(a), ptr(x), float(b), ptr(y) if y is not None else None, ptr(out), stream()),
+        "pxa_axpby",
+    )
+    return out
+
+
+def axpby_bcast(a, x, b, y, out=None):
+    """out = a*x + b*y with y (M,) broadcast over x's leading dims (x: (..., M))."""
+    x, y = require(x, "x"), require(y, "y")
+    if y.numel() == x.numel():
+        return axpby(a, x, b, y, out=out)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_axpby_bcast(dtcode(x), x.numel(), float(a), ptr(x), float(b), ptr(y), y.numel(), ptr(out), stream()), "pxa_axpby_bcast")
+    return out
+
+
+def lincomb3(a, x, b, y, c, z, out=None):
+    x, y, z = require(x), require(y), require(z)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_lincomb3(dtcode(x), x.numel(), float(a), ptr(x), float(b), ptr(y), float(c), ptr(z), ptr(out), stream()), "pxa_lincomb3")
+    return out
+
+
+def extrapolate(a, x, y, out=None):
+    """(x - y) * a + x."""
+    x, y = require(x), require(y)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_extrapolate(dtcode(x), x.numel(), float(a), ptr(x), ptr(y), ptr(out), stream()), "pxa_extrapolate")
+    return out
+
+
+def div(x, d, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_div(dtcode(x), x.numel(), ptr(x), float(d), ptr(out), stream()), "pxa_div")
+    return out
+
+
+def add_scalar(x, s, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_add_scalar(dtcode(x), x.numel(), ptr(x), float(s), ptr(out), stream()), "pxa_add_scalar")
+    return out
+
+
+def fill(out, v):
+    out = require(out)
+    check(lib.pxa_fill(dtcode(out), out.numel(), float(v), ptr(out), stream()), "pxa_fill")
+    return out
+
+
+def zeros(shape, like):
+    return fill(empty(shape, like), 0.0)
+
+
+def mul(x, y, out=None):
+    x, y = require(x), require(y)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_mul(dtcode(x), x.numel(), ptr(x), ptr(y), ptr(out), stream()), "pxa_mul")
+    return out
+
+
+def clip(x, lo, hi=None, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_clip(dtcode(x), x.numel(), ptr(x), float(lo), float(hi or 0.0), int(hi is not None), ptr(out), stream()), "pxa_clip")
+    return out
+
+
+def prox_l1(x, tau, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_prox_l1(dtcode(x), x.numel(), ptr(x), float(tau), ptr(out), stream()), "pxa_prox_l1")
+    return out
+
+
+def fenchel_prox_l1(x, sigma, lam, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_fenchel_prox_l1(dtcode(x), x.numel(), ptr(x), float(sigma), float(lam), ptr(out), stream()), "pxa_fenchel_prox_l1")
+    return out
+
+
+def moreau_grad_l1(x, mu, scale, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_moreau_grad_l1(dtcode(x), x.numel(), ptr(x), float(mu), float(scale), ptr(out), stream()), "pxa_moreau_grad_l1")
+    return out
+
+
+def prox_l21(x, tau, outer, group, inner, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_prox_l21(dtcode(x), outer, group, inner, ptr(x), float(tau), ptr(out), stream()), "pxa_prox_l21")
+    return out
+
+
+def fenchel_prox_l21(x, sigma, lam, outer, group, inner, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(
+        lib.pxa_fenchel_prox_l21(dtcode(x), outer, group, inner, ptr(x), float(sigma), float(lam), ptr(out), stream()),
+        "pxa_fenchel_prox_l21",
+    )
+    return out
+
+
+def moreau_grad_l21(x, mu, scale, outer, group, inner, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(
+        lib.pxa_moreau_grad_l21(dtcode(x), outer, group, inner, ptr(x), float(mu), float(scale), ptr(out), stream()),
+        "pxa_moreau_grad_l21",
+    )
+    return out
+
+
+def group_norm(x, outer, group, inner):
+    x = require(x)
+    out = empty((outer * inner,), x)
+    check(lib.pxa_group_norm(dtcode(x), outer, group, inner, ptr(x), ptr(out), stream()), "pxa_group_norm")
+    return out
+
+
+# ------------------------------------------------------------------ reductions
+def row_reduce(op, x, y=None):
+    """Per-row reduction over the last axis -> float64 device tensor of shape x.shape[:-1] (or (1,))."""
+    torch = _torch()
+    x = require(x)
+    n = x.shape[-1] if x.ndim > 0 else 1
+    rows = x.numel() // max(n, 1) if x.numel() else 0
+    if y is not None:
+        y = require(y)
+        assert y.shape == x.shape
+    out = torch.empty((max(rows, 1),), dtype=torch.float64, device=x.device)
+    if rows == 0:
+        return out.zero_()
+    # rows beyond the grid-y limit are processed in slabs
+    step = 65535
+    for r0 in range(0, rows, step):
+        r1 = min(rows, r0 + step)
+        es = x.element_size()
+        wsz = int(lib.pxa_row_reduce_workspace_bytes(r1 - r0, n))
+        work = torch.empty((max(wsz // 8, 1),), dtype=torch.float64, device=x.device)
+        check(
+            lib.pxa_row_reduce(
+                dtcode(x), op, r1 - r0, n, ptr(x) + r0 * n * es, (ptr(y) + r0 * n * es) if y is not None else None,
+                out.data_ptr() + r0 * 8, ptr(work), stream(),
+            ),
+            "pxa_row_reduce",
+        )
+    return out.reshape(x.shape[:-1]) if x.ndim > 1 else out
+
+
+# ------------------------------------------------------------------ stencils
+def stencil_axis(x, y, stack, shape, axis, offsets, coefs, zero_partial=False, xs=None, ys=None, beta=0.0, x_off=0, y_off=0):
+    """One separable-axis pass (see pxa_stencil_axis).  `x_off`/`y_off`: element offsets into x/y."""
+    N = int(np.prod(shape))
+    es = x.element_size()
+    check(
+        lib.pxa_stencil_axis(
+            dtcode(x), stack, len(shape), i64_array(shape), axis, len(offsets), i32_array(offsets), f64_array(coefs),
+            int(zero_partial), ptr(x) + x_off * es, N if xs is None else xs, ptr(y) + y_off * es, N if ys is None else ys,
+            float(beta), stream(),
+        ),
+        "pxa_stencil_axis",
+    )
+    return y
+
+
+def stencil_sep(x, y, stack, shape, taps, beta=0.0, xs=None, ys=None, x_off=0, y_off=0):
+    """Separable constant-mode filter; taps[d] = (offsets, coefs) or None (identity axis)."""
+    torch = _torch()
+    D = len(shape)
+    MT = 64
+    ntaps = [0 if t is None else len(t[0]) for t in taps]
+    offs = [0] * (D * MT)
+    cfs = [0.0] * (D * MT)
+    for d, t in enumerate(taps):
+        if t is not None:
+            for q, (o, c) in enumerate(zip(*t)):
+                offs[d * MT + q] = o
+                cfs[d * MT + q] = c
+    N = int(np.prod(shape))
+    wsz = int(lib.pxa_stencil_sep_workspace_bytes(dtcode(x), stack, D, i64_array(shape), int_array(ntaps)))
+    work = torch.empty((max(wsz, 1),), dtype=torch.uint8, device=x.device) if wsz else None
+    es = x.element_size()
+    check(
+        lib.pxa_stencil_sep(
+            dtcode(x), stack, D, i64_array(shape), int_array(ntaps), i32_array(offs), f64_array(cfs),
+            ptr(x) + x_off * es, N if xs is None else xs, ptr(y) + y_off * es, N if ys is None else ys, float(beta),
+            ptr(work) if work is not None else None, stream(),
+        ),
+        "pxa_stencil_sep",
+    )
+    return y
+
+
+def stencil_nd(x, y, stack, shape, offsets_dev, coefs_dev, zero_partial=False, beta=0.0, xs=None, ys=None, x_off=0, y_off=0):
+    N = int(np.prod(shape))
+    ntaps = coefs_dev.numel()
+    es = x.element_size()
+    check(
+        lib.pxa_stencil_nd(
+            dtcode(x), stack, len(shape), i64_array(shape), ntaps, ptr(offsets_dev), ptr(coefs_dev), int(zero_partial),
+            ptr(x) + x_off * es, N if xs is None else xs, ptr(y) + y_off * es, N if ys is None else ys, float(beta), stream(),
+        ),
+        "pxa_stencil_nd",
+    )
+    return y
+
+
+def pad(x, stack, shape, lo, hi, modes):
+    pshape = [n + l + h for n, l, h in zip(shape, lo, hi)]
+    y = empty((stack * int(np.prod(pshape)),), x)
+    check(
+        lib.pxa_pad(dtcode(x), stack, len(shape), i64_array(shape), i64_array(lo), i64_array(hi),
+                    int_array([MODES[m] for m in modes]), ptr(x), ptr(y), stream()),
+        "pxa_pad",
+    )
+    return y
+
+
+def pad_adjoint(x, stack, shape, lo, hi, modes):
+    y = empty((stack * int(np.prod(shape)),), x)
+    work = empty((x.numel(),), x)
+    check(
+        lib.pxa_pad_adjoint(dtcode(x), stack, len(shape), i64_array(shape), i64_array(lo), i64_array(hi),
+                            int_array([MODES[m] for m in modes]), ptr(x), ptr(y), ptr(work), stream()),
+        "pxa_pad_adjoint",
+    )
+    return y
+
+
+def trim(x, stack, big_shape, lo, hi, embed):
+    core = [n - l - h for n, l, h in zip(big_shape, lo, hi)]
+    n_out = int(np.prod(big_shape if embed else core))
+    y = empty((stack * n_out,), x)
+    check(
+        lib.pxa_trim(dtcode(x), stack, len(big_shape), i64_array(big_shape), i64_array(lo), i64_array(hi), int(embed),
+                     ptr(x), ptr(y), stream()),
+        "pxa_trim",
+    )
+    return y
+
+
+# ------------------------------------------------------------------ gradient
+def gradient2(x, stack, shape, dirs, o0, c0, o1, c1, adjoint=False):
+    D = len(dirs)
+    N = int(np.prod(shape))
+    out = empty((stack * (N if adjoint else D * N),), x)
+    fn = lib.pxa_gradient2_adjoint if adjoint else lib.pxa_gradient2
+    check(
+        fn(dtcode(x), stack, len(shape), i64_array(shape), D, int_array(dirs), int_array(o0), f64_array(c0),
+           int_array(o1), f64_array(c1), ptr(x), ptr(out), stream()),
+        "pxa_gradient2",
+    )
+    return out
+
+
+# ------------------------------------------------------------------ dense
+def dense_matmat(A, X, trans):
+    """trans=0: Y = X A^T (X: (B, N)); trans=1: Y = X A (X: (B, M))."""
+    torch = _torch()
+    M, N = A.shape
+    B = X.shape[0]
+    Y = empty((B, N if trans else M), X)
+    wsz = int(lib.pxa_dense_workspace_bytes(dtcode(X), int(trans), M, N, B))
+    work = torch.empty((max(wsz, 1),), dtype=torch.uint8, device=X.device) if wsz else None
+    check(
+        lib.pxa_dense_matmat(dtcode(X), int(trans), M, N, B, ptr(A), ptr(X), ptr(Y), ptr(work) if work is not None else None, stream()),
+        "pxa_dense_matmat",
+    )
+    return Y
+
+
+# ------------------------------------------------------------------ fused solver steps
+def pgd_tv2d_step(x, x_prev, y, x_new, stack, y_images, n0, n1, taps0, taps1, h0, h1, lam, mu, a, tau, prox, prox_w, partials=None):
+    o0, k0 = taps0
+    o1, k1 = taps1
+    check(
+        lib.pxa_pgd_tv2d_step(
+            dtcode(x), stack, y_images, n0, n1, len(o0), i32_array(o0), f64_array(k0), len(o1), i32_array(o1), f64_array(k1),
+            float(h0), float(h1), float(lam), float(mu), float(a), float(tau), int(prox), float(prox_w),
+            ptr(x), ptr(x_prev), ptr(y), ptr(x_new), ptr(partials) if partials is not None else None, stream(),
+        ),
+        "pxa_pgd_tv2d_step",
+    )
+    return x_new

@@ -1,0 +1,316 @@
+"""
+Iterative-solver engine (mirrors reference ``pyxu.abc.solver``, src/pyxu/abc/solver.py:26-718).
+
+Same execution modes (BLOCK / ASYNC / MANUAL), stop/log/writeback rates, history records, worker
+thread, exception capture and ``data.npz`` checkpoint format.  The math state lives on the MI355X;
+device -> host copies happen only at stop-criterion evaluations and at writeback.
+"""
+import datetime as dt
+import enum
+import logging
+import operator
+import pathlib as plib
+import shutil
+import sys
+import tempfile
+import threading
+
+import numpy as np
+
+import pyxu_amd.runtime as pxrt
+from pyxu_amd.util import to_NUMPY
+
+__all__ = ["Mode", "Solver", "StoppingCriterion"]
+
+
+@enum.unique
+class Mode(enum.Enum):
+    BLOCK = enum.auto()
+    MANUAL = enum.auto()
+    ASYNC = enum.auto()
+
+
+class StoppingCriterion:
+    """State machine deciding when to stop (solver.py:37-94); compose with ``&`` / ``|``."""
+
+    def stop(self, state) -> bool:
+        raise NotImplementedError
+
+    def info(self) -> dict:
+        raise NotImplementedError
+
+    def clear(self):
+        pass
+
+    def __or__(self, other):
+        return _StoppingCriteriaComposition(lhs=self, rhs=other, op=operator.or_)
+
+    def __and__(self, other):
+        return _StoppingCriteriaComposition(lhs=self, rhs=other, op=operator.and_)
+
+
+class _StoppingCriteriaComposition(StoppingCriterion):
+    def __init__(self, lhs, rhs, op):
+        self._lhs, self._rhs, self._op = lhs, rhs, op
+
+    def stop(self, state) -> bool:
+        return self._op(self._lhs.stop(state), self._rhs.stop(state))
+
+    def info(self):
+        return {**self._lhs.info(), **self._rhs.info()}
+
+    def clear(self):
+        self._lhs.clear()
+        self._rhs.clear()
+
+
+class Solver:
+    """Base class of iterative solvers (solver.py:97-718)."""
+
+    def __init__(self, *, folder=None, exist_ok=False, stop_rate=1, writeback_rate=None, verbosity=None,
+                 show_progress=True, log_var=frozenset()):
+        self._mstate = dict()
+        self._astate = dict(history=None, idx=0, log_rate=None, log_var=None, logger=None, stdout=None, stop_crit=None,
+                            stop_rate=None, track_objective=None, wb_rate=None, workdir=None, mode=None, active=None,
+                            worker=None)
+        try:
+            if folder is None:
+                folder = plib.Path(tempfile.mkdtemp(prefix="pyxu_amd_"))
+            elif (folder := plib.Path(folder).expanduser().resolve()).exists() and (not exist_ok):
+                raise FileExistsError(f"{folder} already exists.")
+            else:
+                shutil.rmtree(folder, ignore_errors=True)
+                folder.mkdir(parents=True)
+            self._astate["workdir"] = folder
+        except FileExistsError:
+            raise
+        except Exception:
+            raise Exception(f"folder: expected path-like, got {type(folder)}.")
+        try:
+            assert stop_rate >= 1
+            self._astate["stop_rate"] = int(stop_rate)
+        except Exception:
+            raise ValueError(f"stop_rate must be positive, got {stop_rate}.")
+        try:
+            self._astate["wb_rate"] = writeback_rate
+            if writeback_rate is not None:
+                assert writeback_rate % self._astate["stop_rate"] == 0
+                self._astate["wb_rate"] = int(writeback_rate)
+        except Exception:
+            raise ValueError(f"writeback_rate must be a multiple of stop_rate({stop_rate}), got {writeback_rate}.")
+        try:
+            if verbosity is None:
+                verbosity = self._astate["stop_rate"]
+            assert verbosity % self._astate["stop_rate"] == 0
+            self._astate["log_rate"] = int(verbosity)
+            self._astate["stdout"] = bool(show_progress)
+        except Exception:
+            raise ValueError(f"verbosity must be a multiple of stop_rate({stop_rate}), got {verbosity}.")
+        if isinstance(log_var, str):
+            log_var = (log_var,)
+        self._astate["log_var"] = frozenset(log_var)
+
+    # ------------------------------------------------------------------ public API
+    def fit(self, **kwargs):
+        self._fit_init(
+            mode=kwargs.pop("mode", Mode.BLOCK),
+            stop_crit=kwargs.pop("stop_crit", None),
+            track_objective=kwargs.pop("track_objective", False),
+        )
+        self.m_init(**kwargs)
+        self._fit_run()
+
+    def m_init(self, **kwargs):
+        raise NotImplementedError
+
+    def m_step(self):
+        raise NotImplementedError
+
+    def steps(self, n=None):
+        self._check_mode(Mode.MANUAL)
+        i = 0
+        while (n is None) or (i < n):
+            if self._step():
+                data, _ = self.stats()
+                yield data
+                i += 1
+            else:
+                self._astate["mode"] = None
+                self._cleanup_logger()
+                return
+
+    def stats(self):
+        history = self._astate["history"]
+        if history is not None:
+            history = np.concatenate(history, dtype=history[0].dtype, axis=0) if len(history) > 0 else None
+        data = {k: self._mstate.get(k) for k in self._astate["log_var"]}
+        return data, history
+
+    @property
+    def workdir(self):
+        return self._astate["workdir"]
+
+    @property
+    def logfile(self):
+        return self.workdir / "solver.log"
+
+    @property
+    def datafile(self):
+        return self.workdir / "data.npz"
+
+    def busy(self) -> bool:
+        self._check_mode(Mode.ASYNC, Mode.BLOCK)
+        return self._astate["active"].is_set()
+
+    def solution(self):
+        raise NotImplementedError
+
+    def stop(self):
+        self._check_mode(Mode.ASYNC, Mode.BLOCK)
+        self._astate["active"].clear()
+        self._astate["worker"].join()
+        self._astate.update(mode=None, active=None, worker=None)
+        self._cleanup_logger()
+
+    def writeback(self):
+        """Checkpoint ``log_var`` + history to ``workdir/data.npz`` (solver.py:562-570)."""
+        data, history = self.stats()
+        kwargs = {k: to_NUMPY(v) for (k, v) in dict(history=history, **data).items() if (v is not None)}
+        np.savez(self.datafile, **kwargs)
+
+    def default_stop_crit(self):
+        raise NotImplementedError("No default stopping criterion defined.")
+
+    def objective_func(self):
+        raise NotImplementedError("No objective function defined.")
+
+    # ------------------------------------------------------------------ internals
+    def _fit_init(self, mode, stop_crit, track_objective):
+        def _init_logger():
+            logger = logging.getLogger(str(self.workdir))
+            logger.handlers.clear()
+            logger.setLevel("DEBUG")
+            fmt = logging.Formatter(fmt="{levelname} -- {message}", style="{")
+            handlers = [logging.FileHandler(self.logfile, mode="w")]
+            if (mode is Mode.BLOCK) and self._astate["stdout"]:
+                handlers.append(logging.StreamHandler(sys.stdout))
+            for h in handlers:
+                h.setLevel("DEBUG")
+                h.setFormatter(fmt)
+                logger.addHandler(h)
+            logger.propagate = False
+            return logger
+
+        self._mstate.clear()
+        if stop_crit is None:
+            stop_crit = self.default_stop_crit()
+        stop_crit.clear()
+        if track_objective:
+            from pyxu_amd.opt.stop import Memorize
+
+            stop_crit |= Memorize(var="objective_func")
+        self._astate.update(history=[], idx=0, logger=_init_logger(), stop_crit=stop_crit,
+                            track_objective=track_objective, mode=mode, active=None, worker=None)
+
+    def _fit_run(self):
+        mode = self._astate["mode"]
+        if mode is Mode.MANUAL:
+            return
+        self._astate.update(active=threading.Event(), worker=Solver._Worker(self))
+        self._astate["active"].set()
+        self._astate["worker"].start()
+        if mode is Mode.BLOCK:
+            self._astate["worker"].join()
+            self.stop()
+
+    def _check_mode(self, *modes):
+        m = self._astate["mode"]
+        if m not in modes:
+            if m is None:
+                raise ValueError("Illegal method call: invoke Solver.fit() first.")
+            raise ValueError("Illegal method call: can only be used if Solver.fit() invoked with mode=Any["
+                             + ", ".join(_.name for _ in modes) + "]")
+
+    def _step(self) -> bool:
+        ast = self._astate
+        idx = ast["idx"]
+        _ms = idx % ast["stop_rate"] == 0
+        _ml = idx % ast["log_rate"] == 0
+        _mw = (ast["wb_rate"] is not None) and (idx % ast["wb_rate"] == 0)
+
+        def _log(msg=None):
+            if msg is None:
+                h = ast["history"][-1][0]
+                lines = [f"[{dt.datetime.now()}] Iteration {ast['idx']:>_d}"]
+                for field, value in zip(h.dtype.names, h):
+                    lines.append(f"\t{field}: {value}")
+                msg = "\n".join(lines)
+            ast["logger"].info(msg)
+
+        def _update_history():
+            data = ast["stop_crit"].info()
+            ftype = pxrt.getPrecision().value
+            dtype = np.dtype([("iteration", np.int64)] + [(k, ftype) for k in data])
+            rec = np.zeros(1, dtype=dtype)
+            rec["iteration"] = ast["idx"]
+            for k, v in data.items():
+                rec[k] = v
+            ast["history"].append(rec)
+
+        try:
+            if _ms and ast["track_objective"]:
+                self._mstate["objective_func"] = self.objective_func().reshape(-1)
+            if _ms and ast["stop_crit"].stop(self._mstate):
+                _update_history()
+                _log()
+                _log(msg=f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
+                self.writeback()
+                return False
+            if _ms:
+                _update_history()
+            if _ml:
+                _log()
+            if _mw:
+                self.writeback()
+            ast["idx"] += 1
+            self.m_step()
+            return True
+        except Exception as e:
+            msg = f"[{dt.datetime.now()}] Something went wrong -> EXCEPTION RAISED"
+            print("\n".join([msg, f"More information: {self.logfile}."]), file=sys.stderr)
+            if ast["wb_rate"] is not None:
+                _, r = divmod(ast["idx"], ast["wb_rate"])
+                msg = "\n".join([msg, f"Last valid checkpoint done at iteration={ast['idx'] - r}."])
+            ast["logger"].exception(msg, exc_info=e)
+            ast["exception"] = e
+            return False
+
+    def _cleanup_logger(self):
+        logger = logging.getLogger(str(self.workdir))
+        for handler in logger.handlers:
+            handler.close()
+
+    class _Worker(threading.Thread):
+        def __init__(self, solver):
+            super().__init__()
+            self.slvr = solver
+            # the worker must launch on the caller's device and stream (torch keeps both per thread)
+            import torch
+
+            self._dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+            self._stream = torch.cuda.current_stream() if torch.cuda.is_available() else None
+
+        def run(self):
+            import torch
+
+            if self._dev is not None:
+                torch.cuda.set_device(self._dev)
+                with torch.cuda.stream(self._stream):
+                    self._loop()
+            else:
+                self._loop()
+
+        def _loop(self):
+            while self.slvr.busy() and self.slvr._step():
+                pass
+            self.slvr._astate["active"].clear()

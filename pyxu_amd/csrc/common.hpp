@@ -1,0 +1,66 @@
+// pyxu_amd — shared helpers for the gfx950 kernels behind the C-ABI (include/pyxu_amd.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pyxu_amd.h"
+
+namespace pxa {
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+// Launch geometry for streaming kernels: 256 threads, at most 8 blocks per CU (256 CUs).
+constexpr int kBlock = 256;
+constexpr int kMaxGrid = 256 * 8;
+
+inline int grid_for(int64_t work_items, int per_block = kBlock) {
+  int64_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > kMaxGrid) g = kMaxGrid;
+  return (int)g;
+}
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int last_launch_status() {
+  hipError_t e = hipGetLastError();
+  return (int)e;
+}
+
+template <typename T>
+struct Vec4;
+template <>
+struct Vec4<float> {
+  using type = float4;
+};
+template <>
+struct Vec4<double> {
+  using type = double2;  // 16 B per lane for both precisions
+};
+
+// Elements per 16-byte vector.
+template <typename T>
+constexpr int kVecN = 16 / sizeof(T);
+
+}  // namespace pxa
+
+// dtype dispatch: `code` is PXA_F32 / PXA_F64.
+#define PXA_DISPATCH(code, T, ...)                 \
+  do {                                             \
+    if ((code) == PXA_F32) {                       \
+      using T = float;                             \
+      __VA_ARGS__;                                 \
+    } else if ((code) == PXA_F64) {                \
+      using T = double;                            \
+      __VA_ARGS__;                                 \
+    } else {                                       \
+      return PXA_ERR_DTYPE;                        \
+    }                                              \
+  } while (0)
+
+#define PXA_CHECK_ARG(cond)        \
+  do {                             \
+    if (!(cond)) return PXA_ERR_ARG; \
+  } while (0)

@@ -1,0 +1,300 @@
+// Element-wise kernels: operator-algebra glue, solver updates and the separable proxes.
+//
+// HBM-bound streaming: 16 B per lane per access (float4 / double2), grid-stride over at most
+// 8 workgroups per CU.  A scalar tail handles n % V and unaligned views.
+#include "common.hpp"
+
+namespace pxa {
+namespace {
+
+// ---------------------------------------------------------------- generic vectorised map
+// Op::operator()(T* v[NIN], T& out) style is awkward in device code; use per-element functors
+// that receive the element index so each kernel reads exactly what it needs.
+template <typename T, int NIN, typename Op>
+__global__ void __launch_bounds__(kBlock) map_kernel(int64_t n, Op op, const T* __restrict__ a,
+                                                     const T* __restrict__ b, const T* __restrict__ c,
+                                                     T* __restrict__ out, bool vec) {
+  constexpr int V = kVecN<T>;
+  using VT = typename Vec4<T>::type;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t nv = vec ? n / V : 0;
+  for (int64_t i = tid; i < nv; i += stride) {
+    T va[V], vb[V], vc[V], vo[V];
+    *reinterpret_cast<VT*>(va) = reinterpret_cast<const VT*>(a)[i];
+    if (NIN > 1) *reinterpret_cast<VT*>(vb) = reinterpret_cast<const VT*>(b)[i];
+    if (NIN > 2) *reinterpret_cast<VT*>(vc) = reinterpret_cast<const VT*>(c)[i];
+#pragma unroll
+    for (int k = 0; k < V; ++k) vo[k] = op(va[k], NIN > 1 ? vb[k] : T(0), NIN > 2 ? vc[k] : T(0));
+    reinterpret_cast<VT*>(out)[i] = *reinterpret_cast<VT*>(vo);
+  }
+  for (int64_t i = nv * V + tid; i < n; i += stride) {
+    out[i] = op(a[i], NIN > 1 ? b[i] : T(0), NIN > 2 ? c[i] : T(0));
+  }
+}
+
+template <typename T, int NIN, typename Op>
+int launch_map(int64_t n, Op op, const void* a, const void* b, const void* c, void* out, void* stream) {
+  PXA_CHECK_ARG(n >= 0);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(a != nullptr && out != nullptr);
+  if (NIN > 1) PXA_CHECK_ARG(b != nullptr);
+  if (NIN > 2) PXA_CHECK_ARG(c != nullptr);
+  bool vec = aligned16(a) && aligned16(out) && (NIN < 2 || aligned16(b)) && (NIN < 3 || aligned16(c));
+  int64_t items = vec ? (n + kVecN<T> - 1) / kVecN<T> : n;
+  hipLaunchKernelGGL((map_kernel<T, NIN, Op>), dim3(grid_for(items)), dim3(kBlock), 0, as_stream(stream), n, op,
+                     (const T*)a, (const T*)b, (const T*)c, (T*)out, vec);
+  return last_launch_status();
+}
+
+template <typename T>
+struct AxpbyOp {
+  T a, b;
+  __device__ T operator()(T x, T y, T) const { return a * x + b * y; }
+};
+template <typename T>
+struct ScaleOp {
+  T a;
+  __device__ T operator()(T x, T, T) const { return a * x; }
+};
+template <typename T>
+struct ExtrapOp {  // (x - y) * a + x   (PGD momentum, pgd.py:179-181)
+  T a;
+  __device__ T operator()(T x, T y, T) const {
+    T d = x - y;
+    d = d * a;
+    return d + x;
+  }
+};
+template <typename T>
+struct Lin3Op {
+  T a, b, c;
+  __device__ T operator()(T x, T y, T z) const { return a * x + b * y + c * z; }
+};
+template <typename T>
+struct DivOp {
+  T d;
+  __device__ T operator()(T x, T, T) const { return x / d; }
+};
+template <typename T>
+struct AddScalarOp {
+  T s;
+  __device__ T operator()(T x, T, T) const { return x + s; }
+};
+template <typename T>
+struct FillOp {
+  T v;
+  __device__ T operator()(T, T, T) const { return v; }
+};
+template <typename T>
+struct MulOp {
+  __device__ T operator()(T x, T y, T) const { return x * y; }
+};
+template <typename T>
+struct ClipOp {
+  T lo, hi;
+  bool has_hi;
+  __device__ T operator()(T x, T, T) const {
+    // numpy clip(x, lo, None): max(x, lo); NaN propagates like numpy.
+    T r = x < lo ? lo : x;
+    if (has_hi) r = r > hi ? hi : r;
+    return r;
+  }
+};
+
+// L1Norm.prox: fmax(0, |x| - tau) * sign(x)   (norm.py:47-52)
+template <typename T>
+__device__ inline T soft(T x, T tau) {
+  T m = fabs(x) - tau;
+  m = m > T(0) ? m : T(0);
+  T s = x > T(0) ? T(1) : (x < T(0) ? T(-1) : T(0));
+  return m * s;
+}
+
+template <typename T>
+struct ProxL1Op {
+  T tau;
+  __device__ T operator()(T x, T, T) const { return soft(x, tau); }
+};
+// x - sigma * prox_{lam/sigma}(x / sigma)
+template <typename T>
+struct FenchelL1Op {
+  T sigma, t;  // t = (1/sigma) * lam, computed in T on the host exactly like the reference
+  __device__ T operator()(T x, T, T) const {
+    T p = soft(x / sigma, t);
+    return p * (-sigma) + x;
+  }
+};
+// scale * (x - prox_{mu}(x)) / mu
+template <typename T>
+struct MoreauL1Op {
+  T mu, scale;
+  __device__ T operator()(T x, T, T) const {
+    T r = x - soft(x, mu);
+    r = r / mu;
+    return r * scale;
+  }
+};
+
+// ---------------------------------------------------------------- grouped (L21) kernels
+// x viewed as (outer, group, inner): one thread per (outer, inner) column.
+enum GroupMode { kProx = 0, kFenchel = 1, kMoreau = 2, kNorm = 3 };
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(kBlock) group_kernel(int64_t outer, int64_t group, int64_t inner,
+                                                       const T* __restrict__ x, T* __restrict__ out, T p0, T p1,
+                                                       T p2) {
+  const int64_t total = outer * inner;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    int64_t o = t / inner, i = t - o * inner;
+    const T* xp = x + o * group * inner + i;
+    T* op = out + o * group * inner + i;
+    // Pass 1: l2 norm over the group (reference: (arr**2).sum(l2_axis); sqrt).
+    T s = T(0);
+    for (int64_t g = 0; g < group; ++g) {
+      T v = xp[g * inner];
+      if (MODE == kFenchel) v = v / p0;
+      s += v * v;
+    }
+    T n = sqrt(s);
+    if (MODE == kNorm) {
+      out[t] = n;
+      continue;
+    }
+    T tau = (MODE == kProx) ? p0 : (MODE == kFenchel ? p1 : p0);
+    T f = T(1) - tau / (n > tau ? n : tau);  // 1 - tau / fmax(n, tau)
+    for (int64_t g = 0; g < group; ++g) {
+      T v = xp[g * inner];
+      T r;
+      if (MODE == kProx) {
+        r = v * f;
+      } else if (MODE == kFenchel) {  // x - sigma * prox(x/sigma, lam/sigma)
+        T p = (v / p0) * f;
+        r = p * (-p0) + v;
+      } else {  // kMoreau: scale * (x - prox_mu(x)) / mu
+        r = (v - v * f) / p0;
+        r = r * p2;
+      }
+      op[g * inner] = r;
+    }
+  }
+}
+
+template <typename T, int MODE>
+int launch_group(int64_t outer, int64_t group, int64_t inner, const void* x, void* out, double p0, double p1,
+                 double p2, void* stream) {
+  PXA_CHECK_ARG(outer >= 0 && group >= 1 && inner >= 0);
+  if (outer * inner == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && out != nullptr);
+  hipLaunchKernelGGL((group_kernel<T, MODE>), dim3(grid_for(outer * inner)), dim3(kBlock), 0, as_stream(stream),
+                     outer, group, inner, (const T*)x, (T*)out, (T)p0, (T)p1, (T)p2);
+  return last_launch_status();
+}
+
+// out[i] = a*x[i] + b*y[i % ny]   (stack broadcast of a (ny,) vector; ArgShiftRule / AddRule)
+template <typename T>
+__global__ void __launch_bounds__(kBlock) bcast_kernel(int64_t n, int64_t ny, T a, const T* __restrict__ x, T b,
+                                                       const T* __restrict__ y, T* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = a * x[i] + b * y[i % ny];
+}
+
+}  // namespace
+}  // namespace pxa
+
+using namespace pxa;
+
+extern "C" {
+
+int pxa_axpby(int dtype, int64_t n, double a, const void* x, double b, const void* y, void* out, void* stream) {
+  if (y == nullptr) {
+    PXA_DISPATCH(dtype, T, return (launch_map<T, 1>(n, ScaleOp<T>{(T)a}, x, nullptr, nullptr, out, stream)));
+  }
+  PXA_DISPATCH(dtype, T, return (launch_map<T, 2>(n, AxpbyOp<T>{(T)a, (T)b}, x, y, nullptr, out, stream)));
+}
+
+int pxa_axpby_bcast(int dtype, int64_t n, double a, const void* x, double b, const void* y, int64_t ny, void* out,
+                    void* stream) {
+  PXA_CHECK_ARG(n >= 0 && ny >= 1 && n % ny == 0);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(x && y && out);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((bcast_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, ny, (T)a,
+                       (const T*)x, (T)b, (const T*)y, (T*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_lincomb3(int dtype, int64_t n, double a, const void* x, double b, const void* y, double c, const void* z,
+                 void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_map<T, 3>(n, Lin3Op<T>{(T)a, (T)b, (T)c}, x, y, z, out, stream)));
+}
+
+int pxa_extrapolate(int dtype, int64_t n, double a, const void* x, const void* y, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_map<T, 2>(n, ExtrapOp<T>{(T)a}, x, y, nullptr, out, stream)));
+}
+
+int pxa_div(int dtype, int64_t n, const void* x, double d, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_map<T, 1>(n, DivOp<T>{(T)d}, x, nullptr, nullptr, out, stream)));
+}
+
+int pxa_add_scalar(int dtype, int64_t n, const void* x, double s, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_map<T, 1>(n, AddScalarOp<T>{(T)s}, x, nullptr, nullptr, out, stream)));
+}
+
+int pxa_mul(int dtype, int64_t n, const void* x, const void* y, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_map<T, 2>(n, MulOp<T>{}, x, y, nullptr, out, stream)));
+}
+
+int pxa_clip(int dtype, int64_t n, const void* x, double lo, double hi, int has_hi, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T,
+               return (launch_map<T, 1>(n, ClipOp<T>{(T)lo, (T)hi, has_hi != 0}, x, nullptr, nullptr, out, stream)));
+}
+
+int pxa_prox_l1(int dtype, int64_t n, const void* x, double tau, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_map<T, 1>(n, ProxL1Op<T>{(T)tau}, x, nullptr, nullptr, out, stream)));
+}
+
+int pxa_fenchel_prox_l1(int dtype, int64_t n, const void* x, double sigma, double lam, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, {
+    T s = (T)sigma;
+    T t = (T(1) / s) * (T)lam;
+    return (launch_map<T, 1>(n, FenchelL1Op<T>{s, t}, x, nullptr, nullptr, out, stream));
+  });
+}
+
+int pxa_moreau_grad_l1(int dtype, int64_t n, const void* x, double mu, double scale, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T,
+               return (launch_map<T, 1>(n, MoreauL1Op<T>{(T)mu, (T)scale}, x, nullptr, nullptr, out, stream)));
+}
+
+int pxa_fill(int dtype, int64_t n, double v, void* out, void* stream) {
+  // `a` is read but ignored by FillOp; pass `out` so the pointer is valid and aligned alike.
+  PXA_DISPATCH(dtype, T, return (launch_map<T, 1>(n, FillOp<T>{(T)v}, out, nullptr, nullptr, out, stream)));
+}
+
+int pxa_prox_l21(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, double tau, void* out,
+                 void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_group<T, kProx>(outer, group, inner, x, out, tau, 0, 0, stream)));
+}
+
+int pxa_fenchel_prox_l21(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, double sigma,
+                         double lam, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, {
+    T s = (T)sigma;
+    T t = (T(1) / s) * (T)lam;
+    return (launch_group<T, kFenchel>(outer, group, inner, x, out, (double)s, (double)t, 0, stream));
+  });
+}
+
+int pxa_moreau_grad_l21(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, double mu,
+                        double scale, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_group<T, kMoreau>(outer, group, inner, x, out, mu, 0, scale, stream)));
+}
+
+int pxa_group_norm(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, void* out, void* stream) {
+  PXA_DISPATCH(dtype, T, return (launch_group<T, kNorm>(outer, group, inner, x, out, 0, 0, 0, stream)));
+}
+
+}  // extern "C"

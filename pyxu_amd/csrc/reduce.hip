@@ -1,0 +1,132 @@
+// Deterministic row reductions (RelError / AbsError norms, CG dot products, L1/L2 norms).
+//
+// Two launches: (1) a (blocks_per_row x rows) grid accumulates fixed chunks in double and writes
+// one partial per workgroup; (2) one thread per row sums its partials in index order.  The
+// partition depends only on (rows, n), so results are bitwise reproducible run to run.
+#include "common.hpp"
+
+namespace pxa {
+namespace {
+
+inline int blocks_per_row(int64_t rows, int64_t n) {
+  int64_t per = (n + 16383) / 16384;  // >= 16 K elements per workgroup
+  int64_t cap = rows > 0 ? (2048 + rows - 1) / rows : 1;
+  if (cap < 1) cap = 1;
+  if (per > cap) per = cap;
+  if (per > 1024) per = 1024;
+  if (per < 1) per = 1;
+  return (int)per;
+}
+
+template <typename T, int OP>
+__device__ inline double elem(T x, T y) {
+  if (OP == PXA_RED_SUMSQ) return (double)x * (double)x;
+  if (OP == PXA_RED_DIFFSQ) {
+    double d = (double)x - (double)y;
+    return d * d;
+  }
+  if (OP == PXA_RED_DOT) return (double)x * (double)y;
+  if (OP == PXA_RED_ABS) return fabs((double)x);
+  if (OP == PXA_RED_MAXABS) return fabs((double)x);
+  if (OP == PXA_RED_SUM) return (double)x;
+  if (OP == PXA_RED_NEGCNT) return x < T(0) ? 1.0 : 0.0;
+  return 0.0;
+}
+
+template <int OP>
+__device__ inline double combine(double a, double b) {
+  if (OP == PXA_RED_MAXABS) return a > b ? a : b;
+  return a + b;
+}
+
+template <int OP>
+__device__ inline double wave_reduce(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = combine<OP>(v, __shfl_down(v, off, 64));
+  return v;
+}
+
+template <typename T, int OP>
+__global__ void __launch_bounds__(kBlock) row_partial_kernel(int64_t n, int nb, const T* __restrict__ x,
+                                                             const T* __restrict__ y, double* __restrict__ part) {
+  const int64_t row = blockIdx.y;
+  const T* xr = x + row * n;
+  const T* yr = y ? y + row * n : nullptr;
+  int64_t chunk = (n + nb - 1) / nb;
+  int64_t lo = (int64_t)blockIdx.x * chunk;
+  int64_t hi = lo + chunk < n ? lo + chunk : n;
+  double acc = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc = combine<OP>(acc, elem<T, OP>(xr[i], yr ? yr[i] : T(0)));
+  acc = wave_reduce<OP>(acc);
+  __shared__ double sw[kBlock / kWave];
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) sw[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = sw[0];
+    for (int k = 1; k < kBlock / kWave; ++k) r = combine<OP>(r, sw[k]);
+    part[row * nb + blockIdx.x] = r;
+  }
+}
+
+template <int OP>
+__global__ void row_final_kernel(int64_t rows, int nb, const double* __restrict__ part, double* __restrict__ out) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  double acc = part[r * nb];
+  for (int k = 1; k < nb; ++k) acc = combine<OP>(acc, part[r * nb + k]);
+  out[r] = acc;
+}
+
+template <typename T, int OP>
+int launch_reduce(int64_t rows, int64_t n, const void* x, const void* y, double* out, void* work, void* stream) {
+  int nb = blocks_per_row(rows, n);
+  double* part = (double*)work;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL((row_partial_kernel<T, OP>), dim3(nb, (unsigned)rows), dim3(kBlock), 0, s, n, nb, (const T*)x,
+                     (const T*)y, part);
+  int e = last_launch_status();
+  if (e) return e;
+  hipLaunchKernelGGL((row_final_kernel<OP>), dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, rows, nb, part,
+                     out);
+  return last_launch_status();
+}
+
+}  // namespace
+}  // namespace pxa
+
+using namespace pxa;
+
+extern "C" {
+
+size_t pxa_row_reduce_workspace_bytes(int64_t rows, int64_t n) {
+  if (rows <= 0) return 0;
+  return (size_t)rows * (size_t)blocks_per_row(rows, n) * sizeof(double);
+}
+
+int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, const void* y, double* out, void* work,
+                   void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && n >= 0);
+  if (rows == 0) return PXA_OK;
+  PXA_CHECK_ARG(rows <= 65535);  // grid.y limit
+  PXA_CHECK_ARG(x != nullptr && out != nullptr && work != nullptr);
+  if (op == PXA_RED_DIFFSQ || op == PXA_RED_DOT) PXA_CHECK_ARG(y != nullptr);
+  if (n == 0) return (int)hipMemsetAsync(out, 0, rows * sizeof(double), as_stream(stream));
+#define PXA_RED_CASE(OPC) \
+  case OPC:               \
+    PXA_DISPATCH(dtype, T, return (launch_reduce<T, OPC>(rows, n, x, y, out, work, stream)));
+  switch (op) {
+    PXA_RED_CASE(PXA_RED_SUMSQ)
+    PXA_RED_CASE(PXA_RED_DIFFSQ)
+    PXA_RED_CASE(PXA_RED_DOT)
+    PXA_RED_CASE(PXA_RED_ABS)
+    PXA_RED_CASE(PXA_RED_MAXABS)
+    PXA_RED_CASE(PXA_RED_SUM)
+    PXA_RED_CASE(PXA_RED_NEGCNT)
+    default:
+      return PXA_ERR_ARG;
+  }
+#undef PXA_RED_CASE
+}
+
+}  // extern "C"

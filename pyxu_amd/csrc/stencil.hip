@@ -1,0 +1,426 @@
+// Stencil family: separable-axis passes, N-D stencils, Pad / Pad^T / Trim / Trim^T.
+//
+// Semantics follow the reference exactly (see include/pyxu_amd.h); the constant-mode path
+// (zero_partial = 0) evaluates Trim o S o Pad without ever materialising the padded array.
+// Memory-bound: one thread per output, lanes contiguous along the last (fastest) axis so every
+// tap load is a coalesced row segment; tap re-reads are served by L1/L2.
+#include "common.hpp"
+
+namespace pxa {
+namespace {
+
+struct Geom {
+  int nd;
+  int64_t n[PXA_MAX_DIM];
+  int64_t st[PXA_MAX_DIM];  // element strides (row-major)
+  int64_t size;             // prod(n)
+};
+
+inline bool make_geom(int ndim, const int64_t* shape, Geom& g) {
+  if (ndim < 1 || ndim > PXA_MAX_DIM || shape == nullptr) return false;
+  g.nd = ndim;
+  int64_t s = 1;
+  for (int i = ndim - 1; i >= 0; --i) {
+    if (shape[i] < 1) return false;
+    g.n[i] = shape[i];
+    g.st[i] = s;
+    s *= shape[i];
+  }
+  for (int i = ndim; i < PXA_MAX_DIM; ++i) {
+    g.n[i] = 1;
+    g.st[i] = 0;
+  }
+  g.size = s;
+  return true;
+}
+
+template <typename T>
+struct AxisTaps {
+  int n;
+  int off[PXA_MAX_TAPS];
+  T coef[PXA_MAX_TAPS];
+};
+
+// ------------------------------------------------------------------ one separable-axis pass
+template <typename T, bool ZERO_PARTIAL>
+__global__ void __launch_bounds__(kBlock) axis_kernel(int64_t stack, Geom g, int axis, AxisTaps<T> tp,
+                                                      const T* __restrict__ x, int64_t xs, T* __restrict__ y,
+                                                      int64_t ys, T beta) {
+  const int64_t total = stack * g.size;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t sa = g.st[axis], na = g.n[axis];
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    int64_t s = t / g.size, r = t - s * g.size;
+    int64_t ca = (r / sa) % na;
+    const T* xr = x + s * xs + r;
+    T acc = T(0);
+    bool inside = true;
+    for (int q = 0; q < tp.n; ++q) {
+      int64_t c = ca + tp.off[q];
+      if (c >= 0 && c < na) {
+        acc += tp.coef[q] * xr[(int64_t)tp.off[q] * sa];
+      } else if (ZERO_PARTIAL) {
+        inside = false;
+      }
+    }
+    if (ZERO_PARTIAL && !inside) acc = T(0);
+    T* yp = y + s * ys + r;
+    *yp = (beta == T(0)) ? acc : acc + beta * (*yp);
+  }
+}
+
+template <typename T>
+int launch_axis(int64_t stack, const Geom& g, int axis, int ntaps, const int32_t* offs, const double* coefs,
+                int zero_partial, const void* x, int64_t xs, void* y, int64_t ys, double beta, hipStream_t s) {
+  AxisTaps<T> tp;
+  tp.n = ntaps;
+  for (int q = 0; q < ntaps; ++q) {
+    tp.off[q] = offs[q];
+    tp.coef[q] = (T)coefs[q];
+  }
+  int64_t total = stack * g.size;
+  if (zero_partial)
+    hipLaunchKernelGGL((axis_kernel<T, true>), dim3(grid_for(total)), dim3(kBlock), 0, s, stack, g, axis, tp,
+                       (const T*)x, xs, (T*)y, ys, (T)beta);
+  else
+    hipLaunchKernelGGL((axis_kernel<T, false>), dim3(grid_for(total)), dim3(kBlock), 0, s, stack, g, axis, tp,
+                       (const T*)x, xs, (T*)y, ys, (T)beta);
+  return last_launch_status();
+}
+
+// ------------------------------------------------------------------ N-D stencil (device taps)
+template <typename T, bool ZERO_PARTIAL>
+__global__ void __launch_bounds__(kBlock) nd_kernel(int64_t stack, Geom g, int ntaps, const int32_t* __restrict__ offs,
+                                                    const T* __restrict__ coefs, const T* __restrict__ x, int64_t xs,
+                                                    T* __restrict__ y, int64_t ys, T beta) {
+  const int64_t total = stack * g.size;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    int64_t s = t / g.size, r = t - s * g.size;
+    int64_t c[PXA_MAX_DIM];
+    int64_t rem = r;
+#pragma unroll
+    for (int d = 0; d < PXA_MAX_DIM; ++d) {
+      if (d < g.nd) {
+        c[d] = rem / g.st[d];
+        rem -= c[d] * g.st[d];
+      }
+    }
+    const T* xr = x + s * xs;
+    T acc = T(0);
+    bool inside = true;
+    for (int q = 0; q < ntaps; ++q) {
+      int64_t idx = 0;
+      bool ok = true;
+      for (int d = 0; d < g.nd; ++d) {
+        int64_t cc = c[d] + offs[q * g.nd + d];
+        ok = ok && (cc >= 0) && (cc < g.n[d]);
+        idx += cc * g.st[d];
+      }
+      if (ok)
+        acc += coefs[q] * xr[idx];
+      else if (ZERO_PARTIAL)
+        inside = false;
+    }
+    if (ZERO_PARTIAL && !inside) acc = T(0);
+    T* yp = y + s * ys + r;
+    *yp = (beta == T(0)) ? acc : acc + beta * (*yp);
+  }
+}
+
+// ------------------------------------------------------------------ Pad / Pad^T / Trim
+struct PadGeom {
+  Geom core;  // unpadded shape
+  Geom pad;   // padded shape
+  int64_t lo[PXA_MAX_DIM], hi[PXA_MAX_DIM];
+  int mode[PXA_MAX_DIM];
+};
+
+// Map a padded coordinate j (0 <= j < n + lo + hi) to the core coordinate it copies
+// (pad.py:254-304); returns -1 for constant-mode padding (value 0).
+__device__ inline int64_t pad_src(int64_t j, int64_t n, int64_t lo, int mode) {
+  int64_t c = j - lo;
+  if (c >= 0 && c < n) return c;
+  switch (mode) {
+    case PXA_MODE_CONSTANT:
+      return -1;
+    case PXA_MODE_WRAP:
+      return c < 0 ? c + n : c - n;
+    case PXA_MODE_REFLECT:
+      return c < 0 ? -c : 2 * (n - 1) - c;
+    case PXA_MODE_SYMMETRIC:
+      return c < 0 ? -c - 1 : 2 * n - 1 - c;
+    default:  // edge
+      return c < 0 ? 0 : n - 1;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) pad_kernel(int64_t stack, PadGeom pg, const T* __restrict__ x,
+                                                     T* __restrict__ y) {
+  const int64_t total = stack * pg.pad.size;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    int64_t s = t / pg.pad.size, r = t - s * pg.pad.size;
+    int64_t src = 0;
+    bool zero = false;
+    for (int d = 0; d < pg.pad.nd; ++d) {
+      int64_t j = (r / pg.pad.st[d]) % pg.pad.n[d];
+      int64_t c = pad_src(j, pg.core.n[d], pg.lo[d], pg.mode[d]);
+      if (c < 0) zero = true;
+      src += (c < 0 ? 0 : c) * pg.core.st[d];
+    }
+    y[t] = zero ? T(0) : x[s * pg.core.size + src];
+  }
+}
+
+// Fold the pad region of axis `a` back onto the core of that axis (Pad^T for one axis, in place on
+// a buffer whose axes < a are still padded and axes > a already folded... all strides given by
+// `cur`).  One thread per element whose axis-a coordinate lies in the core.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) fold_axis_kernel(int64_t stack, Geom cur, int a, int64_t n, int64_t lo,
+                                                           int64_t hi, int mode, T* __restrict__ buf) {
+  // iterate over all elements with axis-a coordinate in [lo, lo+n)
+  Geom it = cur;
+  it.n[a] = n;
+  int64_t inner = 1;
+  for (int d = 0; d < it.nd; ++d) inner *= it.n[d];
+  const int64_t total = stack * inner;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    int64_t s = t / inner, r = t - s * inner;
+    // unravel r over `it` shape
+    int64_t off = 0, ca = 0;
+    int64_t rem = r;
+    for (int d = it.nd - 1; d >= 0; --d) {
+      int64_t cd = rem % it.n[d];
+      rem /= it.n[d];
+      if (d == a) {
+        ca = cd;
+        cd += lo;
+      }
+      off += cd * cur.st[d];
+    }
+    T* base = buf + s * cur.size + off - (ca + lo) * cur.st[a];  // axis-a line start
+    T v = base[(ca + lo) * cur.st[a]];
+    // LHS images first, then RHS (pad.py:318-365 order).
+    for (int64_t j = 0; j < lo; ++j)
+      if (pad_src(j, n, lo, mode) == ca) v += base[j * cur.st[a]];
+    for (int64_t j = lo + n; j < lo + n + hi; ++j)
+      if (pad_src(j, n, lo, mode) == ca) v += base[j * cur.st[a]];
+    base[(ca + lo) * cur.st[a]] = v;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) trim_kernel(int64_t stack, PadGeom pg, int embed, const T* __restrict__ x,
+                                                      T* __restrict__ y) {
+  // embed = 0: y (core) <- x (padded) core window; embed = 1: y (padded) <- 0 | x (core)
+  const Geom& big = pg.pad;
+  const int64_t total = stack * (embed ? big.size : pg.core.size);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    if (embed) {
+      int64_t s = t / big.size, r = t - s * big.size;
+      int64_t src = 0;
+      bool in = true;
+      for (int d = 0; d < big.nd; ++d) {
+        int64_t c = (r / big.st[d]) % big.n[d] - pg.lo[d];
+        in = in && c >= 0 && c < pg.core.n[d];
+        src += c * pg.core.st[d];
+      }
+      y[t] = in ? x[s * pg.core.size + src] : T(0);
+    } else {
+      int64_t s = t / pg.core.size, r = t - s * pg.core.size;
+      int64_t dst = 0;
+      for (int d = 0; d < big.nd; ++d) {
+        int64_t c = (r / pg.core.st[d]) % pg.core.n[d] + pg.lo[d];
+        dst += c * big.st[d];
+      }
+      y[t] = x[s * big.size + dst];
+    }
+  }
+}
+
+inline bool make_pad_geom(int ndim, const int64_t* shape, const int64_t* lo, const int64_t* hi, const int* modes,
+                          PadGeom& pg) {
+  if (!make_geom(ndim, shape, pg.core)) return false;
+  int64_t ps[PXA_MAX_DIM];
+  for (int d = 0; d < ndim; ++d) {
+    if (lo[d] < 0 || hi[d] < 0) return false;
+    ps[d] = shape[d] + lo[d] + hi[d];
+    pg.lo[d] = lo[d];
+    pg.hi[d] = hi[d];
+    pg.mode[d] = modes ? modes[d] : PXA_MODE_CONSTANT;
+    if (pg.mode[d] < 0 || pg.mode[d] > 4) return false;
+    int64_t w = lo[d] > hi[d] ? lo[d] : hi[d];
+    int64_t wmax = pg.mode[d] == PXA_MODE_WRAP || pg.mode[d] == PXA_MODE_SYMMETRIC ? shape[d]
+                   : pg.mode[d] == PXA_MODE_REFLECT                                ? shape[d] - 1
+                                                                                   : INT64_MAX;
+    if (w > wmax) return false;  // pad.py:215-228
+  }
+  for (int d = ndim; d < PXA_MAX_DIM; ++d) {
+    pg.lo[d] = pg.hi[d] = 0;
+    pg.mode[d] = 0;
+  }
+  return make_geom(ndim, ps, pg.pad);
+}
+
+}  // namespace
+}  // namespace pxa
+
+using namespace pxa;
+
+extern "C" {
+
+int pxa_stencil_axis(int dtype, int64_t stack, int ndim, const int64_t* shape, int axis, int ntaps,
+                     const int32_t* offsets, const double* coefs, int zero_partial, const void* x,
+                     int64_t x_stack_stride, void* y, int64_t y_stack_stride, double beta, void* stream) {
+  Geom g;
+  PXA_CHECK_ARG(make_geom(ndim, shape, g));
+  PXA_CHECK_ARG(axis >= 0 && axis < ndim && stack >= 0);
+  PXA_CHECK_ARG(ntaps >= 0 && ntaps <= PXA_MAX_TAPS);
+  PXA_CHECK_ARG(ntaps == 0 || (offsets != nullptr && coefs != nullptr));
+  if (stack == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && y != nullptr);
+  PXA_DISPATCH(dtype, T,
+               return launch_axis<T>(stack, g, axis, ntaps, offsets, coefs, zero_partial, x, x_stack_stride, y,
+                                     y_stack_stride, beta, as_stream(stream)));
+}
+
+size_t pxa_stencil_sep_workspace_bytes(int dtype, int64_t stack, int ndim, const int64_t* shape, const int* ntaps) {
+  Geom g;
+  if (!make_geom(ndim, shape, g) || ntaps == nullptr) return 0;
+  int k = 0;
+  for (int d = 0; d < ndim; ++d) k += ntaps[d] > 0;
+  size_t fields = k <= 1 ? 0 : (k == 2 ? 1 : 2);
+  size_t es = dtype == PXA_F64 ? 8 : 4;
+  return fields * (size_t)stack * (size_t)g.size * es;
+}
+
+int pxa_stencil_sep(int dtype, int64_t stack, int ndim, const int64_t* shape, const int* ntaps,
+                    const int32_t* offsets, const double* coefs, const void* x, int64_t x_stack_stride, void* y,
+                    int64_t y_stack_stride, double beta, void* work, void* stream) {
+  Geom g;
+  PXA_CHECK_ARG(make_geom(ndim, shape, g));
+  PXA_CHECK_ARG(ntaps != nullptr && offsets != nullptr && coefs != nullptr);
+  if (stack == 0) return PXA_OK;
+  int axes[PXA_MAX_DIM], k = 0;
+  for (int d = 0; d < ndim; ++d) {
+    PXA_CHECK_ARG(ntaps[d] >= 0 && ntaps[d] <= PXA_MAX_TAPS);
+    if (ntaps[d] > 0) axes[k++] = d;
+  }
+  hipStream_t s = as_stream(stream);
+  size_t es = dtype == PXA_F64 ? 8 : 4;
+  if (k == 0) {  // all-identity kernel: y = x + beta*y
+    PXA_CHECK_ARG(x_stack_stride == g.size && y_stack_stride == g.size);
+    return pxa_axpby(dtype, stack * g.size, 1.0, x, beta, beta == 0.0 ? nullptr : y, y, stream);
+  }
+  PXA_CHECK_ARG(k == 1 || work != nullptr);
+  char* w0 = (char*)work;
+  char* w1 = w0 + (size_t)stack * g.size * es;
+  const void* src = x;
+  int64_t srcs = x_stack_stride;
+  for (int p = 0; p < k; ++p) {
+    int a = axes[p];
+    bool last = p == k - 1;
+    void* dst = last ? y : (void*)((p % 2 == 0) ? w0 : w1);
+    int64_t dsts = last ? y_stack_stride : g.size;
+    int e;
+    PXA_DISPATCH(dtype, T,
+                 e = launch_axis<T>(stack, g, a, ntaps[a], offsets + a * PXA_MAX_TAPS, coefs + a * PXA_MAX_TAPS, 0,
+                                    src, srcs, dst, dsts, last ? beta : 0.0, s));
+    if (e) return e;
+    src = dst;
+    srcs = dsts;
+  }
+  return PXA_OK;
+}
+
+int pxa_stencil_nd(int dtype, int64_t stack, int ndim, const int64_t* shape, int ntaps, const int32_t* offsets_dev,
+                   const void* coefs_dev, int zero_partial, const void* x, int64_t x_stack_stride, void* y,
+                   int64_t y_stack_stride, double beta, void* stream) {
+  Geom g;
+  PXA_CHECK_ARG(make_geom(ndim, shape, g));
+  PXA_CHECK_ARG(ntaps >= 0 && stack >= 0);
+  PXA_CHECK_ARG(ntaps == 0 || (offsets_dev != nullptr && coefs_dev != nullptr));
+  if (stack == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && y != nullptr);
+  int64_t total = stack * g.size;
+  PXA_DISPATCH(dtype, T, {
+    if (zero_partial)
+      hipLaunchKernelGGL((nd_kernel<T, true>), dim3(grid_for(total)), dim3(kBlock), 0, as_stream(stream), stack, g,
+                         ntaps, offsets_dev, (const T*)coefs_dev, (const T*)x, x_stack_stride, (T*)y, y_stack_stride,
+                         (T)beta);
+    else
+      hipLaunchKernelGGL((nd_kernel<T, false>), dim3(grid_for(total)), dim3(kBlock), 0, as_stream(stream), stack, g,
+                         ntaps, offsets_dev, (const T*)coefs_dev, (const T*)x, x_stack_stride, (T*)y, y_stack_stride,
+                         (T)beta);
+    return last_launch_status();
+  });
+}
+
+int pxa_pad(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* pad_lo, const int64_t* pad_hi,
+            const int* modes, const void* x, void* y, void* stream) {
+  PadGeom pg;
+  PXA_CHECK_ARG(pad_lo != nullptr && pad_hi != nullptr);
+  PXA_CHECK_ARG(make_pad_geom(ndim, shape, pad_lo, pad_hi, modes, pg));
+  if (stack == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && y != nullptr);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((pad_kernel<T>), dim3(grid_for(stack * pg.pad.size)), dim3(kBlock), 0, as_stream(stream),
+                       stack, pg, (const T*)x, (T*)y);
+    return last_launch_status();
+  });
+}
+
+int pxa_pad_adjoint(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* pad_lo,
+                    const int64_t* pad_hi, const int* modes, const void* x, void* y, void* work, void* stream) {
+  PadGeom pg;
+  PXA_CHECK_ARG(pad_lo != nullptr && pad_hi != nullptr);
+  PXA_CHECK_ARG(make_pad_geom(ndim, shape, pad_lo, pad_hi, modes, pg));
+  if (stack == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && y != nullptr && work != nullptr);
+  hipStream_t s = as_stream(stream);
+  size_t es = dtype == PXA_F64 ? 8 : 4;
+  hipError_t me = hipMemcpyAsync(work, x, (size_t)stack * pg.pad.size * es, hipMemcpyDeviceToDevice, s);
+  if (me) return (int)me;
+  PXA_DISPATCH(dtype, T, {
+    // Fold axes last -> first (pad.py:318-366), in place on `work` (padded layout throughout).
+    for (int a = ndim - 1; a >= 0; --a) {
+      if (pg.mode[a] == PXA_MODE_CONSTANT || (pg.lo[a] == 0 && pg.hi[a] == 0)) continue;
+      int64_t items = stack * (pg.pad.size / pg.pad.n[a]) * pg.core.n[a];
+      hipLaunchKernelGGL((fold_axis_kernel<T>), dim3(grid_for(items)), dim3(kBlock), 0, s, stack, pg.pad, a,
+                         pg.core.n[a], pg.lo[a], pg.hi[a], pg.mode[a], (T*)work);
+      int e = last_launch_status();
+      if (e) return e;
+    }
+    hipLaunchKernelGGL((trim_kernel<T>), dim3(grid_for(stack * pg.core.size)), dim3(kBlock), 0, s, stack, pg, 0,
+                       (const T*)work, (T*)y);
+    return last_launch_status();
+  });
+}
+
+int pxa_trim(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* lo, const int64_t* hi,
+             int embed, const void* x, void* y, void* stream) {
+  // `shape` is the PADDED (big) shape; the core is shape - lo - hi.
+  PXA_CHECK_ARG(shape != nullptr && lo != nullptr && hi != nullptr && ndim >= 1 && ndim <= PXA_MAX_DIM);
+  int64_t core[PXA_MAX_DIM];
+  int modes[PXA_MAX_DIM] = {0, 0, 0, 0};
+  for (int d = 0; d < ndim; ++d) {
+    core[d] = shape[d] - lo[d] - hi[d];
+    PXA_CHECK_ARG(core[d] >= 1);
+  }
+  PadGeom pg;
+  PXA_CHECK_ARG(make_pad_geom(ndim, core, lo, hi, modes, pg));
+  if (stack == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && y != nullptr);
+  int64_t total = stack * (embed ? pg.pad.size : pg.core.size);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((trim_kernel<T>), dim3(grid_for(total)), dim3(kBlock), 0, as_stream(stream), stack, pg,
+                       embed, (const T*)x, (T*)y);
+    return last_launch_status();
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,27 @@
+"""Indicator functions (reference operator/func/indicator.py) — PositiveOrthant (hot path)."""
+import numpy as np
+
+import pyxu_amd.abc as pxa
+import pyxu_amd.runtime as pxrt
+from pyxu_amd import _dev
+
+__all__ = ["PositiveOrthant"]
+
+
+class PositiveOrthant(pxa.ProxFunc):
+    """Indicator of {x >= 0} (indicator.py:174-206); prox = clip(0, None)."""
+
+    def __init__(self, dim):
+        super().__init__(shape=(1, dim))
+        self.lipschitz = np.inf
+
+    @pxrt.enforce_precision(i="arr")
+    def apply(self, arr):
+        neg = _dev.row_reduce(_dev.RED_NEGCNT, arr.reshape(-1, arr.shape[-1]))
+        out = neg.clone()
+        out[neg > 0] = float("inf")
+        return out.to(arr.dtype).reshape(*arr.shape[:-1], 1)
+
+    @pxrt.enforce_precision(i=("arr", "tau"))
+    def prox(self, arr, tau):
+        return _dev.clip(arr, 0.0)

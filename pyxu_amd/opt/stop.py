@@ -1,0 +1,205 @@
+"""
+Stopping criteria (mirrors reference ``pyxu.opt.stop``, src/pyxu/opt/stop.py).
+
+Norms are evaluated on the device (``pxa_row_reduce``, double accumulation) and only the per-row
+scalars cross to the host — the single device->host sync of a stop check (stop.py:381).
+"""
+import datetime as dt
+import numbers
+import warnings
+
+import numpy as np
+
+import pyxu_amd.abc as pxa
+from pyxu_amd import _dev
+
+__all__ = ["MaxIter", "ManualStop", "MaxDuration", "Memorize", "AbsError", "RelError"]
+
+
+def _rownorm(x, norm):
+    """(..., N) device tensor -> numpy (..., 1) Ln norm over the last axis."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if norm == 2:
+        v = _dev.row_reduce(_dev.RED_SUMSQ, x2).cpu().numpy() ** 0.5
+    elif norm == 1:
+        v = _dev.row_reduce(_dev.RED_ABS, x2).cpu().numpy()
+    elif norm == np.inf:
+        v = _dev.row_reduce(_dev.RED_MAXABS, x2).cpu().numpy()
+    else:
+        raise NotImplementedError(f"pyxu_amd: norm={norm} not supported on device (1, 2, inf).")
+    return v.reshape(*x.shape[:-1], 1)
+
+
+def _as_vec(x):
+    if isinstance(x, numbers.Real):
+        return None
+    return x
+
+
+class MaxIter(pxa.StoppingCriterion):
+    """Stop after `n` stop-checks (stop.py:29-68)."""
+
+    def __init__(self, n):
+        try:
+            assert int(n) > 0
+            self._n = int(n)
+        except Exception:
+            raise ValueError(f"n: expected positive integer, got {n}.")
+        self._i = 0
+
+    def stop(self, state) -> bool:
+        self._i += 1
+        return self._i > self._n
+
+    def info(self):
+        return dict(N_iter=self._i)
+
+    def clear(self):
+        self._i = 0
+
+
+class ManualStop(pxa.StoppingCriterion):
+    def stop(self, state) -> bool:
+        return False
+
+    def info(self):
+        return dict()
+
+
+class MaxDuration(pxa.StoppingCriterion):
+    def __init__(self, t: dt.timedelta):
+        try:
+            assert t > dt.timedelta()
+            self._t_max = t
+        except Exception:
+            raise ValueError(f"t: expected positive duration, got {t}.")
+        self._t_start = dt.datetime.now()
+        self._t_now = self._t_start
+
+    def stop(self, state) -> bool:
+        self._t_now = dt.datetime.now()
+        return (self._t_now - self._t_start) > self._t_max
+
+    def info(self):
+        return dict(duration=(self._t_now - self._t_start).total_seconds())
+
+    def clear(self):
+        self._t_start = dt.datetime.now()
+        self._t_now = self._t_start
+
+
+class Memorize(pxa.StoppingCriterion):
+    def __init__(self, var):
+        self._var = var
+        self._val = np.r_[0]
+
+    def stop(self, state) -> bool:
+        x = state[self._var]
+        if isinstance(x, numbers.Real):
+            x = np.r_[x]
+        x = x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
+        assert x.ndim == 1
+        self._val = x
+        return False
+
+    def info(self):
+        if self._val.size == 1:
+            return {f"Memorize[{self._var}]": float(self._val.max())}
+        return {f"Memorize[{self._var}]_min": float(self._val.min()), f"Memorize[{self._var}]_max": float(self._val.max())}
+
+    def clear(self):
+        self._val = np.r_[0]
+
+
+class AbsError(pxa.StoppingCriterion):
+    """Stop when ||f(x)|| <= eps (stop.py:222-297)."""
+
+    def __init__(self, eps, var="x", f=None, norm=2, satisfy_all=True):
+        try:
+            assert eps > 0
+            self._eps = eps
+        except Exception:
+            raise ValueError(f"eps: expected positive threshold, got {eps}.")
+        self._var = var
+        self._f = f if (f is not None) else (lambda _: _)
+        try:
+            assert norm >= 0
+            self._norm = norm
+        except Exception:
+            raise ValueError(f"norm: expected non-negative, got {norm}.")
+        self._satisfy_all = satisfy_all
+        self._val = np.r_[0]
+
+    def stop(self, state) -> bool:
+        fx = self._f(state[self._var])
+        if isinstance(fx, numbers.Real):
+            self._val = np.abs(np.r_[fx])
+        else:
+            self._val = _rownorm(fx, self._norm)
+        rule = np.all if self._satisfy_all else np.any
+        return bool(rule(self._val <= self._eps))
+
+    def info(self):
+        if self._val.size == 1:
+            return {f"AbsError[{self._var}]": float(self._val.max())}
+        return {f"AbsError[{self._var}]_min": float(self._val.min()), f"AbsError[{self._var}]_max": float(self._val.max())}
+
+    def clear(self):
+        self._val = np.r_[0]
+
+
+class RelError(pxa.StoppingCriterion):
+    """Stop when ||f(x) - f(x_prev)|| <= eps ||f(x_prev)|| (stop.py:300-396)."""
+
+    def __init__(self, eps, var="x", f=None, norm=2, satisfy_all=True):
+        try:
+            assert eps > 0
+            self._eps = eps
+        except Exception:
+            raise ValueError(f"eps: expected positive threshold, got {eps}.")
+        self._var = var
+        self._f = f if (f is not None) else (lambda _: _)
+        try:
+            assert norm >= 0
+            self._norm = norm
+        except Exception:
+            raise ValueError(f"norm: expected non-negative, got {norm}.")
+        self._satisfy_all = satisfy_all
+        self._val = np.r_[0]
+        self._x_prev = None
+
+    def stop(self, state) -> bool:
+        x = state[self._var]
+        if isinstance(x, numbers.Real):
+            raise NotImplementedError("pyxu_amd: RelError on scalar state variables is not supported.")
+        if self._x_prev is None:
+            self._x_prev = _dev.copy(x)
+            self._val = np.zeros(shape=(1,) if (x.ndim == 1) else tuple(x.shape[:-1]))
+            return False
+        fx_prev = self._f(self._x_prev)
+        fx = self._f(x)
+        if self._norm == 2:
+            a = fx.reshape(-1, fx.shape[-1])
+            b = fx_prev.reshape(-1, fx_prev.shape[-1])
+            num = (_dev.row_reduce(_dev.RED_DIFFSQ, a, b).cpu().numpy() ** 0.5).reshape(*fx.shape[:-1], 1)
+            den = _rownorm(fx_prev, 2)
+        else:
+            num = _rownorm(_dev.axpby(1.0, fx, -1.0, fx_prev), self._norm)
+            den = _rownorm(fx_prev, self._norm)
+        rule = np.all if self._satisfy_all else np.any
+        decision = bool(rule(num <= self._eps * den))
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            self._val = num / den
+            self._val[np.isnan(self._val)] = 0
+        self._x_prev = _dev.copy(x)
+        return decision
+
+    def info(self):
+        if self._val.size == 1:
+            return {f"RelError[{self._var}]": float(self._val.max())}
+        return {f"RelError[{self._var}]_min": float(self._val.min()), f"RelError[{self._var}]_max": float(self._val.max())}
+
+    def clear(self):
+        self._val = np.r_[0]
+        self._x_prev = None

@@ -1,0 +1,213 @@
+"""CPU-only tests: C-ABI symbol table, operator algebra / Lipschitz bookkeeping, step-size rules,
+tap generation, fused-plan recognition, solver bookkeeping.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from conftest import ROOT, golden_names, load_golden
+
+import pyxu_amd
+import pyxu_amd.abc as pxa
+import pyxu_amd.operator as pxo
+import pyxu_amd.opt.solver as pxs
+import pyxu_amd.opt.stop as pxst
+import pyxu_amd.runtime as pxrt
+from pyxu_amd._lib import EXPORTS, LIB_PATH
+
+
+def _header_functions():
+    txt = open(os.path.join(ROOT, "include", "pyxu_amd.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(pxa_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    assert os.path.exists(LIB_PATH), "run __graft_entry__.build() first"
+    lib = ctypes.CDLL(LIB_PATH)
+    names = _header_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(lib, n), n
+    # the Python binding covers the whole header, and nothing else
+    assert set(names) == set(EXPORTS), set(names) ^ set(EXPORTS)
+    assert lib.pxa_abi_version() == 1
+
+
+def test_error_strings():
+    lib = pyxu_amd.lib
+    assert lib.pxa_error_string(0) == b"success"
+    assert b"invalid argument" in lib.pxa_error_string(-1)
+
+
+def test_argument_validation_without_gpu():
+    # invalid arguments are rejected on the host before any launch
+    lib = pyxu_amd.lib
+    assert lib.pxa_axpby(7, 10, 1.0, None, 0.0, None, None, None) == -2  # bad dtype
+    assert lib.pxa_row_reduce(0, 99, 1, 4, 1, None, 1, 1, None) == -1  # bad op
+    assert lib.pxa_pgd_tv2d_step(0, 1, 1, 8, 8, 0, None, None, 0, None, None, 1, 1, 0, 1, 0, 1, 0, 0, 1, 2, 3, 4, None, None) == -1
+
+
+@pytest.mark.parametrize("name", golden_names("gaussian_"))
+def test_gaussian_taps_match_reference(name):
+    g = load_golden(name)
+    with pxrt.Precision(pxrt.Width.SINGLE if g["x"].dtype == np.float32 else pxrt.Width.DOUBLE):
+        op = pxo.Gaussian(arg_shape=tuple(g["arg_shape"]), sigma=float(g["sigma"]))
+    np.testing.assert_array_equal(op.kernel[0], g["taps"])
+    from scipy.ndimage._filters import _gaussian_kernel1d
+
+    from pyxu_amd.operator.linop.filter import gaussian_kernel1d
+
+    for order in (0, 1, 2):
+        np.testing.assert_allclose(gaussian_kernel1d(1.7, order, 6), _gaussian_kernel1d(1.7, order, 6), rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", golden_names("stencil_"))
+def test_stencil_lipschitz_and_pad(name):
+    g = load_golden(name)
+    dt = g["x"].dtype
+    ks = [g[f"kernel{i}"] for i in range(int(g["n_kernels"]))]
+    kern = ks if bool(g["separable"]) else ks[0]
+    mode = str(g["mode"]) if g["mode"].ndim == 0 else tuple(str(s) for s in g["mode"])
+    with pxrt.Precision(pxrt.Width.SINGLE if dt == np.float32 else pxrt.Width.DOUBLE):
+        op = pxo.Stencil(arg_shape=tuple(g["arg_shape"]), kernel=kern, center=tuple(g["center"]), mode=mode)
+        assert np.isclose(float(op.lipschitz), float(g["lipschitz"]), rtol=1e-6)
+        assert op.shape == (int(np.prod(g["arg_shape"])),) * 2
+
+
+@pytest.mark.parametrize("name", golden_names("gradient_"))
+def test_gradient_lipschitz(name):
+    g = load_golden(name)
+    with pxrt.Precision(pxrt.Width.SINGLE if g["x"].dtype == np.float32 else pxrt.Width.DOUBLE):
+        op = pxo.Gradient(arg_shape=tuple(g["arg_shape"]), directions=tuple(g["directions"]), mode=str(g["mode"]),
+                          scheme=str(g["scheme"]), accuracy=int(g["accuracy"]), sampling=float(g["sampling"]))
+    assert np.isclose(float(op.lipschitz), float(g["lipschitz"]), rtol=1e-6)
+    assert op.shape == (len(g["directions"]) * int(np.prod(g["arg_shape"])), int(np.prod(g["arg_shape"])))
+    # default forward scheme (and backward) run through the one-pass fused kernel
+    if str(g["mode"]) == "constant" and (str(g["scheme"]) != "central"):
+        assert op._fused is not None
+
+
+def test_fd_taps_match_oracle():
+    from pyxu_amd.operator.linop.diff import fd_coefficients
+
+    for scheme in ("forward", "backward", "central"):
+        for acc in (1, 2, 3):
+            for dt in (np.float32, np.float64):
+                a = fd_coefficients(1, scheme, acc, 0.5, dt)
+                b = orc.fd_taps(1, scheme, acc, 0.5, dt)
+                assert a[0] == b[0] and a[2] == b[2]
+                np.testing.assert_array_equal(a[1], b[1])
+
+
+def test_operator_algebra_types():
+    torch = pytest.importorskip("torch")
+    sh = (16, 20)
+    N = 320
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        H = pxo.Gaussian(arg_shape=sh, sigma=2.0)
+        G = pxo.Gradient(arg_shape=sh)
+        y = torch.zeros(N)  # host tensor: construction only
+        data = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H
+        assert isinstance(data, pxa.QuadraticFunc)
+        assert np.isinf(data.diff_lipschitz)  # reference semantics: unknown until set
+        tv = 0.01 * pxo.L21Norm(arg_shape=(2, *sh)).moreau_envelope(0.01) * G
+        assert isinstance(tv, pxa.DiffFunc) and np.isclose(tv.diff_lipschitz, 0.01 / 0.01 * 8, rtol=1e-6)
+        f = data + tv
+        assert isinstance(f, pxa.DiffFunc) and not isinstance(f, pxa.ProxFunc)
+        assert isinstance(G.T, pxa.LinOp) and G.T.shape == (N, 2 * N)
+        assert isinstance(2 * pxo.L1Norm(dim=N), pxa.ProxFunc)
+        assert isinstance(-pxo.L1Norm(dim=N), pxa.Func) and not isinstance(-pxo.L1Norm(dim=N), pxa.ProxFunc)
+        assert isinstance(H.gram(), pxa.SelfAdjointOp)
+
+
+def test_fused_plan_recognition():
+    torch = pytest.importorskip("torch")
+    from pyxu_amd.opt.solver._fused import match_pgd_deblur
+
+    sh = (64, 48)
+    N = int(np.prod(sh))
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        y = torch.zeros(N)
+        x0 = torch.zeros(N)
+        H = pxo.Gaussian(arg_shape=sh, sigma=2.0)
+        data = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H
+        tv = 0.01 * pxo.L21Norm(arg_shape=(2, *sh)).moreau_envelope(0.02) * pxo.Gradient(arg_shape=sh)
+        p = match_pgd_deblur(data + tv, pxo.PositiveOrthant(dim=N), x0)
+        assert p is not None and p["prox"] == 1 and np.isclose(p["lam"], 0.01) and np.isclose(p["mu"], 0.02)
+        assert p["n0"] == 64 and p["n1"] == 48 and len(p["taps0"][0]) == 13
+        p = match_pgd_deblur(data, 0.3 * pxo.L1Norm(dim=N), x0)
+        assert p is not None and p["prox"] == 2 and np.isclose(p["prox_scale"], 0.3) and p["lam"] == 0.0
+        # not recognised -> generic path
+        assert match_pgd_deblur(data, pxo.L21Norm(arg_shape=(2, 32, 48)), x0) is None
+        Hs = pxo.Gaussian(arg_shape=sh, sigma=2.0, mode="symmetric")
+        assert match_pgd_deblur(0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * Hs, None, x0) is None
+        # batch-as-axis
+        B = 3
+        Hb = pxo.Gaussian(arg_shape=(B, *sh), sigma=(0, 2.0, 2.0))
+        Gb = pxo.Gradient(arg_shape=(B, *sh), directions=(1, 2))
+        fb = 0.5 * pxo.SquaredL2Norm(dim=B * N).asloss(torch.zeros(B * N)) * Hb + 0.01 * pxo.L21Norm(arg_shape=(2, B, *sh)).moreau_envelope(0.01) * Gb
+        pb = match_pgd_deblur(fb, pxo.PositiveOrthant(dim=B * N), torch.zeros(B * N))
+        assert pb is not None and pb["B"] == B
+
+
+@pytest.mark.parametrize("name", golden_names("pds_"))
+def test_pds_step_sizes_match_reference(name):
+    g = load_golden(name)
+    dt = g["x0"].dtype
+    sh = tuple(g["arg_shape"])
+    N = int(np.prod(sh))
+    torch = pytest.importorskip("torch")
+    with pxrt.Precision(pxrt.Width.SINGLE if dt == np.float32 else pxrt.Width.DOUBLE):
+        H = pxo.Gaussian(arg_shape=sh, sigma=2.0)
+        f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(torch.zeros(N)) * H
+        f.diff_lipschitz = float(g["diff_lipschitz"])
+        K = pxo.Gradient(arg_shape=sh)
+        assert np.isclose(float(K.lipschitz), float(g["K_lipschitz"]), rtol=1e-7)
+        h = 0.01 * pxo.L1Norm(dim=len(sh) * N)
+        for key, klass in (("pd3o", pxs.PD3O), ("cv", pxs.CondatVu)):
+            s = klass(f=f, h=h, K=K, show_progress=False)
+            s._tuning_strategy = 1
+            tau, sigma, delta = s._set_step_sizes(None, None, s._set_gamma(1))
+            assert tau == g[f"{key}_tau"] and sigma == g[f"{key}_sigma"], key
+            assert s._set_momentum_term(None, delta) == g[f"{key}_rho"]
+
+
+def test_stop_criteria_host_logic():
+    m = pxst.MaxIter(3)
+    assert [m.stop({}) for _ in range(4)] == [False, False, False, True]
+    m.clear()
+    assert m.info() == {"N_iter": 0}
+    c = pxst.MaxIter(1) | pxst.ManualStop()
+    assert c.stop({}) is False and c.stop({}) is True
+    with pytest.raises(ValueError):
+        pxst.MaxIter(0)
+    with pytest.raises(ValueError):
+        pxst.RelError(eps=-1)
+    with pytest.raises(ValueError):
+        pxs.PGD(f=None, g=None)
+    with pytest.raises(ValueError):
+        pxs.PGD(f=pxo.L1Norm(3), stop_rate=0)
+
+
+def test_precision_runtime():
+    assert pxrt.getPrecision() == pxrt.Width.DOUBLE
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        assert pxrt.coerce(1.5).dtype == np.float32
+        with pxrt.EnforcePrecision(False):
+            assert pxrt.coerce(1.5) == 1.5
+    assert pxrt.coerce(np.arange(3)).dtype == np.float64
+    with pytest.raises(TypeError):
+        pxrt.coerce(np.ones(2, dtype=complex))
+
+
+def test_host_arrays_are_rejected_loudly():
+    torch = pytest.importorskip("torch")
+    op = pxo.L1Norm(dim=4)
+    with pytest.raises(TypeError):
+        op.prox(np.ones(4), 0.1)
+    with pytest.raises(TypeError):
+        op.prox(torch.ones(4, dtype=torch.float64), 0.1)  # CPU tensor: no CPU compute path
