@@ -32,6 +32,13 @@ def _unscale(op):
     return op, s
 
 
+def _core(op):
+    """Undo asop()/squeeze() re-wrapping (a 1x1 operator is squeezed to a LinFunc shell)."""
+    while hasattr(op, "_core"):
+        op = op._core
+    return op
+
+
 def _data_term(f):
     """f = c * SquaredL2Norm.argshift(-y) o H  ->  (H, y, c) ; the reference's 1/2||H.-y||^2 has c=1/2."""
     if not (hasattr(f, "_lhs") and f._expr()[0] == "compose"):
@@ -44,7 +51,7 @@ def _data_term(f):
         return None
     if not np.isclose(c, 0.5):
         return None
-    return H, lhs._cst  # shift = -y
+    return _core(H), lhs._cst  # shift = -y
 
 
 def _tv_term(t):
@@ -52,7 +59,7 @@ def _tv_term(t):
     t, s_out = _unscale(t)
     if not (hasattr(t, "_lhs") and t._expr()[0] == "compose"):
         return None
-    env, G = t._lhs, t._rhs
+    env, G = t._lhs, _core(t._rhs)
     env, s_in = _unscale(env)
     if getattr(env, "_name", None) != "moreau_envelope" or not hasattr(env, "_inner"):
         return None
