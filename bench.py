@@ -24,6 +24,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+KERNEL = "pgd_tv2d_kernel"
+ALG_BYTES_PER_PIXEL = 48  # 8 reads + 4 writes of fp32 per pixel per PGD iteration
+FUSED_BYTES_PER_PIXEL = 16  # compulsory traffic of the one-launch step: x, x_prev, y read + x_new write
 
 
 def phantom(shape, rng):
@@ -58,8 +61,33 @@ def build_problem(n0, n1, seed, lam=0.01, mu=0.01, sigma=2.0):
     return f, g, y
 
 
-def cpu_baseline(n0, n1, seed, iters, lam=0.01, mu=0.01, sigma=2.0):
-    """Oracle (NumPy port of the reference path) on the host: same problem, `iters` PGD iterations."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def measured_traffic(kernel, n0, n1):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic.json,
+    written by scripts/pmc_traffic.py: (2 * FETCH_SIZE + WRITE_SIZE) * 1024, the gfx950 correction of
+    MI355X_MICROARCH.md §HBM), or None when no profile of this workload exists."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as fh:
+            tab = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    ent = tab.get(f"{kernel}@{n0}x{n1}")
+    return None if ent is None else ent.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(n0, n1, seed, budget_s, lam=0.01, mu=0.01, sigma=2.0):
+    """Oracle (NumPy restatement of the reference path) on the host: same problem; as many PGD
+    iterations as fit in about `budget_s` seconds (bounded sample; at least 2)."""
     import oracle as orc
 
     sh = (n0, n1)
@@ -74,11 +102,14 @@ def cpu_baseline(n0, n1, seed, iters, lam=0.01, mu=0.01, sigma=2.0):
     prox = lambda z, t: orc.positive_orthant_prox(z)
     tau = np.float32(1 / np.float32(1.0 + (lam / mu) * 8.0))
     x0 = np.zeros(N, dtype=np.float32)
-    orc.pgd(x0, grad, prox, tau, 1)  # warm-up (page-in, allocator)
+    t0 = time.perf_counter()
+    orc.pgd(x0, grad, prox, tau, 1)  # warm-up (page-in, allocator) and per-iteration estimate
+    t1 = time.perf_counter() - t0
+    iters = int(max(2, min(500, budget_s / max(t1, 1e-3))))
     t0 = time.perf_counter()
     orc.pgd(x0, grad, prox, tau, iters)
     dt = time.perf_counter() - t0
-    return iters / dt, dt
+    return iters / dt, iters, dt
 
 
 def main():
@@ -88,7 +119,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=2048, help="image side (configs[1]: 2048)")
     ap.add_argument("--stop-rate", type=int, default=50, help="stop-criterion evaluation rate (reference default 1)")
-    ap.add_argument("--cpu-iters", type=int, default=4, help="oracle iterations for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget in s (0 = skip)")
     ap.add_argument("--generic", action="store_true", help="disable the fused m_step (rule-by-rule HIP path)")
     args = ap.parse_args()
 
@@ -126,6 +157,8 @@ def main():
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
+        timer = _dev.LaunchTimer(window=10)
+        _dev.set_launch_timer(timer)  # HIP events around each fused-step launch, on its stream
         t0 = time.perf_counter()
         for _ in range(args.steps):
             next(gen)
@@ -133,31 +166,11 @@ def main():
         if distributed:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        _dev.set_launch_timer(None)
+        kern_ms = timer.mean_ms() if fused else None
 
         # ---- dominant-kernel duration: HIP events on the launch stream, kernel-only replay of the
         # same fused step (same buffers, same parameters) back to back.
-        stream = torch.cuda.current_stream()
-        kern_ms = None
-        alg_bytes = None
-        if fused:
-            p = slvr._plan
-            x, xp = slvr._mstate["x"], slvr._mstate["x_prev"]
-            out = _dev.empty_like(x)
-            reps = 50
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            tau = slvr._mstate["tau"]
-            for _ in range(5):
-                _dev.pgd_tv2d_step(x, xp, p["y"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
-                                   p["h0"], p["h1"], p["lam"], p["mu"], 0.9, tau, p["prox"], 0.0)
-            ev0.record(stream)
-            for _ in range(reps):
-                _dev.pgd_tv2d_step(x, xp, p["y"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
-                                   p["h0"], p["h1"], p["lam"], p["mu"], 0.9, tau, p["prox"], 0.0)
-            ev1.record(stream)
-            ev1.synchronize()
-            kern_ms = ev0.elapsed_time(ev1) / reps
-            alg_bytes = 4 * 4 * N * p["stack"]  # x, x_prev, y read + x_new write, fp32, once each
-
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -167,15 +180,22 @@ def main():
         value = world * args.steps / elapsed_max
         roof = None
         if kern_ms is not None:
+            pix = N * slvr._plan["stack"]
+            alg_bytes = ALG_BYTES_PER_PIXEL * pix  # 48 B/pixel/iteration
             achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+            traffic = measured_traffic(KERNEL, n0, n1)
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "pgd_tv2d_kernel",
-                    "kernel_ms": round(kern_ms, 5), "bytes_per_launch": alg_bytes}
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": KERNEL,
+                    "kernel_ms": round(kern_ms, 5), "launches_timed": timer.launches,
+                    "alg_bytes_per_launch": alg_bytes,
+                    "fused_compulsory_bytes_per_launch": FUSED_BYTES_PER_PIXEL * pix,
+                    "frac_vs_fused_compulsory": round(FUSED_BYTES_PER_PIXEL * pix / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         cpu = None
-        if args.cpu_iters > 0 and world == 1:
-            v, dt = cpu_baseline(n0, n1, seed=1234, iters=args.cpu_iters)
-            cpu = {"value": round(v, 4), "unit": "iterations/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle NumPy PGD, same {n0}x{n1} TV-deblur problem, {args.cpu_iters} iterations in {dt:.1f} s"}
+        if args.cpu_seconds > 0 and world == 1:
+            v, it, dt = cpu_baseline(n0, n1, seed=1234, budget_s=args.cpu_seconds)
+            cpu = {"value": round(v, 4), "unit": "image-iterations/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle/ NumPy restatement of the reference PGD path (single thread), same {n0}x{n1} "
+                             f"TV-deblur problem, {it} iterations in {dt:.1f} s on {cpu_model()}"}
         line = {
             "metric": "solver iterations/s (PGD, TV-regularised deblur)",
             "value": round(value, 2),

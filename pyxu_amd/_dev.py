@@ -34,6 +34,8 @@ def dtcode(t) -> int:
 
 def require(t, name="arr"):
     """Validate a device operand: CUDA (ROCm) tensor, float32/64, contiguous."""
+    if _TIMER is not None:  # other device work is about to be enqueued: close the timing window
+        _TIMER.interrupt()
     if not (type(t).__module__.startswith("torch") and hasattr(t, "is_cuda")):
         raise TypeError(
             f"pyxu_amd: `{name}` must be an MI355X device tensor (got {type(t).__name__}); "
@@ -51,6 +53,66 @@ def ptr(t) -> int:
 
 def stream():
     return ct.c_void_p(_torch().cuda.current_stream().cuda_stream)
+
+
+class LaunchTimer:
+    """HIP-event windows around runs of back-to-back fused solver-step launches.
+
+    Measurement hook for bench.py: while installed (``set_launch_timer``), the fused step kernels
+    open a window (start event on the launch stream = torch's current stream, which the kernel runs
+    on) and close it after ``window`` consecutive launches, or earlier when any other device work
+    (a stop-criterion reduction / copy) is about to be enqueued (``interrupt``).  ``mean_ms()`` =
+    total window time / launches inside windows = the average launch duration, measured live on
+    the timed region's own launches, with one event pair per window rather than per launch.
+    """
+
+    def __init__(self, window=10):
+        self.windows = []  # (ev0, ev1, launches)
+        self.window = max(1, int(window))
+        self._open = None
+        self._count = 0
+
+    def _event(self):
+        ev = _torch().cuda.Event(enable_timing=True)
+        ev.record(_torch().cuda.current_stream())
+        return ev
+
+    def begin(self):
+        if self._open is None:
+            self._open = self._event()
+            self._count = 0
+        return True
+
+    def end(self, _tok=None):
+        self._count += 1
+        if self._count >= self.window:
+            self.interrupt()
+
+    def interrupt(self):
+        if self._open is not None and self._count > 0:
+            self.windows.append((self._open, self._event(), self._count))
+        self._open = None
+        self._count = 0
+
+    @property
+    def launches(self):
+        return sum(c for _, _, c in self.windows)
+
+    def mean_ms(self):
+        self.interrupt()
+        if not self.windows:
+            return None
+        self.windows[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b, _ in self.windows) / self.launches
+
+
+_TIMER = None
+
+
+def set_launch_timer(timer):
+    """Install (or remove, with None) the LaunchTimer of the fused solver-step kernels."""
+    global _TIMER
+    _TIMER = timer
 
 
 def empty(shape, like):
@@ -359,6 +421,7 @@ def dense_matmat(A, X, trans):
 def pgd_tv2d_step(x, x_prev, y, x_new, stack, y_images, n0, n1, taps0, taps1, h0, h1, lam, mu, a, tau, prox, prox_w, partials=None):
     o0, k0 = taps0
     o1, k1 = taps1
+    ev = _TIMER.begin() if _TIMER is not None else None  # measurement hook (bench.py), normally None
     check(
         lib.pxa_pgd_tv2d_step(
             dtcode(x), stack, y_images, n0, n1, len(o0), i32_array(o0), f64_array(k0), len(o1), i32_array(o1), f64_array(k1),
@@ -367,4 +430,6 @@ def pgd_tv2d_step(x, x_prev, y, x_new, stack, y_images, n0, n1, taps0, taps1, h0
         ),
         "pxa_pgd_tv2d_step",
     )
+    if ev is not None:
+        _TIMER.end(ev)
     return x_new

@@ -1,16 +1,17 @@
 // Deterministic row reductions (RelError / AbsError norms, CG dot products, L1/L2 norms).
 //
 // Two launches: (1) a (blocks_per_row x rows) grid accumulates fixed chunks in double and writes
-// one partial per workgroup; (2) one thread per row sums its partials in index order.  The
-// partition depends only on (rows, n), so results are bitwise reproducible run to run.
+// one partial per workgroup; (2) one wavefront per row folds its partials (lane-strided, then a
+// fixed shuffle tree).  The partition and the combine order depend only on (rows, n), so results
+// are bitwise reproducible run to run.
 #include "common.hpp"
 
 namespace pxa {
 namespace {
 
 inline int blocks_per_row(int64_t rows, int64_t n) {
-  int64_t per = (n + 16383) / 16384;  // >= 16 K elements per workgroup
-  int64_t cap = rows > 0 ? (2048 + rows - 1) / rows : 1;
+  int64_t per = (n + 4095) / 4096;  // >= 4 K elements per workgroup
+  int64_t cap = rows > 0 ? (4096 + rows - 1) / rows : 1;  // ~16 workgroups per CU in total
   if (cap < 1) cap = 1;
   if (per > cap) per = cap;
   if (per > 1024) per = 1024;
@@ -70,12 +71,16 @@ __global__ void __launch_bounds__(kBlock) row_partial_kernel(int64_t n, int nb, 
 }
 
 template <int OP>
-__global__ void row_final_kernel(int64_t rows, int nb, const double* __restrict__ part, double* __restrict__ out) {
-  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(kBlock) row_final_kernel(int64_t rows, int nb, const double* __restrict__ part,
+                                                           double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wavefront per row
   if (r >= rows) return;
-  double acc = part[r * nb];
-  for (int k = 1; k < nb; ++k) acc = combine<OP>(acc, part[r * nb + k]);
-  out[r] = acc;
+  const double* pr = part + r * nb;
+  double acc = lane < nb ? pr[lane] : 0.0;
+  for (int k = lane + 64; k < nb; k += 64) acc = combine<OP>(acc, pr[k]);
+  acc = wave_reduce<OP>(acc);
+  if (lane == 0) out[r] = acc;
 }
 
 template <typename T, int OP>
@@ -87,8 +92,9 @@ int launch_reduce(int64_t rows, int64_t n, const void* x, const void* y, double*
                      (const T*)y, part);
   int e = last_launch_status();
   if (e) return e;
-  hipLaunchKernelGGL((row_final_kernel<OP>), dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, rows, nb, part,
-                     out);
+  const int64_t rows_per_block = kBlock / kWave;
+  hipLaunchKernelGGL((row_final_kernel<OP>), dim3((unsigned)((rows + rows_per_block - 1) / rows_per_block)), dim3(kBlock),
+                     0, s, rows, nb, part, out);
   return last_launch_status();
 }
 

@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout
  && echo "smoke ok" \
  && timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 \
  && tail -1 gpurun_out/bench.log \
- && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run --output-format csv -- python3 bench.py --cpu-iters 0 > gpurun_out/prof_bench.log 2>&1 \
+ && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run --output-format csv -- python3 bench.py --cpu-seconds 0 > gpurun_out/prof_bench.log 2>&1 \
  && echo "prof ok"
 rc=$?
 tail -5 gpurun_out/pytest_gpu.log
