@@ -119,6 +119,10 @@ def empty(shape, like):
     return _torch().empty(shape, dtype=like.dtype, device=like.device)
 
 
+def empty_f64(shape, like):
+    return _torch().empty(shape, dtype=_torch().float64, device=like.device)
+
+
 def empty_like(t):
     return _torch().empty_like(t, memory_format=_torch().contiguous_format)
 
@@ -266,8 +270,9 @@ def group_norm(x, outer, group, inner):
 
 
 # ------------------------------------------------------------------ reductions
-def row_reduce(op, x, y=None):
-    """Per-row reduction over the last axis -> float64 device tensor of shape x.shape[:-1] (or (1,))."""
+def row_reduce(op, x, y=None, out=None):
+    """Per-row reduction over the last axis -> float64 device tensor of shape x.shape[:-1] (or (1,)).
+    `out`: optional contiguous float64 device buffer of max(rows, 1) elements to write into."""
     torch = _torch()
     x = require(x)
     n = x.shape[-1] if x.ndim > 0 else 1
@@ -275,7 +280,10 @@ def row_reduce(op, x, y=None):
     if y is not None:
         y = require(y)
         assert y.shape == x.shape
-    out = torch.empty((max(rows, 1),), dtype=torch.float64, device=x.device)
+    if out is None:
+        out = torch.empty((max(rows, 1),), dtype=torch.float64, device=x.device)
+    else:
+        assert out.dtype == torch.float64 and out.is_contiguous() and out.numel() == max(rows, 1)
     if rows == 0:
         return out.zero_()
     # rows beyond the grid-y limit are processed in slabs

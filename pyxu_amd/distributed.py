@@ -1,0 +1,176 @@
+"""
+Multi-GPU sharding of the proximal-splitting path.
+
+One process per GPU, ``torch.distributed`` with backend ``"nccl"`` (= RCCL over xGMI on MI355X);
+``"gloo"`` serves the CPU tests.  The reference has no multi-device solver (its Dask backend chunks
+arrays, ``operator/linop/stencil/stencil.py:578-606``); this module adds exactly the two exchange
+steps the hot path has, and nothing else:
+
+* **Batched independent stacks** (C5: ``(B, n0, n1)`` batch-as-axis problems).  Axis 0 is split into
+  contiguous slabs (:func:`shard_range`); the blur / gradient have size-1 taps on that axis, so a
+  slab iterates with no halo and no data-path collective.  The only exchange is the stopping
+  criterion: :class:`ShardedRelError` / :class:`ShardedAbsError` all-reduce their two device row
+  statistics (sum for L1/L2, max for Linf) once per stop check, so every rank takes the same
+  decision as the unsharded solver.  :func:`gather_slabs` assembles ``solution()`` on demand.
+* **Row-sharded dense LinOp** (C4: ADMM / CG with ``K`` of shape ``(M, N)``).  Rank r holds rows
+  ``shard_range(M)`` of K.  ``apply`` is local (the rank's slice of ``Kx``); ``adjoint`` sums the
+  ranks' partial ``K_r^T z_r`` with one all-reduce of ``(B, N)`` values.  Through the operator
+  algebra ``K.T * K`` (the CG normal-equation operator of ``QuadraticFunc.prox``,
+  ``abc/operator.py:1273-1291``) therefore costs one all-reduce per CG iteration, and the CG
+  vectors (x, r, p) and their dot products stay replicated — no further communication.
+
+Message sizes are a few doubles (stop checks) or ``4·N·B`` bytes (C4: 256 KiB per right-hand side at
+N = 65 536): latency-bound on xGMI, so RCCL's default (LL/one-shot) protocols are the right choice.
+"""
+import numpy as np
+
+import pyxu_amd.abc as pxa
+import pyxu_amd.runtime as pxrt
+from pyxu_amd.opt.stop import AbsError, RelError
+
+__all__ = [
+    "world",
+    "shard_range",
+    "allreduce",
+    "gather_slabs",
+    "ShardedRelError",
+    "ShardedAbsError",
+    "RowShardedLinOp",
+]
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist
+
+
+def world(group=None):
+    """(rank, world_size) of `group` (default group), or (0, 1) when torch.distributed is not initialised."""
+    dist = _dist()
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
+def shard_range(n, rank=None, world_size=None, group=None):
+    """Contiguous balanced block [lo, hi) of `n` items owned by `rank`: the first n % world ranks
+    own one extra item.  Deterministic, so every rank computes every other rank's range."""
+    if rank is None or world_size is None:
+        r, w = world(group)
+        rank = r if rank is None else rank
+        world_size = w if world_size is None else world_size
+    if not (0 <= rank < world_size):
+        raise ValueError(f"rank {rank} outside [0, {world_size})")
+    q, rem = divmod(int(n), int(world_size))
+    lo = rank * q + min(rank, rem)
+    return lo, lo + q + (1 if rank < rem else 0)
+
+
+def allreduce(t, op="sum", group=None):
+    """In-place all-reduce of tensor `t` over `group` (no-op on one process).  Device tensors go
+    through RCCL, host tensors through gloo; the reduction order is the library's (fixed for a
+    given world size)."""
+    rank, w = world(group)
+    if w == 1:
+        return t
+    dist = _dist()
+    ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+    if t.is_cuda and _host_backend(group):
+        h = t.cpu()  # gloo (CPU tests / several ranks sharing one card): stage through the host
+        dist.all_reduce(h, op=ops[op], group=group)
+        t.copy_(h)
+        return t
+    dist.all_reduce(t, op=ops[op], group=group)
+    return t
+
+
+def _host_backend(group=None):
+    return str(_dist().get_backend(group)).lower() == "gloo"
+
+
+def gather_slabs(x_local, n_global, group=None):
+    """All-gather of contiguous slabs along axis 0 (shard_range partition of `n_global` rows):
+    returns the full (n_global, ...) array on every rank.  Unequal slabs are padded to the largest
+    one for the collective and trimmed afterwards."""
+    import torch
+
+    rank, w = world(group)
+    if w == 1:
+        return x_local
+    sizes = [shard_range(n_global, r, w)[1] - shard_range(n_global, r, w)[0] for r in range(w)]
+    if x_local.shape[0] != sizes[rank]:
+        raise ValueError(f"rank {rank} holds {x_local.shape[0]} rows, expected {sizes[rank]}")
+    m = max(sizes)
+    buf = x_local
+    if x_local.shape[0] != m:
+        buf = torch.zeros((m, *x_local.shape[1:]), dtype=x_local.dtype, device=x_local.device)
+        buf[: x_local.shape[0]] = x_local
+    dev = buf.device
+    if buf.is_cuda and _host_backend(group):
+        buf = buf.cpu()
+    parts = [torch.empty_like(buf) for _ in range(w)]
+    _dist().all_gather(parts, buf.contiguous(), group=group)
+    return torch.cat([p[:s] for p, s in zip(parts, sizes)], dim=0).to(dev)
+
+
+class _ShardedMixin:
+    def _bind_group(self, group):
+        self._group = group
+
+    def _reduce(self, stat, op):
+        return allreduce(stat.contiguous(), op=op, group=self._group)
+
+
+class ShardedRelError(_ShardedMixin, RelError):
+    """RelError (``opt/stop.py:300-396``) of a problem whose state is split across ranks along the
+    last axis (batch-as-axis slabs): ``||x - x_prev|| / ||x_prev||`` with the norms taken over the
+    WHOLE state, i.e. the per-rank row statistics all-reduced before the ratio.  Every rank returns
+    the same decision."""
+
+    def __init__(self, eps, var="x", f=None, norm=2, satisfy_all=True, group=None):
+        super().__init__(eps=eps, var=var, f=f, norm=norm, satisfy_all=satisfy_all)
+        self._bind_group(group)
+
+
+class ShardedAbsError(_ShardedMixin, AbsError):
+    """AbsError (``opt/stop.py:222-297``) over a state split across ranks (see ShardedRelError)."""
+
+    def __init__(self, eps, var="x", f=None, norm=2, satisfy_all=True, group=None):
+        super().__init__(eps=eps, var=var, f=f, norm=norm, satisfy_all=satisfy_all)
+        self._bind_group(group)
+
+
+def RowShardedLinOp(mat_local, M, group=None, enable_warnings=True):
+    """Rank-local row block of a dense ``(M, N)`` operator K (``operator/linop/base.py:334-512``).
+
+    ``mat_local`` holds rows ``shard_range(M)`` of K on this rank's device.  The returned LinOp has
+    shape ``(M_r, N)``: ``apply(x)`` gives this rank's slice of ``K x`` (local GEMV, no
+    communication), ``adjoint(z_r)`` gives the FULL ``K^T z = sum_r K_r^T z_r`` (local GEMV + one
+    all-reduce).  Combined by the operator algebra, ``K.T * K`` is the global normal operator.
+    """
+    from pyxu_amd.operator.interop import from_source
+    from pyxu_amd.operator.linop.base import _ExplicitLinOp
+
+    rank, w = world(group)
+    lo, hi = shard_range(M, rank, w)
+    if mat_local.shape[0] != hi - lo:
+        raise ValueError(f"rank {rank}: expected rows [{lo}, {hi}) of K, got {mat_local.shape[0]} rows")
+    local = _ExplicitLinOp(pxa.LinOp, mat_local, enable_warnings=enable_warnings)
+
+    @pxrt.enforce_precision(i="arr")
+    def op_apply(_, arr):
+        return local.apply(arr)
+
+    @pxrt.enforce_precision(i="arr")
+    def op_adjoint(_, arr):
+        return allreduce(local.adjoint(arr).contiguous(), "sum", group)
+
+    op = from_source(
+        cls=pxa.LinOp,
+        shape=(hi - lo, int(mat_local.shape[1])),
+        embed=dict(_name="RowShardedLinOp", _rows=(lo, hi), _M=int(M), _group=group, _local=local),
+        apply=op_apply,
+        adjoint=op_adjoint,
+    )
+    return op

@@ -16,18 +16,35 @@ from pyxu_amd import _dev
 __all__ = ["MaxIter", "ManualStop", "MaxDuration", "Memorize", "AbsError", "RelError"]
 
 
-def _rownorm(x, norm):
-    """(..., N) device tensor -> numpy (..., 1) Ln norm over the last axis."""
-    x2 = x.reshape(-1, x.shape[-1])
-    if norm == 2:
-        v = _dev.row_reduce(_dev.RED_SUMSQ, x2).cpu().numpy() ** 0.5
-    elif norm == 1:
-        v = _dev.row_reduce(_dev.RED_ABS, x2).cpu().numpy()
-    elif norm == np.inf:
-        v = _dev.row_reduce(_dev.RED_MAXABS, x2).cpu().numpy()
-    else:
+_RED = {2: "RED_SUMSQ", 1: "RED_ABS", np.inf: "RED_MAXABS"}
+
+
+def _rowstat(x, norm, y=None, out=None):
+    """(..., N) device tensor(s) -> float64 DEVICE (rows,) row statistic of (x - y) for the Ln norm:
+    sum of squares (2), sum of |.| (1) or max |.| (inf).  Stays on the device so that sharded
+    criteria can all-reduce it before the single host sync (pyxu_amd.distributed)."""
+    if norm not in _RED:
         raise NotImplementedError(f"pyxu_amd: norm={norm} not supported on device (1, 2, inf).")
-    return v.reshape(*x.shape[:-1], 1)
+    x2 = x.reshape(-1, x.shape[-1])
+    if y is not None:
+        y2 = y.reshape(-1, y.shape[-1])
+        if norm == 2:
+            return _dev.row_reduce(_dev.RED_DIFFSQ, x2, y2, out=out)
+        x2 = _dev.axpby(1.0, x2, -1.0, y2)
+    return _dev.row_reduce(getattr(_dev, _RED[norm]), x2, out=out)
+
+
+def _finish(stat, norm):
+    """host row statistic -> Ln norm."""
+    return stat**0.5 if norm == 2 else stat
+
+
+def _rownorm(x, norm, reduce=None):
+    """(..., N) device tensor -> numpy (..., 1) Ln norm over the last axis."""
+    st = _rowstat(x, norm)
+    if reduce is not None:
+        st = reduce(st, "max" if norm == np.inf else "sum")
+    return _finish(st.cpu().numpy(), norm).reshape(*x.shape[:-1], 1)
 
 
 def _as_vec(x):
@@ -135,9 +152,12 @@ class AbsError(pxa.StoppingCriterion):
         if isinstance(fx, numbers.Real):
             self._val = np.abs(np.r_[fx])
         else:
-            self._val = _rownorm(fx, self._norm)
+            self._val = _rownorm(fx, self._norm, reduce=self._reduce)
         rule = np.all if self._satisfy_all else np.any
         return bool(rule(self._val <= self._eps))
+
+    # hook: combine a device row statistic across shards (identity on one process)
+    _reduce = None
 
     def info(self):
         if self._val.size == 1:
@@ -178,14 +198,16 @@ class RelError(pxa.StoppingCriterion):
             return False
         fx_prev = self._f(self._x_prev)
         fx = self._f(x)
-        if self._norm == 2:
-            a = fx.reshape(-1, fx.shape[-1])
-            b = fx_prev.reshape(-1, fx_prev.shape[-1])
-            num = (_dev.row_reduce(_dev.RED_DIFFSQ, a, b).cpu().numpy() ** 0.5).reshape(*fx.shape[:-1], 1)
-            den = _rownorm(fx_prev, 2)
-        else:
-            num = _rownorm(_dev.axpby(1.0, fx, -1.0, fx_prev), self._norm)
-            den = _rownorm(fx_prev, self._norm)
+        # numerator and denominator row statistics in one device tensor -> one host sync
+        rows = fx.numel() // fx.shape[-1]
+        st = _dev.empty_f64((2, max(rows, 1)), fx)
+        _rowstat(fx, self._norm, fx_prev, out=st[0])
+        _rowstat(fx_prev, self._norm, out=st[1])
+        if self._reduce is not None:
+            st = self._reduce(st, "max" if self._norm == np.inf else "sum")
+        st = _finish(st.cpu().numpy(), self._norm)
+        num = st[0].reshape(*fx.shape[:-1], 1)
+        den = st[1].reshape(*fx.shape[:-1], 1)
         rule = np.all if self._satisfy_all else np.any
         decision = bool(rule(num <= self._eps * den))
         with warnings.catch_warnings():
@@ -194,6 +216,9 @@ class RelError(pxa.StoppingCriterion):
             self._val[np.isnan(self._val)] = 0
         self._x_prev = _dev.copy(x)
         return decision
+
+    # hook: combine a device row statistic across shards (identity on one process)
+    _reduce = None
 
     def info(self):
         if self._val.size == 1:

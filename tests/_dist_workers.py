@@ -1,0 +1,190 @@
+"""
+Worker bodies of the multi-process tests (spawned by test_distributed_cpu.py / test_gpu_distributed.py).
+
+Each worker initialises torch.distributed (gloo, 127.0.0.1), runs one scenario and puts
+(rank, result-dict) on a queue.  Kept in a module of its own so torch.multiprocessing's spawn can
+import it by name.
+"""
+import os
+import sys
+import traceback
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def run(rank, world, port, scenario, q, kwargs):
+    try:
+        dist = _init(rank, world, port)
+        out = globals()[scenario](rank, world, **kwargs)
+        q.put((rank, out))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported by the parent
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+# ------------------------------------------------------------------ CPU scenarios (host logic)
+def collectives(rank, world):
+    import torch
+
+    import pyxu_amd.distributed as pd
+
+    t = torch.tensor([1.0 + rank, 10.0 * rank], dtype=torch.float64)
+    s = pd.allreduce(t.clone(), "sum").tolist()
+    m = pd.allreduce(t.clone(), "max").tolist()
+    lo, hi = pd.shard_range(5)
+    x = torch.arange(lo, hi, dtype=torch.float32).reshape(-1, 1).repeat(1, 3)
+    g = pd.gather_slabs(x, 5)
+    crit = pd.ShardedRelError(eps=1e-3)
+    r = crit._reduce(torch.tensor([[1.0], [2.0]], dtype=torch.float64), "sum").tolist()
+    return dict(sum=s, max=m, gathered=g.numpy(), crit_reduce=r)
+
+
+def batched_pgd_oracle(rank, world, B, sh, iters, eps):
+    """C5 host logic: batch-as-axis PGD, slabs of images per rank, global RelError via allreduce.
+    The per-slab arithmetic is the CPU oracle (stand-in for the HIP kernels in this CPU test)."""
+    import torch
+
+    import oracle as orc
+    import pyxu_amd.distributed as pd
+
+    rng = np.random.default_rng(11)
+    N = int(np.prod(sh))
+    ys = rng.standard_normal((B, N)).astype(np.float32)
+    lo, hi = pd.shard_range(B)
+    lam, mu = 0.02, 0.01
+    taps, c = orc.gaussian_taps(2.0, 3.0, np.float32)
+    blur = dict(arg_shape=sh, kernel=[taps, taps], center=[c, c])
+    tau = np.float32(1 / np.float32(1 + 8 * lam / mu))
+    x = np.zeros((hi - lo, N), np.float32)
+    xp = x.copy()
+    k = 0
+    stopped_at = None
+    for k in range(iters):
+        a = np.float32(k / (k + 1 + 75))
+        yk = (x - xp) * a + x
+        z = np.stack([yk[i] - tau * orc.deblur_tv_grad(yk[i], blur, ys[lo + i], lam, mu, dict(arg_shape=sh))
+                      for i in range(hi - lo)]).astype(np.float32)
+        xn = np.maximum(z, 0).astype(np.float32)
+        st = torch.tensor([float(((xn.astype(np.float64) - x) ** 2).sum()), float((x.astype(np.float64) ** 2).sum())],
+                          dtype=torch.float64)
+        pd.allreduce(st, "sum")
+        xp, x = x, xn
+        if k > 0 and st[0].item() ** 0.5 <= eps * st[1].item() ** 0.5:
+            stopped_at = k
+            break
+    full = pd.gather_slabs(torch.from_numpy(x), B).numpy()
+    return dict(x=full, stopped_at=stopped_at)
+
+
+def row_sharded_normal_cg(rank, world, M, N, iters):
+    """C4 host logic: K row-sharded; K^T K p = allreduce(K_r^T K_r p); CG on (K^T K + I/tau) with
+    replicated vectors equals the unsharded CG."""
+    import torch
+
+    import oracle as orc
+    import pyxu_amd.distributed as pd
+
+    rng = np.random.default_rng(5)
+    K = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float64)
+    b = rng.standard_normal(N)
+    lo, hi = pd.shard_range(M)
+    Kr = K[lo:hi]
+    tau = 0.7
+
+    def A(p):
+        part = torch.from_numpy((Kr.T @ (Kr @ p.T)).T.copy())
+        return pd.allreduce(part, "sum").numpy() + p / tau
+
+    x, n = orc.cg(A, b[None, :], max_iter=iters)
+    return dict(x=x, n=n)
+
+
+# ------------------------------------------------------------------ GPU scenarios (real HIP path)
+def gpu_batched_pgd(rank, world, B, sh, iters, eps):
+    """C5 on the MI355X: each rank solves its slab with the fused kernel; ShardedRelError."""
+    import torch
+
+    torch.cuda.set_device(0)
+    import pyxu_amd.distributed as pd
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.opt.solver as pxs
+    import pyxu_amd.opt.stop as pxst
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd.util import to_device, to_NUMPY
+
+    rng = np.random.default_rng(13)
+    N = int(np.prod(sh))
+    ys = rng.standard_normal((B, N)).astype(np.float32)
+    lam, mu = 0.02, 0.01
+
+    def solve(lo, hi, crit):
+        b = hi - lo
+        with pxrt.Precision(pxrt.Width.SINGLE):
+            H = pxo.Gaussian(arg_shape=(b, *sh), sigma=(0, 2.0, 2.0))
+            G = pxo.Gradient(arg_shape=(b, *sh), directions=(1, 2))
+            f = 0.5 * pxo.SquaredL2Norm(dim=b * N).asloss(to_device(ys[lo:hi].reshape(-1))) * H + \
+                lam * pxo.L21Norm(arg_shape=(2, b, *sh)).moreau_envelope(mu) * G
+            f.diff_lipschitz = 1 + 8 * lam / mu
+            s = pxs.PGD(f=f, g=pxo.PositiveOrthant(dim=b * N), show_progress=False)
+            s.fit(x0=to_device(np.zeros(b * N, np.float32)), stop_crit=pxst.MaxIter(iters) | crit)
+            assert s._plan is not None
+            _, hist = s.stats()
+            return s.solution(), int(hist["iteration"][-1])
+
+    lo, hi = pd.shard_range(B)
+    x_loc, it_sh = solve(lo, hi, pd.ShardedRelError(eps=eps))
+    x_all = to_NUMPY(pd.gather_slabs(x_loc.reshape(hi - lo, N), B))
+    out = dict(x=x_all, it=it_sh)
+    if rank == 0:  # unsharded reference run of the same batched problem
+        x_ref, it_ref = solve(0, B, pxst.RelError(eps=eps))
+        out.update(x_ref=to_NUMPY(x_ref).reshape(B, N), it_ref=it_ref)
+    return out
+
+
+def gpu_row_sharded_admm(rank, world, M, N, n_iter):
+    """C4 on the MI355X: ADMM (prox path, CG x-update) with K row-sharded vs unsharded."""
+    import torch
+
+    torch.cuda.set_device(0)
+    import pyxu_amd.abc as pxa
+    import pyxu_amd.distributed as pd
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.opt.solver as pxs
+    import pyxu_amd.opt.stop as pxst
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd.util import to_device, to_NUMPY
+
+    rng = np.random.default_rng(17)
+    K = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float32)
+    xs = np.zeros(N, np.float32)
+    xs[rng.choice(N, 8, replace=False)] = rng.standard_normal(8)
+    y = (K @ xs).astype(np.float32)
+    lam, tau = 0.05, 1.0
+    lo, hi = pd.shard_range(M)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        Ks = pd.RowShardedLinOp(to_device(K[lo:hi].copy()), M)
+        f = 0.5 * pxo.SquaredL2Norm(dim=hi - lo).asloss(to_device(y[lo:hi].copy())) * Ks
+        s = pxs.ADMM(f=f, h=lam * pxo.L1Norm(dim=N), show_progress=False)
+        s.fit(x0=to_device(np.zeros(N, np.float32)), tau=tau, stop_crit=pxst.MaxIter(n_iter))
+        out = dict(x=to_NUMPY(s.solution()))
+        if rank == 0:
+            Kf = pxa.LinOp.from_array(to_device(K))
+            f1 = 0.5 * pxo.SquaredL2Norm(dim=M).asloss(to_device(y)) * Kf
+            s1 = pxs.ADMM(f=f1, h=lam * pxo.L1Norm(dim=N), show_progress=False)
+            s1.fit(x0=to_device(np.zeros(N, np.float32)), tau=tau, stop_crit=pxst.MaxIter(n_iter))
+            out["x_ref"] = to_NUMPY(s1.solution())
+    return out

@@ -309,3 +309,21 @@ def test_fused_step_matches_generic_full_size():
             s.fit(x0=x0, stop_crit=pxst.MaxIter(3), fused=fused)
             res[fused] = to_NUMPY(s.solution())
     assert rel_err(res[True], res[False]) <= 1e-5
+
+
+def test_xp_shim_numpy_semantics():
+    """NDArrayInfo.MI355X.module(): NumPy-named functions computed by the HIP kernels."""
+    from pyxu_amd.info.deps import NDArrayInfo
+
+    xp = NDArrayInfo.MI355X.module()
+    rng = np.random.default_rng(9)
+    a = rng.standard_normal((3, 257)).astype(np.float32)
+    t = D(a)
+    np.testing.assert_array_equal(to_NUMPY(xp.fabs(t)), np.fabs(a))
+    np.testing.assert_array_equal(to_NUMPY(xp.fmax(t, 0.25)), np.fmax(a, np.float32(0.25)))
+    np.testing.assert_array_equal(to_NUMPY(xp.fmin(t, 0.25)), np.fmin(a, np.float32(0.25)))
+    np.testing.assert_array_equal(to_NUMPY(xp.clip(t, -0.5, 0.5)), np.clip(a, -0.5, 0.5))
+    for ord_ in (None, 1, np.inf):
+        ref = np.linalg.norm(a.astype(np.float64), ord=ord_, axis=-1, keepdims=True)
+        assert rel_err(to_NUMPY(xp.linalg.norm(t, ord=ord_, axis=-1, keepdims=True)), ref) <= 1e-6
+    assert NDArrayInfo.from_obj(t) is NDArrayInfo.MI355X
