@@ -221,22 +221,25 @@ int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, cons
  * PGD on  F(x) = 1/2||H x - y||^2 + lam * env_mu(L21 o Grad)(x),  G = PositiveOrthant | l1w*L1 | 0
  * (opt/solver/pgd.py:173-191 with the arithmetic of AddRule/ChainRule/ScaleRule/ArgShiftRule):
  *   yk   = x + a (x - x_prev)
- *   grad = H^T (H yk - y) + Grad^T( lam * (v - prox_{mu L21}(v)) / mu ),  v = Grad yk
+ *   grad = (H^T H) yk - H^T y + Grad^T( lam * (v - prox_{mu L21}(v)) / mu ),  v = Grad yk
  *   x_new = prox_{tau G}( yk - tau * grad )
  * H is a separable zero-boundary (mode="constant") correlation over 2 spatial axes (taps0 on axis
  * 0, taps1 on axis 1, offsets/coefs in code-generation order); Grad the forward-difference
- * Gradient (diff.py default scheme) with spacing h0, h1.  `stack` independent images, each
- * (n0, n1), contiguous; image s uses data image (s % y_images) of y (1 = one y shared by a stack of
- * initial points, stack = batch-as-axis images with their own data).  x_new must not alias x or x_prev.  If `partials` is not NULL, each
- * workgroup writes (sum (x_new-x)^2, sum x^2) for RelError into partials[2*blk..] (double) —
- * pxa_pgd_tv2d_partials_count() gives the number of workgroups.
- * prox codes: 0 none, 1 positive orthant, 2 l1 with weight prox_w.
+ * Gradient (diff.py default scheme) with spacing h0, h1.  H^T H is applied as the exact banded
+ * normal operator (interior: autocorrelation of the taps; boundary rows: the truncated sums), which
+ * equals the reference's H^T (H yk - y) up to fp rounding; `hty` = H^T y is iteration-invariant and
+ * computed once by the caller (e.g. pxa_stencil_sep with the flipped taps).  `stack` independent
+ * images, each (n0, n1), contiguous; image s uses data image (s % y_images) of hty (1 = one y shared
+ * by a stack of initial points, stack = batch-as-axis images with their own data).  x_new must not
+ * alias x or x_prev.  If `partials` is not NULL, each workgroup writes (sum (x_new-x)^2, sum x^2)
+ * for RelError into partials[2*blk..] (double) — pxa_pgd_tv2d_partials_count() gives the number of
+ * workgroups.  prox codes: 0 none, 1 positive orthant, 2 l1 with weight prox_w.
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
 int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
                       const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
-                      const void* x_prev, const void* y, void* x_new, double* partials, void* stream);
+                      const void* x_prev, const void* hty, void* x_new, double* partials, void* stream);
 
 #ifdef __cplusplus
 }

@@ -77,11 +77,14 @@ class _Lib:
                 return
             try:
                 h = ct.CDLL(LIB_PATH, mode=ct.RTLD_GLOBAL)
+                fns = {}
                 for name, (res, args) in EXPORTS.items():
                     fn = getattr(h, name)
                     fn.restype = res
                     fn.argtypes = args
+                    fns[name] = fn
                 self._handle = h
+                self.__dict__.update(fns)  # later lookups bypass __getattr__ (no lock on the hot path)
             except OSError as e:  # missing / unloadable .so
                 self._err = e
 

@@ -131,8 +131,9 @@ class Solver:
         i = 0
         while (n is None) or (i < n):
             if self._step():
-                data, _ = self.stats()
-                yield data
+                # == stats()[0]; the history concatenation of stats() is O(#records) per step and its
+                # result is discarded here (reference solver.py:378 computes and drops it)
+                yield {k: self._mstate.get(k) for k in self._astate["log_var"]}
                 i += 1
             else:
                 self._astate["mode"] = None

@@ -1,35 +1,37 @@
-// Fused PGD step for 2-D TV-regularised deblurring: one launch per solver iteration.
+// Fused PGD step for 2-D TV-regularised deblurring, normal-operator form: one launch per iteration.
 //
-//   yk     = x + a (x - x_prev)
-//   r      = H yk - y                                  (H: separable zero-boundary correlation)
-//   q_d    = lam * (v_d - prox_{mu L21}(v)_d) / mu,     v = Grad yk (forward differences)
-//   x_new  = prox_{tau G}( yk - tau (H^T r + Grad^T q) )
+//   yk     = x + a (x - x_prev)                                            (pgd.py:179-181)
+//   grad   = (G yk - b) + Grad^T q,   G = H^T H,  b = H^T y  (b precomputed once per solve)
+//   q      = lam * v / max(|v|, mu)  ==  lam (v - prox_{mu L21}(v)) / mu,  v = Grad yk
+//   x_new  = prox_{tau g}( grad * (-tau) + yk )                            (pgd.py:185-191)
 //
 // Reference dataflow: PGD.m_step (opt/solver/pgd.py:173-191) through AddRule.grad,
 // ChainRule.grad, ScaleRule.grad, ArgShiftRule.grad (abc/arithmetic.py), Stencil.apply/adjoint
-// (operator/linop/stencil/stencil.py:441-461), Gradient (operator/linop/diff.py:1113-1265),
-// moreau_envelope grad (abc/operator.py:1053-1058), L21Norm.prox (operator/func/norm.py:352-364),
+// (operator/linop/stencil/stencil.py:441-461), Gradient (operator/linop/diff.py:1113-1265), the
+// moreau_envelope gradient (abc/operator.py:1053-1058), L21Norm.prox (operator/func/norm.py:352-364),
 // PositiveOrthant.prox / L1Norm.prox.
 //
-// One workgroup owns a TY x TX output tile and recomputes its halo in LDS.  HBM traffic per
-// iteration is the compulsory 3 reads (x, x_prev, y) + 1 write (x_new) per pixel; halo re-reads
-// hit L2 (tiles are dealt so that each XCD works on a contiguous band of the image).
+// Why the normal form.  The reference evaluates H^T (H yk - y): two zero-boundary separable
+// correlations in sequence, i.e. four 1-D passes of 2R+1 taps whose halos compound (a fused tile
+// must recompute a 2R halo of H yk).  H is separable, H = H0 (x) H1, so G = H^T H = G0 (x) G1 with
+// G_a = H_a^T H_a a banded n_a x n_a matrix: in rows R <= i < n_a - R it is the Toeplitz filter
+// g[d] = sum_t k[t] k[t+d], |d| <= 2R (autocorrelation of the taps); in the R boundary rows on each
+// side the zero-boundary truncation of the inner H changes the coefficients, and those rows are
+// evaluated exactly as sum_t k[t] [0 <= i-t < n] sum_s k[s] yk[i-t+s].  G is therefore EXACTLY the
+// reference's operator (fp64 trajectories agree to 1e-16); only fp32 rounding order differs
+// (measured 1.5e-7 relative after 100 PGD iterations vs fp64, the same as the reference's own fp32
+// path).  Two passes of 4R+1 taps replace four passes of 2R+1, one LDS round trip and two barriers
+// disappear, and b = H^T y replaces y in the compulsory traffic (x, x_prev, b in; x_new out).
 //
-// Work unit = a V x V block (V = elements per 16-B vector: 4 fp32, 2 fp64).  Every separable pass
-// is a register-blocked sweep ALONG its stencil axis: a lane loads a (V+2R) x V window with
-// ds_read_b128, forms V x V outputs with packed FMAs (v_pk_fma_f32 on the V-vector), and writes
-// them TRANSPOSED, so the next pass (the other axis) again sweeps along rows of its input:
-//
-//   A   yk  row-major   rows [ty0-2R, ty0-2R+AR)   cols [tx0-CA, tx0-CA+AC)       (phase 0)
-//   P1T H0 yk  [col][row]  cols = A cols          rows [ty0-R, ty0-R+P1R)        (pass 1, A -> P1T)
-//   Rb  r = H1 P1 - y, row-major, rows = P1 rows  cols [tx0-R, tx0-R+RC)         (pass 2, P1T -> Rb, aliases A)
-//   P3T H0^T r [col][row]  cols = Rb cols         rows [ty0, ty0+TY)             (pass 3, Rb -> P3T, aliases P1T)
-//   out H1^T P3 + Grad^T q, prox                   rows [ty0, ty0+TY) cols [tx0, tx0+TX)  (pass 4)
-//   Q   q0, q1 row-major  rows [ty0-1, ty0+TY)    cols [tx0-V, tx0+TX)            (from A, beside pass 1)
-//
-// Lane orders and LDS pitches are chosen with scripts/ldsbank.py (the MI355X_MICROARCH.md §LDS
-// bank model: ds_read_b128 in four 16-lane groups on 64 banks, ds_write_b128 in 8-lane groups on
-// 32 banks); for R = 6 every pass except pass 1 (+35 %) and the Q pass is at its conflict-free cost.
+// One 256-thread workgroup owns a TY x TX output tile:
+//   phase 0  A  = yk on rows [ty0-2R, ty0+TY+2R) x cols [tx0-CA, tx0+TX+CA), zero outside the image
+//   pass A   PT = (G0 yk) on the tile rows, all A columns, stored TRANSPOSED ([col][row])   (V x V
+//                 register blocks: ds_read_b128 rows, packed FMAs, ds_write_b128 columns)
+//   pass B   out = G1 along each row (sweeps PT rows = image columns) - b + Grad^T q, prox, store;
+//                 q is evaluated on the fly from yk in A (5 x 3 stencil of yk per 4 x 2 block).
+// LDS pitches / lane orders are conflict-free for R = 6 fp32 under the MI355X_MICROARCH.md §LDS
+// bank model (scripts/ldsbank.py).  The blockIdx -> tile map is XCD-aware: each of the 8 XCDs owns a
+// contiguous band of tiles so that halo re-reads of x / x_prev hit its own L2.
 #include "common.hpp"
 
 namespace pxa {
@@ -39,58 +41,48 @@ constexpr int TY = 32;
 constexpr int TX = 64;
 constexpr int kThreads = 256;
 constexpr int kMaxR = 8;
+constexpr int kMaxG = 4 * kMaxR + 1;
+constexpr int kKT = 2 * kMaxR + 2;  // per-axis stride of the LDS tap copy (edge tiles)
 
 __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ constexpr int rup(int a, int b) { return cdiv(a, b) * b; }
-__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 template <typename T>
 struct PgdParams {
-  int64_t stack, n0, n1;
-  int64_t y_images;  // y is shared by stack entries s with equal s % y_images
+  int64_t stack, y_images;
+  int n0, n1;
   int tiles0, tiles1;
-  int64_t ntiles;  // stack * tiles0 * tiles1
-  T k0[2 * kMaxR + 1], k1[2 * kMaxR + 1];  // H taps, dense window offsets -R..R (code-gen order)
-  T g0a, g0b, g1a, g1b;                     // forward-difference taps per axis (-1/h, 1/h)
+  unsigned ntiles;
+  T k0[2 * kMaxR + 1], k1[2 * kMaxR + 1];  // H taps, dense window t = -R..R (index t + R)
+  T g0[kMaxG], g1[kMaxG];                  // interior G taps, d = -2R..2R (index d + 2R)
+  T g0a, g0b, g1a, g1b;                    // forward-difference taps per axis (-1/h, 1/h)
   T lam, mu, inv_mu, a, tau, pw;
+  int prox;  // 0 none, 1 positive orthant, 2 l1 (uniform branch)
+  bool tv;   // lam != 0 (uniform branch)
   bool vec_ok;
 };
 
 template <typename T, int R>
 struct Layout {
-  static constexpr int V = kVecN<T>;  // elements per 16-B vector
+  static constexpr int V = kVecN<T>;  // elements per 16-B vector (4 fp32, 2 fp64)
   static constexpr bool F32 = sizeof(T) == 4;
-  static constexpr int CA = rup(2 * R, V);        // A column halo, vector aligned
-  static constexpr int P1R = rup(TY + 2 * R, V);  // rows of P1 / r
-  static constexpr int AR = P1R + 2 * R, AC = TX + 2 * CA;
-  static constexpr int RC = TX + CA;  // == rup(TX + 2R, V)
-  static constexpr int QR = TY + 1, QC = TX + V;
-  // V x V item grids
-  static constexpr int NGA = AC / V;                       // phase 0: AR x NGA vectors
-  static constexpr int NRG1 = P1R / V, NCG1 = AC / V;      // pass 1
-  static constexpr int NSG2 = RC / V;                      // pass 2: NRG1 x NSG2
-  static constexpr int NRG3 = TY / V, NCG3 = RC / V;       // pass 3
-  static constexpr int NSG4 = TX / V;                      // pass 4: NRG3 x NSG4
-  static constexpr int NQG = QC / V;                       // Q: QR x NQG vectors
-  static constexpr int N0 = AR * NGA, N1 = NRG1 * NCG1, N3 = NRG3 * NCG3, N4 = NRG3 * NSG4, NQ = QR * NQG;
-  static constexpr int N2P = rup(NRG1, 4) * rup(NSG2, 4);  // pass 2 uses padded 4 x 4 lane blocks
-  // pitches (elements): fp32 residues from the bank model, fp64 dense
-  static constexpr int pad(int w, int m, int res) {
+  static constexpr int CA = rup(2 * R, V);  // A column halo (vector aligned)
+  static constexpr int AR = TY + 4 * R;     // A rows
+  static constexpr int AC = TX + 2 * CA;    // A columns = PT rows
+  static constexpr int NGA = AC / V;        // phase 0: AR x NGA vectors
+  static constexpr int NA = TY / V;         // row groups (pass A and pass B)
+  static constexpr int NB = AC / V;         // pass A column groups
+  static constexpr int CW = F32 ? 2 : 1;    // pass B: output columns per item
+  static constexpr int NCB = TX / CW;       // pass B column items
+  static constexpr int pad_to(int w, int m, int res) {
     int p = w;
-    while ((p % m) != res) p += V;
+    while (F32 && (p % m) != res) p += V;
     return p;
   }
-  static constexpr int AP = AC;  // ≡ 12 (mod 16) would make pass 1 conflict-free but costs a WG/CU
-  static constexpr int PT = F32 ? pad(P1R, 8, 4) : P1R;
-  static constexpr int RP = F32 ? pad(RC, 16, 12) : RC;
-  static constexpr int P3P = F32 ? pad(TY, 8, 4) : TY;
-  static constexpr int QP = F32 ? pad(QC, 16, 4) : QC;
-  static constexpr int E_A = cmax(AR * AP, P1R * RP);
-  static constexpr int E_T = cmax(AC * PT, RC * P3P);
-  static constexpr int E_Q = 2 * QR * QP;
-  // (the partial-sum scratch reuses Tb after the last pass).  NB: gfx950 allocates LDS in 2 KiB
-  // granules per workgroup: 3 workgroups/CU need <= 52 KiB, 4 need <= 40 KiB.
-  static constexpr size_t BYTES = (size_t)(E_A + E_T + E_Q) * sizeof(T);
+  static constexpr int AP = pad_to(AC, 32, 28);   // A pitch (elements)
+  static constexpr int PTP = F32 ? TY + 16 : TY;  // PT pitch (elements)
+  static constexpr int N0 = AR * NGA, NPA = NA * NB, NPB = NA * NCB;
+  static constexpr size_t BYTES = (size_t)(AR * AP + AC * PTP + 2 * kKT) * sizeof(T);
 };
 
 template <typename T, int V>
@@ -104,10 +96,11 @@ __device__ inline void st_vec(T* p, const T (&v)[V]) {
   *reinterpret_cast<VT*>(p) = *reinterpret_cast<const VT*>(v);
 }
 
-// q = lam * v / max(|v|, mu)  ==  lam (v - prox_{mu L21}(v)) / mu; returns the scalar weight.
+// q-weight: lam / max(|v|, mu)  (so that q = w v = lam (v - prox_{mu L21}(v)) / mu).
 template <typename T>
 __device__ inline T tv_weight(T n2, T lam, T mu, T inv_mu) {
-  return lam / (sqrt(n2) > mu ? sqrt(n2) : mu);
+  const T n = sqrt(n2);
+  return lam / (n > mu ? n : mu);
 }
 template <>
 __device__ inline float tv_weight<float>(float n2, float lam, float mu, float inv_mu) {
@@ -117,43 +110,13 @@ __device__ inline float tv_weight<float>(float n2, float lam, float mu, float in
 
 template <typename T>
 __device__ inline T apply_prox(int prox, T z, T pw) {
-  if (prox == 1) return fmax(z, T(0));  // PositiveOrthant: clip(0, None) (v_max; finite inputs)
-  if (prox == 2) {                            // L1: sign(z) * max(|z| - pw, 0)
+  if (prox == 1) return fmax(z, T(0));  // PositiveOrthant: clip(0, None)
+  if (prox == 2) {                       // L1: sign(z) * max(|z| - pw, 0)
     T m = (z < T(0) ? -z : z) - pw;
     m = m > T(0) ? m : T(0);
     return z < T(0) ? -m : m;
   }
   return z;
-}
-
-// Lane orders (item id -> (a, b) with a the row-group-like and b the column-group-like index).
-// a4: runs of 4 consecutive a per b, blocks of 4 a-rows; a: a fastest; blk: padded 4 x 4 blocks.
-template <int NA, int NB>
-__device__ inline void ord_a4(int it, int& a, int& b) {
-  const int a0 = (it / (4 * NB)) * 4;
-  const int rem = it - a0 * NB;
-  if (NA % 4 == 0 || a0 + 4 <= NA) {
-    b = rem >> 2;
-    a = a0 + (rem & 3);
-  } else {
-    constexpr int hl = NA % 4 == 0 ? 4 : NA % 4;
-    b = rem / hl;
-    a = a0 + rem % hl;
-  }
-}
-template <int NA, int NB>
-__device__ inline void ord_a(int it, int& a, int& b) {
-  b = it / NA;
-  a = it - b * NA;
-}
-template <int NA, int NB>
-__device__ inline bool ord_blk(int it, int& a, int& b) {
-  constexpr int NBB = cdiv(NB, 4);
-  const int blk = it >> 4, l = it & 15;
-  const int ab = blk / NBB;
-  a = ab * 4 + (l & 3);
-  b = (blk - ab * NBB) * 4 + (l >> 2);
-  return a < NA && b < NB;
 }
 
 // Packed-arithmetic unit: fp32 pairs (v_pk_fma_f32), fp64 scalars.
@@ -170,88 +133,120 @@ struct Pk<float> {
   __device__ static type splat(float v) { return type{v, v}; }
 };
 
-// Sweep along the leading (stencil) axis of a [m][V]-strided source: out[i][v] = sum_j k[j] *
-// src[(i + j) * PS + v], i < V, from a (V + 2R) x V window.  FLIP reads the taps reversed (H^T).
-// The FMAs are written on explicit pairs along v so that they pack as loaded (no operand moves).
-template <typename T, int R, int PS, bool FLIP>
-__device__ inline void sweep(const T* __restrict__ src, const T* __restrict__ k, T (&acc)[kVecN<T>][kVecN<T>]) {
+// Register-blocked sweep along the leading axis of a [m][pitch PS] source: for NO outputs along the
+// sweep and one V-vector across it, out[o][v] = sum_{t=0}^{4R} g[t] src[(o + t) * PS + v].
+template <typename T, int R, int NO, int PS>
+__device__ inline void sweep(const T* __restrict__ src, const T* __restrict__ g, T (&out)[NO][kVecN<T>]) {
   constexpr int V = kVecN<T>;
   using P = typename Pk<T>::type;
-  constexpr int W = Pk<T>::W, NP = V / W;
+  constexpr int NP = V / Pk<T>::W;
   using VT = typename Vec4<T>::type;
-  P win[V + 2 * R][NP];
+  P acc[NO][NP];
 #pragma unroll
-  for (int j = 0; j < V + 2 * R; ++j) {
+  for (int o = 0; o < NO; ++o)
+#pragma unroll
+    for (int h = 0; h < NP; ++h) acc[o][h] = Pk<T>::splat(T(0));
+#pragma unroll
+  for (int j = 0; j < NO + 4 * R; ++j) {
     const VT t = *reinterpret_cast<const VT*>(src + j * PS);
-    __builtin_memcpy(&win[j][0], &t, sizeof(VT));
-  }
-  P a[V][NP];
+    P row[NP];
+    __builtin_memcpy(&row[0], &t, sizeof(VT));
 #pragma unroll
-  for (int i = 0; i < V; ++i)
+    for (int o = 0; o < NO; ++o) {
+      const int k = j - o;
+      if (k >= 0 && k <= 4 * R) {
+        const P gg = Pk<T>::splat(g[k]);
 #pragma unroll
-    for (int h = 0; h < NP; ++h) a[i][h] = Pk<T>::splat(T(0));
-#pragma unroll
-  for (int j = 0; j <= 2 * R; ++j) {
-    const P kk = Pk<T>::splat(FLIP ? k[2 * R - j] : k[j]);
-#pragma unroll
-    for (int i = 0; i < V; ++i)
-#pragma unroll
-      for (int h = 0; h < NP; ++h) a[i][h] = kk * win[i + j][h] + a[i][h];
+        for (int h = 0; h < NP; ++h) acc[o][h] = gg * row[h] + acc[o][h];
+      }
+    }
   }
 #pragma unroll
-  for (int i = 0; i < V; ++i) __builtin_memcpy(&acc[i][0], &a[i][0], sizeof(T) * V);
+  for (int o = 0; o < NO; ++o) __builtin_memcpy(&out[o][0], &acc[o][0], sizeof(T) * V);
 }
 
-// Transposed V x V store: dst[v * PD + i] = acc[i][v].
-template <typename T, int PD>
-__device__ inline void store_t(T* __restrict__ dst, const T (&acc)[kVecN<T>][kVecN<T>]) {
+// Boundary rows of G along one axis, as a correction of the Toeplitz sweep.  The sweep evaluates
+// sum_p k[i-p] (H y)[p] over ALL p, i.e. including the R "ghost" positions p outside [0, n) where the
+// zero-padded H y is still non-zero; the exact G = H^T H only sums p inside [0, n), so
+//   (G y)[i] = sweep[i] - sum_{ghost p, |i - p| <= R} k[i - p] (H y)[p].
+// acc[o][v]: NO outputs along the sweep axis at positions i0 + o, one V-vector across it;
+// the V-vector of position q along the sweep axis is at src + (q - q0) * PS (zero outside [0, n));
+// k: the taps (compile-time indices), kt: the same taps in LDS (runtime indices).
+template <typename T, int R, int NO, int PS>
+__device__ inline void ghost_fix(int i0, int n, int q0, const T* __restrict__ src, const T* __restrict__ k,
+                                 const T* __restrict__ kt, T (&acc)[NO][kVecN<T>]) {
   constexpr int V = kVecN<T>;
+  using VT = typename Vec4<T>::type;
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    T col[V];
+  for (int side = 0; side < 2; ++side) {
+    const int pg = side == 0 ? -R : n;  // first ghost position on this side
+    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
+    if (!hit) continue;
+    T gh[R][V];  // (H y)[pg + m] across the vector
 #pragma unroll
-    for (int i = 0; i < V; ++i) col[i] = acc[i][v];
-    st_vec<T, V>(dst + v * PD, col);
+    for (int m = 0; m < R; ++m) {
+      const int pp = pg + m;
+#pragma unroll
+      for (int v = 0; v < V; ++v) gh[m][v] = T(0);
+      if (pp >= i0 - R && pp <= i0 + NO - 1 + R) {  // used by some output (keeps reads inside the window)
+#pragma unroll
+        for (int s = -R; s <= R; ++s) {
+          T w[V];
+          const VT t = *reinterpret_cast<const VT*>(src + (pp + s - q0) * PS);
+          __builtin_memcpy(&w[0], &t, sizeof(VT));
+#pragma unroll
+          for (int v = 0; v < V; ++v) gh[m][v] = k[s + R] * w[v] + gh[m][v];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = i0 + o;
+      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        const int t = i - (pg + m);
+        if (t < -R || t > R) continue;
+        const T kk = kt[t + R];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[o][v] = acc[o][v] - kk * gh[m][v];
+      }
+    }
   }
 }
 
-// Global V-vector load at an element offset whose alignment is known at compile time (MIS = the
-// offset mod V): one 16-B load, two 8-B loads (fp32, even offset) or scalars.
-template <typename T, int MIS>
-__device__ inline void ld_row(const T* __restrict__ p, T (&v)[kVecN<T>]) {
-  constexpr int V = kVecN<T>;
-  if constexpr (MIS == 0) {
-    ld_vec<T, V>(p, v);
-  } else if constexpr (sizeof(T) == 4 && (MIS % 2) == 0) {
-    const float2 lo = *reinterpret_cast<const float2*>(p);
-    const float2 hi = *reinterpret_cast<const float2*>(p + 2);
-    v[0] = lo.x;
-    v[1] = lo.y;
-    v[2] = hi.x;
-    v[3] = hi.y;
+// Global V-vector load at an element offset whose alignment is known at compile time.
+template <typename T>
+__device__ inline void ld_pair(const T* __restrict__ p, T (&v)[2]) {
+  if constexpr (sizeof(T) == 4) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    v[0] = t.x;
+    v[1] = t.y;
   } else {
-#pragma unroll
-    for (int i = 0; i < V; ++i) v[i] = p[i];
+    v[0] = p[0];
+    v[1] = p[1];
   }
 }
 
-template <typename T, int R, bool TV, int PROX, bool EDGE>
-__device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, int64_t tile, int ty0, int tx0,
-                                const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ ys,
+template <typename T, int R, bool EDGE>
+__device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
+                                const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
                                 T* __restrict__ xns, double* __restrict__ partials) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
-  T* A = reinterpret_cast<T*>(smem);   // yk, later Rb
-  T* Tb = A + L::E_A;                  // P1T, later P3T
-  T* Q0 = Tb + L::E_T;
-  T* Q1 = Q0 + L::QR * L::QP;
-  double* red = reinterpret_cast<double*>(Tb);
-  T* Rb = A;
-  const int n0 = (int)p.n0, n1 = (int)p.n1;
+  constexpr int CW = L::CW;
+  T* A = reinterpret_cast<T*>(smem);
+  T* PT = A + L::AR * L::AP;
+  T* KT = PT + L::AC * L::PTP;  // H taps for runtime-indexed reads (boundary corrections)
+  const int n0 = p.n0, n1 = p.n1;
   const int tid = threadIdx.x;
+  if (EDGE && tid < 2 * R + 1) {
+    KT[tid] = p.k0[tid];
+    KT[kKT + tid] = p.k1[tid];
+  }
 
-  // ---- phase 0: yk = (x - x_prev) * a + x on A, zero outside the image  (pgd.py:179-181)
+  // ---- phase 0: yk = (x - x_prev) * a + x on A, zero outside the image
   constexpr int K0 = cdiv(L::N0, kThreads);
 #pragma unroll
   for (int k = 0; k < K0; ++k) {
@@ -284,191 +279,138 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, int6
       st_vec<T, V>(A + r * L::AP + V * g, out);
     }
   }
-
-  // prefetch y for pass 2 (global latency overlaps the Q / pass-1 phase)
-  constexpr int K2 = cdiv(L::N2P, kThreads);
-  T yv[K2][V][V];
-#pragma unroll
-  for (int k = 0; k < K2; ++k) {
-    int a, b;
-    const bool ok = ord_blk<L::NRG1, L::NSG2>(tid + k * kThreads, a, b) && (tid + k * kThreads < L::N2P);
-#pragma unroll
-    for (int u = 0; u < V; ++u) {
-      const int gr = ty0 - R + V * a + u, gc = tx0 - R + V * b;
-      if (!EDGE) {
-        if (ok) ld_row<T, ((V - R % V) % V)>(ys + (unsigned)(gr * n1 + gc), yv[k][u]);
-      } else {
-#pragma unroll
-        for (int c = 0; c < V; ++c) {
-          const bool in = ok && gr >= 0 && gr < n0 && gc + c >= 0 && gc + c < n1;
-          yv[k][u][c] = in ? ys[(int64_t)gr * n1 + gc + c] : T(0);
-        }
-      }
-    }
-  }
   __syncthreads();
 
-  // ---- Q: Moreau-TV dual field from yk; owned yk for the final combine; pass 1 (H along axis 0)
-  if (TV) {
-    constexpr int KQ = cdiv(L::NQ, kThreads);
+  // ---- pass A: PT[col][row] = (G0 yk)[row][col] for the TY tile rows and all A columns
+  constexpr int KA = cdiv(L::NPA, kThreads);
+  const bool edge_rows = EDGE && (ty0 < R || ty0 + TY > n0 - R);
 #pragma unroll
-    for (int k = 0; k < KQ; ++k) {
-      const int it = tid + k * kThreads;
-      if (it < L::NQ) {
-        int r, g;
-        ord_a<L::QR, L::NQG>(it, r, g);
-        const int arow = r - 1 + 2 * R, acol = V * g + CA - V;
-        T y0[V], y1[V], q0[V], q1[V];
-        ld_vec<T, V>(A + arow * L::AP + acol, y0);
-        ld_vec<T, V>(A + (arow + 1) * L::AP + acol, y1);
-        const T yr = A[arow * L::AP + acol + V];
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          const T yn = v + 1 < V ? y0[v + 1] : yr;
-          const T v0 = p.g0a * y0[v] + p.g0b * y1[v];
-          const T v1 = p.g1a * y0[v] + p.g1b * yn;
-          T w = tv_weight<T>(v0 * v0 + v1 * v1, p.lam, p.mu, p.inv_mu);
-          if (EDGE) {
-            const int gr = ty0 - 1 + r, gc = tx0 - V + V * g + v;
-            if (!(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) w = T(0);
-          }
-          q0[v] = v0 * w;
-          q1[v] = v1 * w;
-        }
-        st_vec<T, V>(Q0 + r * L::QP + V * g, q0);
-        st_vec<T, V>(Q1 + r * L::QP + V * g, q1);
-      }
-    }
-  }
-  constexpr int K4 = cdiv(L::N4, kThreads);
-  T ykown[K4][V][V];
-#pragma unroll
-  for (int k = 0; k < K4; ++k) {
+  for (int k = 0; k < KA; ++k) {
     const int it = tid + k * kThreads;
-    if (it < L::N4) {
-      int a, b;
-      ord_a<L::NRG3, L::NSG4>(it, a, b);
-#pragma unroll
-      for (int u = 0; u < V; ++u) ld_vec<T, V>(A + (V * a + u + 2 * R) * L::AP + CA + V * b, ykown[k][u]);
-    }
-  }
-  constexpr int K1 = cdiv(L::N1, kThreads);
-#pragma unroll
-  for (int k = 0; k < K1; ++k) {
-    const int it = tid + k * kThreads;
-    if (it < L::N1) {
-      int a, b;
-      ord_a4<L::NRG1, L::NCG1>(it, a, b);
+    if (it < L::NPA) {
+      const int a = it % L::NA, b = it / L::NA;  // row group fastest (conflict-free reads/writes)
       T acc[V][V];
-      sweep<T, R, L::AP, false>(A + (V * a) * L::AP + V * b, p.k0, acc);
-      store_t<T, L::PT>(Tb + (V * b) * L::PT + V * a, acc);
-    }
-  }
-  __syncthreads();
-
-  // ---- pass 2: H along axis 1, minus y, zero outside the image: P1T -> Rb (row-major)
+      sweep<T, R, V, L::AP>(A + (V * a) * L::AP + V * b, p.g0, acc);
+      if (edge_rows) ghost_fix<T, R, V, L::AP>(ty0 + V * a, n0, ty0 - 2 * R, A + V * b, p.k0, KT, acc);
 #pragma unroll
-  for (int k = 0; k < K2; ++k) {
-    const int it = tid + k * kThreads;
-    int a, b;
-    if (it < L::N2P && ord_blk<L::NRG1, L::NSG2>(it, a, b)) {
-      T acc[V][V];  // acc[c][u]: column c of the segment, row u of the group
-      sweep<T, R, L::PT, false>(Tb + (V * b + CA - 2 * R) * L::PT + V * a, p.k1, acc);
+      for (int v = 0; v < V; ++v) {
+        T colv[V];
 #pragma unroll
-      for (int u = 0; u < V; ++u) {
-        T row[V];
-#pragma unroll
-        for (int c = 0; c < V; ++c) {
-          T rv = acc[c][u] - yv[k][u][c];
-          if (EDGE) {
-            const int gr = ty0 - R + V * a + u, gc = tx0 - R + V * b + c;
-            if (!(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) rv = T(0);
-          }
-          row[c] = rv;
-        }
-        st_vec<T, V>(Rb + (V * a + u) * L::RP + V * b, row);
+        for (int u = 0; u < V; ++u) colv[u] = acc[u][v];
+        st_vec<T, V>(PT + (V * b + v) * L::PTP + V * a, colv);
       }
     }
   }
   __syncthreads();
 
-  // ---- pass 3: H^T along axis 0 (flipped taps): Rb -> P3T
-  constexpr int K3 = cdiv(L::N3, kThreads);
-#pragma unroll
-  for (int k = 0; k < K3; ++k) {
-    const int it = tid + k * kThreads;
-    if (it < L::N3) {
-      int a, b;
-      ord_a<L::NRG3, L::NCG3>(it, a, b);
-      T acc[V][V];
-      sweep<T, R, L::RP, true>(Rb + (V * a) * L::RP + V * b, p.k0, acc);
-      store_t<T, L::P3P>(Tb + (V * b) * L::P3P + V * a, acc);
-    }
-  }
-  __syncthreads();
-
-  // ---- pass 4: H^T along axis 1 + Grad^T q; z = grad * (-tau) + yk; prox; store  (pgd.py:185-191)
+  // ---- pass B: G1 along rows - b + Grad^T q; z = grad * (-tau) + yk; prox; store
+  constexpr int KB = cdiv(L::NPB, kThreads);
+  const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n1 - R);
   double part_d = 0.0, part_x = 0.0;
 #pragma unroll
-  for (int k = 0; k < K4; ++k) {
+  for (int k = 0; k < KB; ++k) {
     const int it = tid + k * kThreads;
-    if (it < L::N4) {
-      int a, b;
-      ord_a<L::NRG3, L::NSG4>(it, a, b);
-      T acc[V][V];  // acc[c][u]
-      sweep<T, R, L::P3P, true>(Tb + (V * b) * L::P3P + V * a, p.k1, acc);
-      T tv[V][V];  // tv[u][c]
-      if (TV) {
-        T q0r[V + 1][V];
+    if (it < L::NPB) {
+      const int a = it % L::NA, cb = it / L::NA;
+      const int c0 = CW * cb;  // first output column of the item (tile-relative)
+      // yk window: rows V a - 1 .. V a + V (V + 2), cols c0 - 1 .. c0 + CW (CW + 2)
+      T Y[V + 2][CW + 2];
 #pragma unroll
-        for (int u = 0; u <= V; ++u) ld_vec<T, V>(Q0 + (V * a + u) * L::QP + V * b + V, q0r[u]);
+      for (int r = 0; r < V + 2; ++r) {
+        const T* arow = A + (V * a - 1 + r + 2 * R) * L::AP + CA + c0;
+        if constexpr (CW == 2) {
+          T lo[2], mid[2], hi[2];
+          ld_pair<T>(arow - 2, lo);
+          ld_pair<T>(arow, mid);
+          ld_pair<T>(arow + 2, hi);
+          Y[r][0] = lo[1];
+          Y[r][1] = mid[0];
+          Y[r][2] = mid[1];
+          Y[r][3] = hi[0];
+        } else {
 #pragma unroll
-        for (int u = 0; u < V; ++u) {
-          T lo[V], hi[V];
-          ld_vec<T, V>(Q1 + (V * a + u + 1) * L::QP + V * b, lo);
-          ld_vec<T, V>(Q1 + (V * a + u + 1) * L::QP + V * b + V, hi);
-#pragma unroll
-          for (int c = 0; c < V; ++c) {
-            const T q1m = c == 0 ? lo[V - 1] : hi[c - 1];
-            // Grad^T q: flipped 2-tap adjoints, (+1 tap at i - e_d) then (-1 tap at i), summed over d
-            const T t0 = p.g0b * q0r[u][c] + p.g0a * q0r[u + 1][c];
-            const T t1 = p.g1b * q1m + p.g1a * hi[c];
-            tv[u][c] = t0 + t1;
-          }
+          for (int c = 0; c < CW + 2; ++c) Y[r][c] = arow[c - 1];
         }
       }
+      T yc[V][CW];  // yk at the item's own pixels
+#pragma unroll
+      for (int u = 0; u < V; ++u)
+#pragma unroll
+        for (int w = 0; w < CW; ++w) yc[u][w] = Y[u + 1][w + 1];
+      T tv[V][CW];
+      if (p.tv) {
+        // q at rows V a - 1 .. V a + V - 1 (index r = 0..V), cols c0 - 1 .. c0 + CW - 1 (index c = 0..CW)
+        T q0[V + 1][CW + 1], q1[V + 1][CW + 1];
+#pragma unroll
+        for (int r = 0; r <= V; ++r)
+#pragma unroll
+          for (int c = 0; c <= CW; ++c) {
+            const T v0 = p.g0a * Y[r][c] + p.g0b * Y[r + 1][c];
+            const T v1 = p.g1a * Y[r][c] + p.g1b * Y[r][c + 1];
+            T w = tv_weight<T>(v0 * v0 + v1 * v1, p.lam, p.mu, p.inv_mu);
+            if (EDGE) {
+              const int gr = ty0 + V * a - 1 + r, gc = tx0 + c0 - 1 + c;
+              if (!(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) w = T(0);
+            }
+            q0[r][c] = v0 * w;
+            q1[r][c] = v1 * w;
+          }
+        // Grad^T q: flipped 2-tap adjoints, (+1/h tap at i - e_d) then (-1/h tap at i), summed over d
+#pragma unroll
+        for (int u = 0; u < V; ++u)
+#pragma unroll
+          for (int w = 0; w < CW; ++w) {
+            const T t0 = p.g0b * q0[u][w + 1] + p.g0a * q0[u + 1][w + 1];
+            const T t1 = p.g1b * q1[u + 1][w] + p.g1a * q1[u + 1][w + 1];
+            tv[u][w] = t0 + t1;
+          }
+      }
+      T acc[CW][V];            // acc[w][u]: column c0 + w, row V a + u
+      sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g1, acc);
+      if (edge_cols) ghost_fix<T, R, CW, L::PTP>(tx0 + c0, n1, tx0 - CA, PT + V * a, p.k1, KT + kKT, acc);
 #pragma unroll
       for (int u = 0; u < V; ++u) {
-        T out[V];
+        const int gr = ty0 + V * a + u, gc = tx0 + c0;
+        T bv[CW], xo[CW];
+        if (!EDGE) {
+          if constexpr (CW == 2) ld_pair<T>(bs + (unsigned)(gr * n1 + gc), bv);
+          else bv[0] = bs[(unsigned)(gr * n1 + gc)];
+        } else {
 #pragma unroll
-        for (int c = 0; c < V; ++c) {
-          const T gsum = TV ? acc[c][u] + tv[u][c] : acc[c][u];  // AddRule.grad: data + TV
-          T z = gsum * (-p.tau);
-          z = z + ykown[k][u][c];
-          out[c] = apply_prox<T>(PROX, z, p.pw);
+          for (int w = 0; w < CW; ++w) bv[w] = (gr < n0 && gc + w < n1) ? bs[(int64_t)gr * n1 + gc + w] : T(0);
         }
-        const int gr = ty0 + V * a + u, gc = tx0 + V * b;
+#pragma unroll
+        for (int w = 0; w < CW; ++w) {
+          T gsum = acc[w][u] - bv[w];  // G yk - H^T y
+          if (p.tv) gsum = gsum + tv[u][w];
+          T z = gsum * (-p.tau);
+          z = z + yc[u][w];
+          xo[w] = apply_prox<T>(p.prox, z, p.pw);
+        }
         if (!EDGE) {
           const unsigned off = (unsigned)(gr * n1 + gc);
-          st_vec<T, V>(xns + off, out);
+          if constexpr (CW == 2) {
+            *reinterpret_cast<float2*>(xns + off) = make_float2(xo[0], xo[1]);
+          } else {
+            xns[off] = xo[0];
+          }
           if (partials) {
-            T xv[V];
-            ld_vec<T, V>(xs + off, xv);
 #pragma unroll
-            for (int c = 0; c < V; ++c) {
-              const double dd = (double)out[c] - (double)xv[c];
+            for (int w = 0; w < CW; ++w) {
+              const T xv = xs[off + w];
+              const double dd = (double)xo[w] - (double)xv;
               part_d += dd * dd;
-              part_x += (double)xv[c] * (double)xv[c];
+              part_x += (double)xv * (double)xv;
             }
           }
         } else if (gr < n0) {
 #pragma unroll
-          for (int c = 0; c < V; ++c) {
-            if (gc + c < n1) {
-              xns[(int64_t)gr * n1 + gc + c] = out[c];
+          for (int w = 0; w < CW; ++w) {
+            if (gc + w < n1) {
+              xns[(int64_t)gr * n1 + gc + w] = xo[w];
               if (partials) {
-                const T xv = xs[(int64_t)gr * n1 + gc + c];
-                const double dd = (double)out[c] - (double)xv;
+                const T xv = xs[(int64_t)gr * n1 + gc + w];
+                const double dd = (double)xo[w] - (double)xv;
                 part_d += dd * dd;
                 part_x += (double)xv * (double)xv;
               }
@@ -484,8 +426,9 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, int6
       part_d += __shfl_down(part_d, off, 64);
       part_x += __shfl_down(part_x, off, 64);
     }
+    double* red = reinterpret_cast<double*>(smem);
     const int lane = tid & 63, w = tid >> 6;
-    __syncthreads();  // Tb (P3T) is free again
+    __syncthreads();  // A / PT are free again
     if (lane == 0) {
       red[w] = part_d;
       red[kThreads / 64 + w] = part_x;
@@ -503,73 +446,61 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, int6
   }
 }
 
-template <typename T, int R, bool TV, int PROX>
-__global__ void __launch_bounds__(kThreads) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
-                                                            const T* __restrict__ xp, const T* __restrict__ y,
+template <typename T, int R>
+__global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
+                                                            const T* __restrict__ xp, const T* __restrict__ b,
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  // XCD-aware tile order (speed only): XCD group g = b % 8 owns a contiguous band of tiles.
-  // (ntiles < 2^31 is checked on the host: 32-bit index math.)
-  const unsigned nb = (unsigned)p.ntiles;
-  const unsigned b = blockIdx.x;
-  const unsigned q8 = nb >> 3, r8 = nb & 7u, g8 = b & 7u;
-  const unsigned tile = g8 * q8 + (g8 < r8 ? g8 : r8) + (b >> 3);
+  // XCD-aware tile order (speed only): XCD group g = blockIdx % 8 owns a contiguous band of tiles.
+  const unsigned nb = p.ntiles;
+  const unsigned bid = blockIdx.x;
+  const unsigned q8 = nb >> 3, r8 = nb & 7u, g8 = bid & 7u;
+  const unsigned tile = g8 * q8 + (g8 < r8 ? g8 : r8) + (bid >> 3);
   const unsigned tpi = (unsigned)p.tiles0 * (unsigned)p.tiles1;
   const unsigned s = tile / tpi;
   const unsigned tr = tile - s * tpi;
   const unsigned trow = tr / (unsigned)p.tiles1;
   const int ty0 = (int)trow * TY, tx0 = (int)(tr - trow * (unsigned)p.tiles1) * TX;
-  const int64_t img = p.n0 * p.n1;
+  const int64_t img = (int64_t)p.n0 * p.n1;
   const T* xs = x + (int64_t)s * img;
   const T* xps = xp + (int64_t)s * img;
-  const T* ys = y + (int64_t)(s % (unsigned)p.y_images) * img;
+  const T* bs = b + (int64_t)(s % (unsigned)p.y_images) * img;
   T* xns = xn + (int64_t)s * img;
-  // interior: the whole A window lies inside the image and rows are 16-B aligned -> no bounds tests
-  const bool interior = p.vec_ok && img <= 0x7fffffff && ty0 - 2 * R >= 0 && ty0 - 2 * R + L::AR <= p.n0 && tx0 - L::CA >= 0 &&
-                        tx0 - L::CA + L::AC <= p.n1;
+  // interior: the whole A window lies inside the image (so no boundary rows / columns of G either),
+  // rows are 16-B aligned and 32-bit offsets suffice -> no bounds tests
+  const bool interior = p.vec_ok && img <= 0x7fffffff && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0 &&
+                        tx0 - L::CA >= 0 && tx0 + TX + L::CA <= p.n1;
   if (interior)
-    pgd_tile<T, R, TV, PROX, false>(p, smem_raw, tile, ty0, tx0, xs, xps, ys, xns, partials);
+    pgd_tile<T, R, false>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
   else
-    pgd_tile<T, R, TV, PROX, true>(p, smem_raw, tile, ty0, tx0, xs, xps, ys, xns, partials);
+    pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
 }
 
-template <typename T, int R, bool TV, int PROX>
-int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* y, void* xn, double* partials,
+template <typename T, int R>
+int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
                hipStream_t s) {
   using L = Layout<T, R>;
   const size_t smem = L::BYTES;
-  auto kern = pgd_tv2d_kernel<T, R, TV, PROX>;
+  auto kern = pgd_tv2d_kernel<T, R>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp,
-                     (const T*)y, (T*)xn, partials);
+  hipLaunchKernelGGL(kern, dim3(p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp, (const T*)b,
+                     (T*)xn, partials);
   return last_launch_status();
 }
 
-template <typename T, int R>
-int dispatch_flags(const PgdParams<T>& p, bool tv, int prox, const void* x, const void* xp, const void* y, void* xn,
-                   double* partials, hipStream_t s) {
-  if (tv) {
-    if (prox == 0) return launch_pgd<T, R, true, 0>(p, x, xp, y, xn, partials, s);
-    if (prox == 1) return launch_pgd<T, R, true, 1>(p, x, xp, y, xn, partials, s);
-    return launch_pgd<T, R, true, 2>(p, x, xp, y, xn, partials, s);
-  }
-  if (prox == 0) return launch_pgd<T, R, false, 0>(p, x, xp, y, xn, partials, s);
-  if (prox == 1) return launch_pgd<T, R, false, 1>(p, x, xp, y, xn, partials, s);
-  return launch_pgd<T, R, false, 2>(p, x, xp, y, xn, partials, s);
-}
-
 template <typename T>
-int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0, const double* coef0, int nt1,
-              const int32_t* off1, const double* coef1, double h0, double h1, double lam, double mu, double a,
-              double tau, int prox, double prox_w, const void* x, const void* x_prev, const void* y, void* x_new,
-              double* partials, hipStream_t s) {
+int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
+              const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1, double lam,
+              double mu, double a, double tau, int prox, double prox_w, const void* x, const void* x_prev,
+              const void* hty, void* x_new, double* partials, hipStream_t s) {
   PXA_CHECK_ARG(stack >= 1 && n0 >= 1 && n1 >= 1 && y_images >= 1 && stack % y_images == 0);
-  PXA_CHECK_ARG(x && x_prev && y && x_new);
+  PXA_CHECK_ARG(n0 <= 0x7fffffff && n1 <= 0x7fffffff);
+  PXA_CHECK_ARG(x && x_prev && hty && x_new);
   PXA_CHECK_ARG(x_new != x && x_new != x_prev);
   PXA_CHECK_ARG(prox >= 0 && prox <= 2);
   PXA_CHECK_ARG(nt0 >= 1 && nt1 >= 1 && off0 && off1 && coef0 && coef1);
@@ -580,15 +511,32 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   PgdParams<T> p;
   p.stack = stack;
   p.y_images = y_images;
-  p.n0 = n0;
-  p.n1 = n1;
+  p.n0 = (int)n0;
+  p.n1 = (int)n1;
   p.tiles0 = (int)((n0 + TY - 1) / TY);
   p.tiles1 = (int)((n1 + TX - 1) / TX);
-  p.ntiles = stack * (int64_t)p.tiles0 * p.tiles1;
-  PXA_CHECK_ARG(p.ntiles <= 0x7fffffff);
-  for (int j = 0; j <= 2 * kMaxR; ++j) p.k0[j] = p.k1[j] = T(0);
-  for (int q = 0; q < nt0; ++q) p.k0[off0[q] + R] += (T)coef0[q];
-  for (int q = 0; q < nt1; ++q) p.k1[off1[q] + R] += (T)coef1[q];
+  const int64_t ntiles = stack * (int64_t)p.tiles0 * p.tiles1;
+  PXA_CHECK_ARG(ntiles <= 0x7fffffff);
+  p.ntiles = (unsigned)ntiles;
+  // H taps as a dense window in double (code-generation order folded per offset), then G = k (*) k
+  double k0[2 * kMaxR + 1] = {0}, k1[2 * kMaxR + 1] = {0};
+  for (int q = 0; q < nt0; ++q) k0[off0[q] + R] += coef0[q];
+  for (int q = 0; q < nt1; ++q) k1[off1[q] + R] += coef1[q];
+  for (int j = 0; j < 2 * kMaxR + 1; ++j) {
+    p.k0[j] = (T)k0[j];
+    p.k1[j] = (T)k1[j];
+  }
+  for (int d = -2 * R; d <= 2 * R; ++d) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int t = -R; t <= R; ++t) {
+      if (t + d < -R || t + d > R) continue;
+      s0 += k0[t + R] * k0[t + d + R];
+      s1 += k1[t + R] * k1[t + d + R];
+    }
+    p.g0[d + 2 * R] = (T)s0;
+    p.g1[d + 2 * R] = (T)s1;
+  }
+  for (int j = 4 * R + 1; j < kMaxG; ++j) p.g0[j] = p.g1[j] = T(0);
   p.g0a = (T)(-1.0 / h0);
   p.g0b = (T)(1.0 / h0);
   p.g1a = (T)(-1.0 / h1);
@@ -600,17 +548,18 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.tau = (T)tau;
   p.pw = (T)prox_w;
   constexpr int V = kVecN<T>;
-  p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(y) && aligned16(x_new);
-  bool tv = lam != 0.0;
+  p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new);
+  p.tv = lam != 0.0;
+  p.prox = prox;
   switch (R) {
-    case 1: return dispatch_flags<T, 1>(p, tv, prox, x, x_prev, y, x_new, partials, s);
-    case 2: return dispatch_flags<T, 2>(p, tv, prox, x, x_prev, y, x_new, partials, s);
-    case 3: return dispatch_flags<T, 3>(p, tv, prox, x, x_prev, y, x_new, partials, s);
-    case 4: return dispatch_flags<T, 4>(p, tv, prox, x, x_prev, y, x_new, partials, s);
-    case 5: return dispatch_flags<T, 5>(p, tv, prox, x, x_prev, y, x_new, partials, s);
-    case 6: return dispatch_flags<T, 6>(p, tv, prox, x, x_prev, y, x_new, partials, s);
-    case 7: return dispatch_flags<T, 7>(p, tv, prox, x, x_prev, y, x_new, partials, s);
-    default: return dispatch_flags<T, 8>(p, tv, prox, x, x_prev, y, x_new, partials, s);
+    case 1: return launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s);
+    case 2: return launch_pgd<T, 2>(p, x, x_prev, hty, x_new, partials, s);
+    case 3: return launch_pgd<T, 3>(p, x, x_prev, hty, x_new, partials, s);
+    case 4: return launch_pgd<T, 4>(p, x, x_prev, hty, x_new, partials, s);
+    case 5: return launch_pgd<T, 5>(p, x, x_prev, hty, x_new, partials, s);
+    case 6: return launch_pgd<T, 6>(p, x, x_prev, hty, x_new, partials, s);
+    case 7: return launch_pgd<T, 7>(p, x, x_prev, hty, x_new, partials, s);
+    default: return launch_pgd<T, 8>(p, x, x_prev, hty, x_new, partials, s);
   }
 }
 
@@ -629,10 +578,10 @@ int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1) {
 int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
                       const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
-                      const void* x_prev, const void* y, void* x_new, double* partials, void* stream) {
+                      const void* x_prev, const void* hty, void* x_new, double* partials, void* stream) {
   PXA_DISPATCH(dtype, T,
-               return pgd_entry<T>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, a, tau, prox,
-                                   prox_w, x, x_prev, y, x_new, partials, as_stream(stream)));
+               return pgd_entry<T>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, a,
+                                   tau, prox, prox_w, x, x_prev, hty, x_new, partials, as_stream(stream)));
 }
 
 }  // extern "C"

@@ -148,5 +148,5 @@ def match_pgd_deblur(f, g, x0):
     if x0.shape[-1] != N:
         return None
     rows = int(np.prod(x0.shape[:-1])) if x0.ndim > 1 else 1
-    return dict(shift=shift, taps0=taps[0], taps1=taps[1], n0=n0, n1=n1, B=B, rows=rows, lam=lam, mu=mu, h0=h0,
+    return dict(shift=shift, H=H, taps0=taps[0], taps1=taps[1], n0=n0, n1=n1, B=B, rows=rows, lam=lam, mu=mu, h0=h0,
                 h1=h1, prox=prox, prox_scale=pw)

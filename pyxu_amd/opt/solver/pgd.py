@@ -67,8 +67,12 @@ class PGD(pxa.Solver):
         self._plan = match_pgd_deblur(self._f, self._g, x0) if fused else None
         if self._plan is not None:
             p = self._plan
-            p["y"] = _dev.axpby(-1.0, pxrt.coerce(p["shift"]))  # data y = -shift
+            y = _dev.axpby(-1.0, pxrt.coerce(p["shift"]))  # data y = -shift
+            # the fused kernel evaluates H^T (H yk - y) as (H^T H) yk - H^T y: H^T y is iteration-invariant
+            p["hty"] = _dev.copy(p["H"].adjoint(y))
             p["stack"] = p["rows"] * p["B"]
+            p["pre"] = _dev.pgd_tv2d_args(p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"], p["h1"],
+                                          p["lam"], p["mu"], p["prox"], p["prox_scale"])
             self._spare = None
 
     def m_step(self):
@@ -81,8 +85,8 @@ class PGD(pxa.Solver):
             if out is None or out is x or out is xp:
                 out = _dev.empty_like(x)
             tau = mst["tau"]
-            _dev.pgd_tv2d_step(x, xp, p["y"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
-                               p["h0"], p["h1"], p["lam"], p["mu"], a, tau, p["prox"], tau * p["prox_scale"])
+            _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
+                               p["h0"], p["h1"], p["lam"], p["mu"], a, tau, p["prox"], tau * p["prox_scale"], pre=p["pre"])
             mst["x_prev"], mst["x"] = x, out
             # recycle the old x_prev as the next output buffer iff nobody else holds it (the reference
             # allocates fresh arrays, so user-held results must never be overwritten)

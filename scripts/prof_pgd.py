@@ -22,7 +22,7 @@ with pxrt.Precision(pxrt.Width.SINGLE):
     x, xp = s._mstate["x"], s._mstate["x_prev"]
     out = _dev.empty_like(x)
     for _ in range(reps):
-        _dev.pgd_tv2d_step(x, xp, p["y"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
+        _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
                            p["h0"], p["h1"], p["lam"], p["mu"], 0.9, s._mstate["tau"], p["prox"], 0.0)
     torch.cuda.synchronize()
 print("done")

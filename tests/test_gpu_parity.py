@@ -248,6 +248,32 @@ def test_fused_pgd_edges_vs_oracle(sh, stack):
     assert rel_err(x, ref) <= 1e-5
 
 
+@pytest.mark.parametrize("sigma", [0.3, 1.0, 2.5])  # blur radius R = 1, 3, 8 (the kernel's range)
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("sh", [(7, 12), (40, 68), (70, 131)])  # n < 2R, one tile, ragged multi-tile
+def test_fused_pgd_radius_dtype_vs_oracle(sigma, dt, sh):
+    """Normal-operator kernel (H^T H yk - H^T y) incl. its boundary-row corrections, every radius."""
+    rng = np.random.default_rng(int(10 * sigma) + sh[0])
+    N = int(np.prod(sh))
+    y = rng.standard_normal(N).astype(dt)
+    x0 = rng.uniform(0, 1, N).astype(dt)
+    lam, mu = 0.05, 0.02
+    with pxrt.Precision(W(dt)):
+        H = pxo.Gaussian(arg_shape=sh, sigma=sigma)
+        f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(D(y)) * H + lam * pxo.L21Norm(arg_shape=(2, *sh)).moreau_envelope(mu) * pxo.Gradient(arg_shape=sh)
+        f.diff_lipschitz = 1 + 8 * lam / mu
+        s = pxs.PGD(f=f, g=0.01 * pxo.L1Norm(dim=N), show_progress=False)
+        s.fit(x0=D(x0), stop_crit=pxst.MaxIter(6))
+        assert s._plan is not None
+        x = to_NUMPY(s.solution())
+    taps, c = orc.gaussian_taps(sigma, 3.0, dt)
+    blur = dict(arg_shape=sh, kernel=[taps, taps], center=[c, c])
+    grad = lambda v: orc.deblur_tv_grad(v, blur, y, lam, mu, dict(arg_shape=sh))
+    tau = dt(1 / dt(f.diff_lipschitz))
+    ref, _ = orc.pgd(x0, grad, lambda z, t: orc.l1_prox(z, t * dt(0.01)), tau, 6)
+    assert rel_err(x, ref) <= (1e-5 if dt == np.float32 else 1e-12)
+
+
 def test_batch_as_axis_fused_matches_per_image():
     """(B, n0, n1) with identity taps on axis 0 and Gradient(directions=(1,2)) == B independent images."""
     rng = np.random.default_rng(7)
