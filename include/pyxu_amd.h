@@ -210,6 +210,8 @@ int pxa_gradient2_adjoint(int dtype, int64_t stack, int ndim, const int64_t* sha
  *   trans = 0 : Y (B x M) = X (B x N) A^T      (A.dot(x) per stacked row)
  *   trans = 1 : Y (B x N) = X (B x M) A        (A^T.dot(z) per stacked row)
  * A is (M x N) row-major.  `work` must hold pxa_dense_workspace_bytes(...) bytes.
+ * fp32 with B >= 2 stacked right-hand sides runs on the matrix cores (v_mfma_f32_32x32x2_f32, A
+ * streamed once, split-K partials summed in a fixed order); smaller B and fp64 use the GEMV kernels.
  * ------------------------------------------------------------------------------------------- */
 size_t pxa_dense_workspace_bytes(int dtype, int trans, int64_t M, int64_t N, int64_t B);
 int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, const void* A, const void* X, void* Y,

@@ -120,6 +120,160 @@ __global__ void __launch_bounds__(kBlock) gemv_cols_final_kernel(int64_t M, int6
   }
 }
 
+// ------------------------------------------------------------------ MFMA path (fp32, B >= kMfmaMinB)
+// Y (P x Q) = X (P x K) . op(A),  op(A)[k][q] = A[q][k] (apply: P = B, Q = M, K = N) or A[k][q]
+// (adjoint: P = B, Q = N, K = M).  From kMfmaMinB right-hand sides on, A is streamed ONCE through
+// v_mfma_f32_32x32x2_f32 (f32 in / f32 accumulate, the exact fmaf chain, 157 TF/s) instead of once per
+// kBC-chunk of GEMVs; at B >= ~40 the product turns MFMA-bound.
+//
+// Fragments (cdna_hip_programming.md §3): lane l supplies Aop[i = l & 31][k-slot h = l >> 5] and
+// Bop[k-slot h][j = l & 31]; D[i][j] lands in register r of lane l with j = l & 31,
+// i = (r & 3) + 8 (r >> 2) + 4 h.  K advances 16 at a time: MFMA s (0..7) feeds lane half h with
+// k = k0 + 8 h + s, so a lane reads 8 CONSECUTIVE k of its X row (two 16-B loads) and, in the apply,
+// of its A row (two more); the adjoint's A operand is read along q, coalesced across the 32 lanes.
+// A wave owns a (32 PTL) x 32 output block, a 256-thread workgroup four of them along Q (32 PTL x
+// 128).  When the P x Q tiles alone cannot fill the chip, K is split over grid.z; the partial slabs
+// are summed in a fixed order by a second kernel (deterministic run to run).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kMfmaMinB = 2;
+constexpr int kMfmaQ = 128;  // output columns per workgroup
+
+// Operand fragments of one 16-deep k block (zero outside [0, P) x [kb, ke) x [0, Q)).
+template <bool TRANS, int PTL>
+__device__ inline void load_block(int64_t k0, int64_t ke, int64_t P, int64_t Q, int64_t K, int64_t p0, int64_t q,
+                                  bool qok, int h, int r32, bool vec, const float* __restrict__ X,
+                                  const float* __restrict__ A, float (&a)[PTL][8], float (&b)[8]) {
+  const int64_t kk = k0 + 8 * h;
+  const bool full = vec && kk + 8 <= ke;
+#pragma unroll
+  for (int t = 0; t < PTL; ++t) {
+    const int64_t row = p0 + 32 * t + r32;
+    const float* xr = X + row * K + kk;
+    if (row < P && full) {
+      const float4 lo = *reinterpret_cast<const float4*>(xr);
+      const float4 hi = *reinterpret_cast<const float4*>(xr + 4);
+      a[t][0] = lo.x; a[t][1] = lo.y; a[t][2] = lo.z; a[t][3] = lo.w;
+      a[t][4] = hi.x; a[t][5] = hi.y; a[t][6] = hi.z; a[t][7] = hi.w;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) a[t][s] = (row < P && kk + s < ke) ? xr[s] : 0.f;
+    }
+  }
+  if (!TRANS) {
+    const float* ar = A + q * K + kk;
+    if (qok && full) {
+      const float4 lo = *reinterpret_cast<const float4*>(ar);
+      const float4 hi = *reinterpret_cast<const float4*>(ar + 4);
+      b[0] = lo.x; b[1] = lo.y; b[2] = lo.z; b[3] = lo.w;
+      b[4] = hi.x; b[5] = hi.y; b[6] = hi.z; b[7] = hi.w;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) b[s] = (qok && kk + s < ke) ? ar[s] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) b[s] = (qok && kk + s < ke) ? A[(kk + s) * Q + q] : 0.f;
+  }
+}
+
+template <int PTL>
+__device__ inline void mma_block(const float (&a)[PTL][8], const float (&b)[8], f32x16 (&acc)[PTL]) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int t = 0; t < PTL; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][s], b[s], acc[t], 0, 0, 0);
+}
+
+template <bool TRANS, int PTL>
+__global__ void __launch_bounds__(256) mfma_gemm_kernel(int64_t P, int64_t Q, int64_t K, int64_t kchunk,
+                                                        const float* __restrict__ X, const float* __restrict__ A,
+                                                        float* __restrict__ Y, bool vec) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int64_t q = (int64_t)blockIdx.x * kMfmaQ + wave * 32 + r32;  // this lane's B / output column
+  const int64_t p0 = (int64_t)blockIdx.y * (32 * PTL);
+  const int64_t kb = (int64_t)blockIdx.z * kchunk;
+  const int64_t ke = kb + kchunk < K ? kb + kchunk : K;
+  const bool qok = q < Q;
+  f32x16 acc[PTL];
+#pragma unroll
+  for (int t = 0; t < PTL; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  // two named register buffers: the next block's loads are in flight while this block's MFMAs run
+  float a0[PTL][8], b0[8], a1[PTL][8], b1[8];
+  load_block<TRANS, PTL>(kb, ke, P, Q, K, p0, q, qok, h, r32, vec, X, A, a0, b0);
+  for (int64_t k0 = kb; k0 < ke; k0 += 32) {
+    load_block<TRANS, PTL>(k0 + 16, ke, P, Q, K, p0, q, qok, h, r32, vec, X, A, a1, b1);
+    mma_block<PTL>(a0, b0, acc);
+    if (k0 + 32 < ke) load_block<TRANS, PTL>(k0 + 32, ke, P, Q, K, p0, q, qok, h, r32, vec, X, A, a0, b0);
+    if (k0 + 16 < ke) mma_block<PTL>(a1, b1, acc);
+  }
+  float* Yz = Y + (int64_t)blockIdx.z * P * Q;
+  if (qok) {
+#pragma unroll
+    for (int t = 0; t < PTL; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = p0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < P) Yz[row * Q + q] = acc[t][r];
+      }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) splitk_sum_kernel(int64_t n, int splits, const float* __restrict__ part,
+                                                            float* __restrict__ Y) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = part[i];
+    for (int z = 1; z < splits; ++z) s += part[(int64_t)z * n + i];  // fixed order
+    Y[i] = s;
+  }
+}
+
+struct MfmaPlan {
+  int ptl;
+  int64_t gx, gy, splits, kchunk;
+};
+
+inline MfmaPlan mfma_plan(int64_t P, int64_t Q, int64_t K) {
+  MfmaPlan m;
+  m.ptl = P > 32 ? 2 : 1;
+  m.gx = (Q + kMfmaQ - 1) / kMfmaQ;
+  m.gy = (P + 32 * m.ptl - 1) / (32 * m.ptl);
+  const int64_t tiles = m.gx * m.gy;
+  int64_t splits = (1024 + tiles - 1) / tiles;  // ~4 workgroups per CU in total
+  const int64_t max_splits = (K + 255) / 256;   // keep >= 256 k per slice
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  m.kchunk = ((K + splits - 1) / splits + 15) / 16 * 16;
+  m.splits = (K + m.kchunk - 1) / m.kchunk;
+  return m;
+}
+
+template <bool TRANS>
+int launch_mfma(int64_t P, int64_t Q, int64_t K, const float* X, const float* A, float* Y, float* work,
+                hipStream_t s) {
+  const MfmaPlan m = mfma_plan(P, Q, K);
+  const bool vec = aligned16(X) && (K % 4 == 0) && (TRANS || aligned16(A));
+  float* out = m.splits > 1 ? work : Y;
+  if (m.splits > 1 && work == nullptr) return PXA_ERR_ARG;
+  dim3 grid((unsigned)m.gx, (unsigned)m.gy, (unsigned)m.splits);
+  if (m.ptl == 2)
+    hipLaunchKernelGGL((mfma_gemm_kernel<TRANS, 2>), grid, dim3(256), 0, s, P, Q, K, m.kchunk, X, A, out, vec);
+  else
+    hipLaunchKernelGGL((mfma_gemm_kernel<TRANS, 1>), grid, dim3(256), 0, s, P, Q, K, m.kchunk, X, A, out, vec);
+  int e = last_launch_status();
+  if (e || m.splits == 1) return e;
+  hipLaunchKernelGGL(splitk_sum_kernel, dim3(grid_for(P * Q)), dim3(kBlock), 0, s, P * Q, (int)m.splits, work, Y);
+  return last_launch_status();
+}
+
+inline size_t mfma_workspace_bytes(int64_t P, int64_t Q, int64_t K) {
+  const MfmaPlan m = mfma_plan(P, Q, K);
+  return m.splits > 1 ? (size_t)m.splits * (size_t)P * (size_t)Q * sizeof(float) : 0;
+}
+
 }  // namespace
 }  // namespace pxa
 
@@ -128,6 +282,8 @@ using namespace pxa;
 extern "C" {
 
 size_t pxa_dense_workspace_bytes(int dtype, int trans, int64_t M, int64_t N, int64_t B) {
+  if (dtype == PXA_F32 && B >= kMfmaMinB)
+    return trans == 0 ? mfma_workspace_bytes(B, M, N) : mfma_workspace_bytes(B, N, M);
   if (trans == 0) return 0;
   size_t es = dtype == PXA_F64 ? 8 : 4;
   int64_t chunks = (M + kRowChunk - 1) / kRowChunk;
@@ -140,6 +296,12 @@ int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, cons
   if (B == 0) return PXA_OK;
   PXA_CHECK_ARG(A != nullptr && X != nullptr && Y != nullptr);
   hipStream_t s = as_stream(stream);
+  if (dtype == PXA_F32 && B >= kMfmaMinB) {
+    PXA_CHECK_ARG(M * (int64_t)N < ((int64_t)1 << 62));
+    if (trans == 0)
+      return launch_mfma<false>(B, M, N, (const float*)X, (const float*)A, (float*)Y, (float*)work, s);
+    return launch_mfma<true>(B, N, M, (const float*)X, (const float*)A, (float*)Y, (float*)work, s);
+  }
   PXA_DISPATCH(dtype, T, {
     bool vec = aligned16(A) && aligned16(X) && (N % kVecN<T> == 0);
     if (trans == 0) {

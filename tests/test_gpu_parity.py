@@ -137,6 +137,29 @@ def test_dense_golden(name):
         assert rel_err(to_NUMPY(op.adjoint(D(g["z"]))), g["adj"]) <= OP_TOL[dt] * 10
 
 
+@pytest.mark.parametrize("B", [2, 9, 32, 33, 64])  # MFMA path: one and two 32-row tiles per wave, ragged
+@pytest.mark.parametrize("MN", [(96, 640), (300, 1030), (2048, 4096)])  # ragged Q / K, split-K
+def test_dense_mfma_vs_fp64(MN, B):
+    """fp32 matrix-core path of _ExplicitLinOp (B >= 2 stacked inputs) vs an fp64 host product.
+    fp32 sums over K terms carry ~sqrt(K) eps inherent error (SURVEY App. A #13): norm-wise 1e-5."""
+    M, N = MN
+    rng = np.random.default_rng(M + B)
+    A = rng.standard_normal((M, N)).astype(np.float32)
+    X = rng.standard_normal((B, N)).astype(np.float32)
+    Z = rng.standard_normal((B, M)).astype(np.float32)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        op = pxa.LinOp.from_array(D(A))
+        y = to_NUMPY(op.apply(D(X)))
+        z = to_NUMPY(op.adjoint(D(Z)))
+    A64 = A.astype(np.float64)
+    assert rel_err(y, X.astype(np.float64) @ A64.T) <= 1e-5
+    assert rel_err(z, Z.astype(np.float64) @ A64) <= 1e-5
+    # stacked rows are independent: row b equals the single-RHS (GEMV path) product
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        y1 = to_NUMPY(op.apply(D(X[-1])))
+    assert rel_err(y[-1], y1) <= 1e-5
+
+
 # ----------------------------------------------------------------------------- solver trajectories
 def _deblur_f(g, dt, sh, lam=None, mu=None):
     N = int(np.prod(sh))
