@@ -243,6 +243,30 @@ int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, in
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
                       const void* x_prev, const void* hty, void* x_new, double* partials, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Fused primal-dual splitting iteration (replaces PD3O.m_step, opt/solver/pds.py:747-761, algo 0, and
+ * CondatVu.m_step, pds.py:429-442, algo 1) for f = 1/2 ||S . - y||^2, K = Gradient over the D trailing
+ * axes (forward differences, zero boundary), h = lam L1 (h_kind 0, anisotropic TV) or lam L21 over
+ * the D directions (h_kind 1, isotropic TV), g given by `prox` (0 none, 1 positive orthant, 2 l1 with
+ * weight prox_w).  Three launches: axis-0 march, in-plane tile, dual update (pds3d.hip).
+ *   geom  = {stack, y_images, n0, n1, n2, D}: `stack` volumes of (n0, n1, n2) (n0 = 1, D = 2 for
+ *           images); z is (stack, D, n0, n1, n2) direction-major, direction d on axis d + 3 - D.
+ *   ntaps[3], offs[3][17], coefs[3][17]: the separable taps of S per axis (code-generation order;
+ *           axis 0 = {[0], [1.0]} when it is not blurred).
+ *   diff  = {c0[3], c1[3]}: forward-difference taps per AXIS, (K x)[i] = c0 x[i] + c1 x[i + e_a]
+ *           (-1/h, 1/h); entries of non-differentiated axes are ignored.
+ *   scal  = {tau, sigma, rho, lam, prox_w}.
+ *   PD3O : reads u, z; writes x_out = prox_g(u - tau K^T z), u_out, z_out.  x is ignored.
+ *   CV   : reads x, z; writes x_out, z_out (x_out must not alias x).  u / u_out are ignored.
+ *   hty = S^T y (y_images volumes; volume s uses s % y_images), computed once by the caller.
+ *   work_q: stack*n0*n1*n2 scratch (unused when axis 0 is not blurred), work_w: same size, required.
+ *   u_out may alias u and z_out may alias z.  nseg: axis-0 segments of the march (<= 0: 1).
+ * ------------------------------------------------------------------------------------------- */
+int pxa_pds_step(int dtype, int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs,
+                 const double* coefs, const double* diff, const double* scal, int prox, int h_kind, const void* x,
+                 const void* u, const void* z, const void* hty, void* x_out, void* u_out, void* z_out, void* work_q,
+                 void* work_w, int nseg, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

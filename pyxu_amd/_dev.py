@@ -468,3 +468,27 @@ def pgd_tv2d_step(x, x_prev, hty, x_new, stack, y_images, n0, n1, taps0, taps1, 
     if ev is not None:
         _TIMER.end(ev)
     return x_new
+
+
+_PDS_W = 17  # per-axis tap slots of pxa_pds_step (2 * 8 + 1)
+
+
+def pds_args(stack, y_images, n0, n1, n2, D, taps, c0, c1, tau, sigma, rho, lam, prox, prox_w, h_kind):
+    """Pre-built ctypes arguments of pxa_pds_step (everything but the arrays)."""
+    offs, cfs = [], []
+    for o, c in taps:
+        offs += list(o) + [0] * (_PDS_W - len(o))
+        cfs += list(c) + [0.0] * (_PDS_W - len(c))
+    return (i64_array([stack, y_images, n0, n1, n2, D]), i32_array([len(t[0]) for t in taps]), i32_array(offs),
+            f64_array(cfs), f64_array(list(c0) + list(c1)), f64_array([tau, sigma, rho, lam, prox_w]), int(prox),
+            int(h_kind))
+
+
+def pds_step(algo, pre, x, u, z, hty, x_out, u_out, z_out, work_q, work_w, nseg=0):
+    """One fused PD3O (algo 0) / Condat-Vu (algo 1) iteration (pxa_pds_step); `pre` from pds_args."""
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    ev = _TIMER.begin() if _TIMER is not None else None
+    check(lib.pxa_pds_step(dtcode(z), int(algo), *pre, p(x), p(u), p(z), p(hty), p(x_out), p(u_out), p(z_out),
+                           p(work_q), p(work_w), int(nseg), stream()), "pxa_pds_step")
+    if ev is not None:
+        _TIMER.end(ev)

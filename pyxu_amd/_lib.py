@@ -58,6 +58,10 @@ EXPORTS = {
         [i32, i64, i64, i64, i64, i32, P_i32, P_f64, i32, P_i32, P_f64, f64, f64, f64, f64, f64, f64, i32, f64,
          vp, vp, vp, vp, vp, vp],
     ),
+    "pxa_pds_step": (
+        i32,
+        [i32, i32, P_i64, P_i32, P_i32, P_f64, P_f64, P_f64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp],
+    ),
 }
 
 

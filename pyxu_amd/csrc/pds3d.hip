@@ -1,0 +1,340 @@
+// Fused primal-dual splitting iterations (PD3O, Condat-Vu) for TV-regularised deblurring of 2-D
+// images and 3-D volumes: three launches per iteration instead of the reference's ~25 array passes.
+//
+// Problem:  f = 1/2 ||S . - y||^2 with S a separable zero-boundary
+// stencil (Gaussian / Convolve / Stencil, operator/linop/stencil/stencil.py:441-461), K = Grad
+// (forward differences over the D trailing axes, diff.py:1113-1265), h = lam L1 (anisotropic TV) or
+// lam L21 over the D directions (isotropic TV), g in {None, PositiveOrthant, lam L1}.
+//
+// PD3O.m_step (opt/solver/pds.py:747-761):
+//   x      = prox_g(u - tau K^T z)                            kernel A (with the axis-0 half of G x)
+//   u_tmp  = x - tau grad f(x),  grad f(x) = G x - S^T y      kernel B (in-plane half of G x + update)
+//   w      = x + u_tmp - u ;  u = (1 - rho) u + rho u_tmp     kernel B
+//   z      = (1 - rho) z + rho fenchel_prox_h(z + sigma K w)  kernel C
+// CondatVu.m_step (pds.py:429-442):
+//   x_tmp  = prox_g(x - tau grad f(x) - tau K^T z)            kernels A (axis 0 of G x) + B
+//   w      = 2 x_tmp - x ;  x = rho x_tmp + (1 - rho) x       kernel B
+//   z      = rho fenchel_prox_h(z + sigma K w) + (1 - rho) z  kernel C
+//
+// G = S^T S is separable: G = G0 (x) G1 (x) G2 with G_a = H_a^T H_a (H_a the zero-boundary 1-D
+// correlation of axis a), so G x is evaluated as G12 (G0 x):
+//  * kernel A marches each pixel column along axis 0 and keeps the H0 and H0^T windows in two
+//    register rings (2 R0 + 1 planes each): the plain two-pass form, exact at the boundary planes,
+//    one HBM read of the input per voxel.  PD3O builds its input x = prox_g(u - tau K^T z) on the fly
+//    (and stores it: x is the iterate the solver returns); Condat-Vu reads x.
+//  * kernel B is the LDS-tiled in-plane normal-operator sweep of pgd_tv2d.hip (tile2d.hpp: two
+//    register-blocked 4R+1-tap passes with exact boundary-row corrections) over every plane, with the
+//    solver's point-wise update fused into its epilogue.
+//  * kernel C is the dual update: K w (one forward neighbour per direction, from cache), the Moreau
+//    form of fenchel_prox (operator.py:905-944) exactly as pxa_fenchel_prox_l1 / _l21 evaluate it,
+//    and the relaxation.
+// Compulsory HBM traffic per voxel (fp32): PD3O A 24 B + B 24 B + C 28 B = 76 B (80 B);
+// Condat-Vu A 8 B + B 32 B + C 28 B = 68 B (SURVEY: 68 B).
+//
+// Parity: the step follows the reference's arithmetic per voxel except that G x replaces
+// S^T (S x - y) + ... (same operator, different fp32 rounding order: see pgd_tv2d.hip).
+#include "pds3d.hpp"
+
+namespace pxa {
+namespace pds {
+
+// ------------------------------------------------------------------ kernel C: dual update
+template <typename T>
+struct PdsC {
+  PdsGeom<T> g;
+  T sigma, t, rho, omr;  // t = (1 / sigma) * lam, as pxa_fenchel_prox_* computes it
+  int64_t rows;          // stack * n0 * n1
+  int cblocks;           // column blocks per row
+};
+
+template <typename T>
+__device__ inline T soft_thr(T x, T tau) {  // L1Norm.prox (norm.py:47-52), as elementwise.hip
+  T m = fabs(x) - tau;
+  m = m > T(0) ? m : T(0);
+  T sg = x > T(0) ? T(1) : (x < T(0) ? T(-1) : T(0));
+  return m * sg;
+}
+
+// One thread = NV consecutive voxels of a row; workgroups stride over (row, column block) items.
+template <typename T, int NV, bool ISO, bool PD3O>
+__global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __restrict__ w,
+                                                          const T* __restrict__ z, T* __restrict__ zo) {
+  using VT = typename Vec4<T>::type;
+  const PdsGeom<T>& g = p.g;
+  const int n0 = g.n0, n1 = g.n1, n2 = g.n2, D = g.D;
+  const int64_t M = (int64_t)n1 * n2, N = M * n0;
+  const int a_first = 3 - D;
+  const int64_t items = p.rows * p.cblocks;
+  for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
+    const int64_t rowg = item / p.cblocks;
+    const int cb = (int)(item - rowg * p.cblocks);
+    const int c = (cb * kBlock + (int)threadIdx.x) * NV;
+    if (c >= n2) continue;
+    const int64_t vp = rowg / n1;  // volume-plane index s * n0 + plane
+    const int r = (int)(rowg - vp * n1);
+    const int64_t s = vp / n0;
+    const int plane = (int)(vp - s * n0);
+    const int64_t off = vp * M + (int64_t)r * n2 + c;  // in w
+    const int64_t zoff = s * (int64_t)D * N + (int64_t)plane * M + (int64_t)r * n2 + c;
+    T wc[NV];
+    if constexpr (NV == kVecN<T>)
+      *reinterpret_cast<VT*>(wc) = *reinterpret_cast<const VT*>(w + off);
+    else
+      wc[0] = w[off];
+    T zin[3][NV], zc[3][NV];
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      if (ax < a_first) continue;
+      const int d = ax - a_first;
+      T wn[NV];
+      if (ax == 2) {
+#pragma unroll
+        for (int e = 0; e + 1 < NV; ++e) wn[e] = wc[e + 1];
+        wn[NV - 1] = (c + NV < n2) ? w[off + NV] : T(0);
+      } else {
+        const bool has = ax == 1 ? (r + 1 < n1) : (plane + 1 < n0);
+        const int64_t st = ax == 1 ? (int64_t)n2 : M;
+        if (has) {
+          if constexpr (NV == kVecN<T>)
+            *reinterpret_cast<VT*>(wn) = *reinterpret_cast<const VT*>(w + off + st);
+          else
+            wn[0] = w[off + st];
+        } else {
+#pragma unroll
+          for (int e = 0; e < NV; ++e) wn[e] = T(0);
+        }
+      }
+      const T* zd = z + zoff + (int64_t)d * N;
+      if constexpr (NV == kVecN<T>)
+        *reinterpret_cast<VT*>(zc[ax]) = *reinterpret_cast<const VT*>(zd);
+      else
+        zc[ax][0] = zd[0];
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        const T kw = g.c0[ax] * wc[e] + g.c1[ax] * wn[e];  // forward difference (pxa_gradient2)
+        zin[ax][e] = T(1) * zc[ax][e] + p.sigma * kw;       // z + sigma K w
+      }
+    }
+    T zt[3][NV];
+    if constexpr (ISO) {
+      // fenchel_prox of lam L21 (groups over directions): pxa_fenchel_prox_l21
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        T ss = T(0);
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+          if (ax < a_first) continue;
+          const T v = zin[ax][e] / p.sigma;
+          ss += v * v;
+        }
+        const T n = sqrt(ss);
+        const T f = T(1) - p.t / (n > p.t ? n : p.t);
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+          if (ax < a_first) continue;
+          const T pr = (zin[ax][e] / p.sigma) * f;
+          zt[ax][e] = pr * (-p.sigma) + zin[ax][e];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        if (ax < a_first) continue;
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+          const T pr = soft_thr<T>(zin[ax][e] / p.sigma, p.t);  // pxa_fenchel_prox_l1
+          zt[ax][e] = pr * (-p.sigma) + zin[ax][e];
+        }
+      }
+    }
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      if (ax < a_first) continue;
+      T zn[NV];
+#pragma unroll
+      for (int e = 0; e < NV; ++e)
+        zn[e] = PD3O ? p.omr * zc[ax][e] + p.rho * zt[ax][e] : p.rho * zt[ax][e] + p.omr * zc[ax][e];
+      T* zq = zo + zoff + (int64_t)(ax - a_first) * N;
+      if constexpr (NV == kVecN<T>)
+        *reinterpret_cast<VT*>(zq) = *reinterpret_cast<const VT*>(zn);
+      else
+        zq[0] = zn[0];
+    }
+  }
+}
+
+
+template <typename T, int NV, bool PD3O>
+int launch_c(const PdsC<T>& pc, bool iso, const void* w, const void* z, void* zo, hipStream_t st) {
+  const int64_t items = pc.rows * pc.cblocks;
+  const int grid = (int)(items < (int64_t)kMaxGrid ? items : (int64_t)kMaxGrid);
+  if (iso)
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O>), dim3(grid), dim3(kBlock), 0, st, pc, (const T*)w,
+                       (const T*)z, (T*)zo);
+  else
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O>), dim3(grid), dim3(kBlock), 0, st, pc, (const T*)w,
+                       (const T*)z, (T*)zo);
+  return last_launch_status();
+}
+
+// dense tap window (index t + R) of one axis from (offset, coefficient) lists; returns the radius or -1
+inline int tap_window(int nt, const int32_t* off, const double* coef, double (&k)[2 * kMaxR + 1]) {
+  for (double& v : k) v = 0.0;
+  int R = 0;
+  for (int q = 0; q < nt; ++q) R = abs(off[q]) > R ? abs(off[q]) : R;
+  if (R > kMaxR) return -1;
+  for (int q = 0; q < nt; ++q) k[off[q] + kMaxR] += coef[q];
+  return R;
+}
+
+template <typename T>
+int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs, const double* coefs,
+              const double* diff, const double* scal, int prox, int h_kind, const void* x, const void* u,
+              const void* z, const void* hty, void* x_out, void* u_out, void* z_out, void* work_q, void* work_w,
+              int nseg, hipStream_t st) {
+  PXA_CHECK_ARG(algo == 0 || algo == 1);
+  PXA_CHECK_ARG(geom && ntaps && offs && coefs && diff && scal);
+  const int64_t stack = geom[0], y_images = geom[1], n0 = geom[2], n1 = geom[3], n2 = geom[4], D = geom[5];
+  PXA_CHECK_ARG(stack >= 1 && y_images >= 1 && stack % y_images == 0);
+  PXA_CHECK_ARG(n0 >= 1 && n1 >= 1 && n2 >= 1 && n0 <= 0x7fffffff && n1 <= 0x7fffffff && n2 <= 0x7fffffff);
+  PXA_CHECK_ARG(D == 2 || D == 3);
+  PXA_CHECK_ARG(stack <= 65535 && n0 * n1 * n2 <= ((int64_t)1 << 40));
+  PXA_CHECK_ARG(prox >= 0 && prox <= 2 && (h_kind == 0 || h_kind == 1));
+  const bool pd3o = algo == 0;
+  PXA_CHECK_ARG(z && hty && z_out && work_w && x_out && (pd3o ? (u && u_out) : (x != nullptr)));
+  PXA_CHECK_ARG(pd3o || x_out != x);  // kernel B reads x windows (halos) while writing x_out
+  for (int a = 0; a < 3; ++a) PXA_CHECK_ARG(ntaps[a] >= 1 && ntaps[a] <= 2 * kMaxR + 1);
+  double kw[3][2 * kMaxR + 1];
+  int Ra[3];
+  for (int a = 0; a < 3; ++a) {
+    Ra[a] = tap_window(ntaps[a], offs + a * (2 * kMaxR + 1), coefs + a * (2 * kMaxR + 1), kw[a]);
+    if (Ra[a] < 0) return PXA_ERR_UNSUPPORTED;
+  }
+  // axis 0 is the identity iff its window is exactly [1] at offset 0
+  bool id0 = Ra[0] == 0 && kw[0][kMaxR] == 1.0;
+  const int R0 = id0 ? 0 : (Ra[0] > 0 ? Ra[0] : 1);
+  if (!id0) PXA_CHECK_ARG(work_q != nullptr);
+  int R = Ra[1] > Ra[2] ? Ra[1] : Ra[2];
+  if (R < 1) R = 1;
+
+  PdsGeom<T> g;
+  g.stack = stack;
+  g.y_images = y_images;
+  g.n0 = (int)n0;
+  g.n1 = (int)n1;
+  g.n2 = (int)n2;
+  g.D = (int)D;
+  for (int a = 0; a < 3; ++a) {
+    g.c0[a] = (T)diff[a];
+    g.c1[a] = (T)diff[3 + a];
+  }
+  const T tau = (T)scal[0], sigma = (T)scal[1], rho = (T)scal[2], lam = (T)scal[3], pw = (T)scal[4];
+  const T omr = (T)(1.0 - scal[2]);
+  const int64_t M = n1 * n2;
+  constexpr int V = kVecN<T>;
+
+  // ---- kernel A
+  const void* q_src = pd3o ? (const void*)x_out : x;  // kernel B's input plane stack
+  if (pd3o || !id0) {
+    PdsA<T> pa;
+    pa.g = g;
+    for (int t = 0; t < 2 * kMaxR0 + 1; ++t) pa.k0[t] = T(0);
+    for (int t = -R0; t <= R0; ++t) pa.k0[t + R0] = (T)kw[0][t + kMaxR];
+    pa.tau = tau;
+    pa.pw = pw;
+    pa.prox = prox;
+    if (nseg < 1) nseg = 1;
+    if (nseg > n0) nseg = (int)n0;
+    pa.seg = (int)((n0 + nseg - 1) / nseg);
+    nseg = (int)((n0 + pa.seg - 1) / pa.seg);
+    const void* src = pd3o ? u : x;
+    const bool np2 = (n2 % 2 == 0) && ((uintptr_t)src % (2 * sizeof(T)) == 0) &&
+                     ((uintptr_t)z % (2 * sizeof(T)) == 0) && ((uintptr_t)x_out % (2 * sizeof(T)) == 0) &&
+                     (id0 || (uintptr_t)work_q % (2 * sizeof(T)) == 0);
+    void* q = id0 ? x_out : work_q;  // R0 == 0 never writes q
+    const int e = run_a(pa, pd3o, R0, np2 ? 2 : 1, M, nseg, src, z, x_out, q, st);
+    if (e) return e;
+    if (!id0) q_src = work_q;
+  }
+
+  // ---- kernel B
+  {
+    PdsB<T> pb;
+    pb.g = g;
+    pb.tiles1 = (int)((n1 + TY - 1) / TY);
+    pb.tiles2 = (int)((n2 + TX - 1) / TX);
+    const int64_t ntiles = stack * n0 * pb.tiles1 * pb.tiles2;
+    PXA_CHECK_ARG(ntiles <= 0x7fffffff);
+    pb.ntiles = (unsigned)ntiles;
+    for (int j = 0; j < 2 * kMaxR + 1; ++j) pb.k1[j] = pb.k2[j] = T(0);
+    for (int t = -R; t <= R; ++t) {
+      pb.k1[t + R] = (T)kw[1][t + kMaxR];
+      pb.k2[t + R] = (T)kw[2][t + kMaxR];
+    }
+    for (int j = 0; j < kMaxG; ++j) pb.g1[j] = pb.g2[j] = T(0);
+    for (int d = -2 * R; d <= 2 * R; ++d) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int t = -R; t <= R; ++t) {
+        if (t + d < -R || t + d > R) continue;
+        s1 += kw[1][t + kMaxR] * kw[1][t + d + kMaxR];
+        s2 += kw[2][t + kMaxR] * kw[2][t + d + kMaxR];
+      }
+      pb.g1[d + 2 * R] = (T)s1;
+      pb.g2[d + 2 * R] = (T)s2;
+    }
+    pb.tau = tau;
+    pb.rho = rho;
+    pb.omr = omr;
+    pb.pw = pw;
+    pb.prox = prox;
+    const void* xin = pd3o ? (const void*)x_out : x;
+    void* out = pd3o ? u_out : x_out;
+    pb.vec_ok = (n2 % V == 0) && aligned16(q_src) && aligned16(xin) && aligned16(hty) && aligned16(work_w) &&
+                aligned16(out) && aligned16(z) && (!pd3o || aligned16(u));
+    PdsPtrs P{q_src, xin, u, z, hty, work_w, out};
+    const int e = run_b(pb, pd3o, R, P, st);
+    if (e) return e;
+  }
+
+  // ---- kernel C
+  {
+    PdsC<T> pc;
+    pc.g = g;
+    pc.sigma = sigma;
+    pc.t = (T(1) / sigma) * lam;
+    pc.rho = rho;
+    pc.omr = omr;
+    pc.rows = stack * n0 * n1;
+    const bool vec = (n2 % V == 0) && aligned16(work_w) && aligned16(z) && aligned16(z_out);
+    const int nv = vec ? V : 1;
+    pc.cblocks = (int)((n2 + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
+    const bool iso = h_kind == 1;
+    int e;
+    if (vec)
+      e = pd3o ? launch_c<T, V, true>(pc, iso, work_w, z, z_out, st) : launch_c<T, V, false>(pc, iso, work_w, z, z_out, st);
+    else
+      e = pd3o ? launch_c<T, 1, true>(pc, iso, work_w, z, z_out, st) : launch_c<T, 1, false>(pc, iso, work_w, z, z_out, st);
+    if (e) return e;
+  }
+  return PXA_OK;
+}
+
+
+}  // namespace pds
+}  // namespace pxa
+
+using namespace pxa::pds;
+using namespace pxa;
+
+extern "C" {
+
+int pxa_pds_step(int dtype, int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs,
+                 const double* coefs, const double* diff, const double* scal, int prox, int h_kind, const void* x,
+                 const void* u, const void* z, const void* hty, void* x_out, void* u_out, void* z_out, void* work_q,
+                 void* work_w, int nseg, void* stream) {
+  PXA_DISPATCH(dtype, T,
+               return pds_entry<T>(algo, geom, ntaps, offs, coefs, diff, scal, prox, h_kind, x, u, z, hty, x_out, u_out,
+                                   z_out, work_q, work_w, nseg, as_stream(stream)));
+}
+
+}  // extern "C"

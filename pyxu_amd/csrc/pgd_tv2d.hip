@@ -32,20 +32,13 @@
 // LDS pitches / lane orders are conflict-free for R = 6 fp32 under the MI355X_MICROARCH.md §LDS
 // bank model (scripts/ldsbank.py).  The blockIdx -> tile map is XCD-aware: each of the 8 XCDs owns a
 // contiguous band of tiles so that halo re-reads of x / x_prev hit its own L2.
-#include "common.hpp"
+#include "tile2d.hpp"
 
 namespace pxa {
 namespace {
 
-constexpr int TY = 32;
-constexpr int TX = 64;
-constexpr int kThreads = 256;
-constexpr int kMaxR = 8;
-constexpr int kMaxG = 4 * kMaxR + 1;
-constexpr int kKT = 2 * kMaxR + 2;  // per-axis stride of the LDS tap copy (edge tiles)
+using namespace tile2d;
 
-__host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
-__host__ __device__ constexpr int rup(int a, int b) { return cdiv(a, b) * b; }
 
 template <typename T>
 struct PgdParams {
@@ -62,40 +55,6 @@ struct PgdParams {
   bool vec_ok;
 };
 
-template <typename T, int R>
-struct Layout {
-  static constexpr int V = kVecN<T>;  // elements per 16-B vector (4 fp32, 2 fp64)
-  static constexpr bool F32 = sizeof(T) == 4;
-  static constexpr int CA = rup(2 * R, V);  // A column halo (vector aligned)
-  static constexpr int AR = TY + 4 * R;     // A rows
-  static constexpr int AC = TX + 2 * CA;    // A columns = PT rows
-  static constexpr int NGA = AC / V;        // phase 0: AR x NGA vectors
-  static constexpr int NA = TY / V;         // row groups (pass A and pass B)
-  static constexpr int NB = AC / V;         // pass A column groups
-  static constexpr int CW = F32 ? 2 : 1;    // pass B: output columns per item
-  static constexpr int NCB = TX / CW;       // pass B column items
-  static constexpr int pad_to(int w, int m, int res) {
-    int p = w;
-    while (F32 && (p % m) != res) p += V;
-    return p;
-  }
-  static constexpr int AP = pad_to(AC, 32, 28);   // A pitch (elements)
-  static constexpr int PTP = F32 ? TY + 16 : TY;  // PT pitch (elements)
-  static constexpr int N0 = AR * NGA, NPA = NA * NB, NPB = NA * NCB;
-  static constexpr size_t BYTES = (size_t)(AR * AP + AC * PTP + 2 * kKT) * sizeof(T);
-};
-
-template <typename T, int V>
-__device__ inline void ld_vec(const T* p, T (&v)[V]) {
-  using VT = typename Vec4<T>::type;
-  *reinterpret_cast<VT*>(v) = *reinterpret_cast<const VT*>(p);
-}
-template <typename T, int V>
-__device__ inline void st_vec(T* p, const T (&v)[V]) {
-  using VT = typename Vec4<T>::type;
-  *reinterpret_cast<VT*>(p) = *reinterpret_cast<const VT*>(v);
-}
-
 // q-weight: lam / max(|v|, mu)  (so that q = w v = lam (v - prox_{mu L21}(v)) / mu).
 template <typename T>
 __device__ inline T tv_weight(T n2, T lam, T mu, T inv_mu) {
@@ -106,126 +65,6 @@ template <>
 __device__ inline float tv_weight<float>(float n2, float lam, float mu, float inv_mu) {
   const float r = __builtin_amdgcn_rsqf(n2);  // 1/|v| (inf at 0), 1 ulp
   return lam * (r < inv_mu ? r : inv_mu);
-}
-
-template <typename T>
-__device__ inline T apply_prox(int prox, T z, T pw) {
-  if (prox == 1) return fmax(z, T(0));  // PositiveOrthant: clip(0, None)
-  if (prox == 2) {                       // L1: sign(z) * max(|z| - pw, 0)
-    T m = (z < T(0) ? -z : z) - pw;
-    m = m > T(0) ? m : T(0);
-    return z < T(0) ? -m : m;
-  }
-  return z;
-}
-
-// Packed-arithmetic unit: fp32 pairs (v_pk_fma_f32), fp64 scalars.
-template <typename T>
-struct Pk {
-  using type = T;
-  static constexpr int W = 1;
-  __device__ static type splat(T v) { return v; }
-};
-template <>
-struct Pk<float> {
-  typedef float type __attribute__((ext_vector_type(2)));
-  static constexpr int W = 2;
-  __device__ static type splat(float v) { return type{v, v}; }
-};
-
-// Register-blocked sweep along the leading axis of a [m][pitch PS] source: for NO outputs along the
-// sweep and one V-vector across it, out[o][v] = sum_{t=0}^{4R} g[t] src[(o + t) * PS + v].
-template <typename T, int R, int NO, int PS>
-__device__ inline void sweep(const T* __restrict__ src, const T* __restrict__ g, T (&out)[NO][kVecN<T>]) {
-  constexpr int V = kVecN<T>;
-  using P = typename Pk<T>::type;
-  constexpr int NP = V / Pk<T>::W;
-  using VT = typename Vec4<T>::type;
-  P acc[NO][NP];
-#pragma unroll
-  for (int o = 0; o < NO; ++o)
-#pragma unroll
-    for (int h = 0; h < NP; ++h) acc[o][h] = Pk<T>::splat(T(0));
-#pragma unroll
-  for (int j = 0; j < NO + 4 * R; ++j) {
-    const VT t = *reinterpret_cast<const VT*>(src + j * PS);
-    P row[NP];
-    __builtin_memcpy(&row[0], &t, sizeof(VT));
-#pragma unroll
-    for (int o = 0; o < NO; ++o) {
-      const int k = j - o;
-      if (k >= 0 && k <= 4 * R) {
-        const P gg = Pk<T>::splat(g[k]);
-#pragma unroll
-        for (int h = 0; h < NP; ++h) acc[o][h] = gg * row[h] + acc[o][h];
-      }
-    }
-  }
-#pragma unroll
-  for (int o = 0; o < NO; ++o) __builtin_memcpy(&out[o][0], &acc[o][0], sizeof(T) * V);
-}
-
-// Boundary rows of G along one axis, as a correction of the Toeplitz sweep.  The sweep evaluates
-// sum_p k[i-p] (H y)[p] over ALL p, i.e. including the R "ghost" positions p outside [0, n) where the
-// zero-padded H y is still non-zero; the exact G = H^T H only sums p inside [0, n), so
-//   (G y)[i] = sweep[i] - sum_{ghost p, |i - p| <= R} k[i - p] (H y)[p].
-// acc[o][v]: NO outputs along the sweep axis at positions i0 + o, one V-vector across it;
-// the V-vector of position q along the sweep axis is at src + (q - q0) * PS (zero outside [0, n));
-// k: the taps (compile-time indices), kt: the same taps in LDS (runtime indices).
-template <typename T, int R, int NO, int PS>
-__device__ inline void ghost_fix(int i0, int n, int q0, const T* __restrict__ src, const T* __restrict__ k,
-                                 const T* __restrict__ kt, T (&acc)[NO][kVecN<T>]) {
-  constexpr int V = kVecN<T>;
-  using VT = typename Vec4<T>::type;
-#pragma unroll
-  for (int side = 0; side < 2; ++side) {
-    const int pg = side == 0 ? -R : n;  // first ghost position on this side
-    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
-    if (!hit) continue;
-    T gh[R][V];  // (H y)[pg + m] across the vector
-#pragma unroll
-    for (int m = 0; m < R; ++m) {
-      const int pp = pg + m;
-#pragma unroll
-      for (int v = 0; v < V; ++v) gh[m][v] = T(0);
-      if (pp >= i0 - R && pp <= i0 + NO - 1 + R) {  // used by some output (keeps reads inside the window)
-#pragma unroll
-        for (int s = -R; s <= R; ++s) {
-          T w[V];
-          const VT t = *reinterpret_cast<const VT*>(src + (pp + s - q0) * PS);
-          __builtin_memcpy(&w[0], &t, sizeof(VT));
-#pragma unroll
-          for (int v = 0; v < V; ++v) gh[m][v] = k[s + R] * w[v] + gh[m][v];
-        }
-      }
-    }
-#pragma unroll
-    for (int o = 0; o < NO; ++o) {
-      const int i = i0 + o;
-      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
-#pragma unroll
-      for (int m = 0; m < R; ++m) {
-        const int t = i - (pg + m);
-        if (t < -R || t > R) continue;
-        const T kk = kt[t + R];
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[o][v] = acc[o][v] - kk * gh[m][v];
-      }
-    }
-  }
-}
-
-// Global V-vector load at an element offset whose alignment is known at compile time.
-template <typename T>
-__device__ inline void ld_pair(const T* __restrict__ p, T (&v)[2]) {
-  if constexpr (sizeof(T) == 4) {
-    const float2 t = *reinterpret_cast<const float2*>(p);
-    v[0] = t.x;
-    v[1] = t.y;
-  } else {
-    v[0] = p[0];
-    v[1] = p[1];
-  }
 }
 
 template <typename T, int R, bool EDGE>
@@ -452,11 +291,7 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  // XCD-aware tile order (speed only): XCD group g = blockIdx % 8 owns a contiguous band of tiles.
-  const unsigned nb = p.ntiles;
-  const unsigned bid = blockIdx.x;
-  const unsigned q8 = nb >> 3, r8 = nb & 7u, g8 = bid & 7u;
-  const unsigned tile = g8 * q8 + (g8 < r8 ? g8 : r8) + (bid >> 3);
+  const unsigned tile = xcd_tile(blockIdx.x, p.ntiles);
   const unsigned tpi = (unsigned)p.tiles0 * (unsigned)p.tiles1;
   const unsigned s = tile / tpi;
   const unsigned tr = tile - s * tpi;

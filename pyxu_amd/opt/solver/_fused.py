@@ -17,7 +17,7 @@ from pyxu_amd.operator.linop.diff import _DiffStack
 from pyxu_amd.operator.linop.stencil import Stencil
 from pyxu_amd.util import is_device_array
 
-__all__ = ["match_pgd_deblur"]
+__all__ = ["match_pgd_deblur", "match_pds_deblur"]
 
 MAX_R = 8
 
@@ -150,3 +150,91 @@ def match_pgd_deblur(f, g, x0):
     rows = int(np.prod(x0.shape[:-1])) if x0.ndim > 1 else 1
     return dict(shift=shift, H=H, taps0=taps[0], taps1=taps[1], n0=n0, n1=n1, B=B, rows=rows, lam=lam, mu=mu, h0=h0,
                 h1=h1, prox=prox, prox_scale=pw)
+
+
+def _all_axis_taps(H, sh):
+    """Per-axis taps of a separable constant-mode Stencil over ALL axes of sh (identity -> [1] at 0)."""
+    if not isinstance(H, Stencil) or not H._separable or any(m != "constant" for m in H._mode):
+        return None
+    taps = []
+    for st in H._st_fw:
+        if st.identity:
+            taps.append(([0], [1.0]))
+            continue
+        o, c = st.axis_taps()
+        if max(abs(v) for v in o) > MAX_R:
+            return None
+        taps.append((list(o), list(c)))
+    return taps
+
+
+def _g_prox(g):
+    if g is None or getattr(g, "_name", "") == "NullFunc":
+        return 0, 0.0
+    gi, gs = _unscale(g)
+    if isinstance(gi, PositiveOrthant) and gs > 0:
+        return 1, 0.0
+    if isinstance(gi, L1Norm) and gs > 0:
+        return 2, gs
+    return None
+
+
+def match_pds_deblur(f, g, h, K, x0):
+    """PD3O / CondatVu fused step (pxa_pds_step): f = 1/2||S.-y||^2 (S separable zero-boundary
+    stencil, 2-D or 3-D), K = Gradient (all axes, or the trailing two of a batch-as-axis volume),
+    h = lam L1 (anisotropic TV) or lam L21 over the directions (isotropic TV), g in {None,
+    PositiveOrthant, lam L1}.  Returns the kernel parameters or None."""
+    if f is None or h is None or K is None:
+        return None
+    dt = _data_term(f)
+    if dt is None:
+        return None
+    H, shift = dt
+    sh = tuple(getattr(H, "_arg_shape", ()) or ())
+    if len(sh) not in (2, 3) or shift.ndim != 1:
+        return None
+    taps = _all_axis_taps(H, sh)
+    if taps is None:
+        return None
+    G = _core(K)
+    if not isinstance(G, _DiffStack) or G._fused is None or tuple(G.arg_shape) != sh:
+        return None
+    dirs = tuple(G._directions)
+    if len(sh) == 2:
+        if dirs != (0, 1):
+            return None
+        n0, (n1, n2), D = 1, sh, 2
+        taps = [([0], [1.0])] + taps
+        axes = (1, 2)
+    else:
+        if dirs == (0, 1, 2):
+            D = 3
+        elif dirs == (1, 2):
+            D = 2
+        else:
+            return None
+        n0, n1, n2 = sh
+        axes = dirs
+    c0, c1 = [0.0, 0.0, 0.0], [0.0, 0.0, 0.0]
+    for ax, (d, o0, a0, o1, a1) in zip(axes, G._fused):
+        if (o0, o1) != (0, 1):
+            return None
+        c0[ax], c1[ax] = float(a0), float(a1)
+    hi, lam = _unscale(h)
+    if lam <= 0:
+        return None
+    N = int(np.prod(sh))
+    if isinstance(hi, L1Norm) and hi.dim == D * N:
+        h_kind = 0
+    elif isinstance(hi, L21Norm) and tuple(hi._l2_axis.tolist()) == (0,) and tuple(hi._arg_shape) == (D, *sh):
+        h_kind = 1
+    else:
+        return None
+    gp = _g_prox(g)
+    if gp is None:
+        return None
+    if x0.shape[-1] != N:
+        return None
+    rows = int(np.prod(x0.shape[:-1])) if x0.ndim > 1 else 1
+    return dict(shift=shift, H=H, taps=taps, n0=n0, n1=n1, n2=n2, D=D, c0=c0, c1=c1, lam=float(lam), h_kind=h_kind,
+                prox=gp[0], prox_scale=gp[1], rows=rows)

@@ -7,6 +7,7 @@ Step-size rules, momentum and initialisation follow the reference line by line (
 444-517, 763-864, 1604-1687); the iterates live on the MI355X and every update is a HIP kernel.
 """
 import math
+import sys
 import types
 import warnings
 
@@ -65,7 +66,7 @@ class _PrimalDualSplitting(pxa.Solver):
         self._objective_func_cache = None  # f + g + h o K, built on first use (construction stays compute-free)
 
     @pxrt.enforce_precision(i=("x0", "z0", "tau", "sigma", "rho"), allow_None=True)
-    def m_init(self, x0, z0=None, tau=None, sigma=None, rho=None, tuning_strategy=1):
+    def m_init(self, x0, z0=None, tau=None, sigma=None, rho=None, tuning_strategy=1, fused=True):
         mst = self._mstate
         mst["x"] = _dev.require(x0, "x0")
         mst["z"] = self._set_dual_variable(z0)
@@ -73,6 +74,38 @@ class _PrimalDualSplitting(pxa.Solver):
         gamma = self._set_gamma(tuning_strategy)
         mst["tau"], mst["sigma"], delta = self._set_step_sizes(tau, sigma, gamma)
         mst["rho"] = self._set_momentum_term(rho, delta)
+        self._spare = None
+        self._plan = self._fused_plan(mst["x"]) if fused else None
+
+    _FUSED_ALGO = None  # pxa_pds_step algo code of the subclass (0 PD3O, 1 CondatVu), None: no fused step
+
+    def _fused_plan(self, x0):
+        """Parameters of the fused pxa_pds_step iteration, or None (generic rule-by-rule path)."""
+        from pyxu_amd.opt.solver._fused import match_pds_deblur
+
+        if self._FUSED_ALGO is None or _is_null(self._h) or x0.dtype != self._mstate["z"].dtype:
+            return None
+        p = match_pds_deblur(self._f, self._g, self._h, self._K, x0)
+        if p is None:
+            return None
+        mst = self._mstate
+        y = _dev.axpby(-1.0, pxrt.coerce(p["shift"]))  # data y = -shift
+        p["hty"] = _dev.copy(p["H"].adjoint(y))  # S^T y: iteration-invariant (G x - S^T y = grad f(x))
+        stack = p["rows"]
+        p["pre"] = _dev.pds_args(stack, 1, p["n0"], p["n1"], p["n2"], p["D"], p["taps"], p["c0"], p["c1"], mst["tau"],
+                                 mst["sigma"], mst["rho"], p["lam"], p["prox"], mst["tau"] * p["prox_scale"], p["h_kind"])
+        x = mst["x"]
+        p["w"] = _dev.empty_like(x)
+        p["q"] = None if p["taps"][0] == ([0], [1.0]) else _dev.empty_like(x)
+        p["nseg"] = 0  # axis-0 march segments (0: one per column; tuning knob of pxa_pds_step)
+        return p
+
+    @staticmethod
+    def _owned(t, extra=0):
+        """True iff `t` is referenced only by the solver state (+ `extra` caller locals): it may be
+        overwritten in place.  The reference allocates fresh arrays each step, so arrays a user holds
+        (z0, logged iterates) are never modified."""
+        return sys.getrefcount(t) <= 3 + extra
 
     def m_step(self):
         raise NotImplementedError
@@ -144,8 +177,21 @@ def _knorm_msg():
 class CondatVu(_PrimalDualSplitting):
     """Condat-Vu primal-dual splitting (pds.py:207-520)."""
 
+    _FUSED_ALGO = 1
+
     def m_step(self):
         mst = self._mstate
+        if self._plan is not None:
+            p = self._plan
+            x, z = mst["x"], mst["z"]
+            out = self._spare
+            if out is None or out is x:
+                out = _dev.empty_like(x)
+            z_out = z if self._owned(z, extra=1) else _dev.empty_like(z)
+            _dev.pds_step(1, p["pre"], x, None, z, p["hty"], out, None, z_out, p["q"], p["w"], nseg=p["nseg"])
+            mst["x"], mst["z"] = out, z_out
+            self._spare = x if sys.getrefcount(x) == 2 else None
+            return
         x = mst["x"]
         tau = mst["tau"]
         # x - tau*grad_f(x) - tau*K^T z
@@ -216,9 +262,11 @@ CV = CondatVu
 class PD3O(_PrimalDualSplitting):
     """Primal-Dual Three-Operator splitting (pds.py:523-864)."""
 
+    _FUSED_ALGO = 0
+
     @pxrt.enforce_precision(i=("x0", "z0", "tau", "sigma", "rho"), allow_None=True)
-    def m_init(self, x0, z0=None, tau=None, sigma=None, rho=None, tuning_strategy=1):
-        super().m_init(x0=x0, z0=z0, tau=tau, sigma=sigma, rho=rho, tuning_strategy=tuning_strategy)
+    def m_init(self, x0, z0=None, tau=None, sigma=None, rho=None, tuning_strategy=1, fused=True):
+        super().m_init(x0=x0, z0=z0, tau=tau, sigma=sigma, rho=rho, tuning_strategy=tuning_strategy, fused=fused)
         if _is_null(self._g) and _is_null(self._h):
             self._mstate["u"] = _dev.axpby(1.01, self._mstate["x"])
         else:
@@ -226,6 +274,15 @@ class PD3O(_PrimalDualSplitting):
 
     def m_step(self):
         mst = self._mstate
+        if self._plan is not None:
+            p = self._plan
+            x, u, z = mst["x"], mst["u"], mst["z"]
+            x_out = x if self._owned(x, extra=1) else _dev.empty_like(x)
+            u_out = u if self._owned(u, extra=1) else _dev.empty_like(u)
+            z_out = z if self._owned(z, extra=1) else _dev.empty_like(z)
+            _dev.pds_step(0, p["pre"], None, u, z, p["hty"], x_out, u_out, z_out, p["q"], p["w"], nseg=p["nseg"])
+            mst["x"], mst["u"], mst["z"] = x_out, u_out, z_out
+            return
         tau, rho = mst["tau"], mst["rho"]
         t = _dev.axpby(1.0, mst["u"], -tau, self._K.jacobian(mst["u"]).adjoint(mst["z"]))
         mst["x"] = self._g.prox(t, tau=tau)

@@ -206,8 +206,9 @@ def test_pgd_stacked_golden():
             assert rel_err(to_NUMPY(s.solution()), g["x_20"]) <= 1e-5
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("name", golden_names("pds_"))
-def test_pds_trajectory_golden(name):
+def test_pds_trajectory_golden(name, fused):
     g = load_golden(name)
     dt = g["x0"].dtype.type
     sh = tuple(g["arg_shape"])
@@ -222,7 +223,8 @@ def test_pds_trajectory_golden(name):
         for key, klass in (("pd3o", pxs.PD3O), ("cv", pxs.CondatVu)):
             for n in (1, 10, 100):
                 s = klass(f=f, g=None, h=h, K=K, show_progress=False)
-                s.fit(x0=D(g["x0"]), stop_crit=pxst.MaxIter(n))
+                s.fit(x0=D(g["x0"]), stop_crit=pxst.MaxIter(n), fused=fused)
+                assert (s._plan is not None) == fused
                 assert s._mstate["tau"] == g[f"{key}_tau"] and s._mstate["sigma"] == g[f"{key}_sigma"]
                 data, _ = s.stats()
                 assert rel_err(to_NUMPY(data["x"]), g[f"{key}_x_{n}"]) <= TRAJ_TOL[dt], (key, n)

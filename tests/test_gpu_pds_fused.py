@@ -1,0 +1,174 @@
+"""
+GPU parity of the fused primal-dual splitting step (pxa_pds_step: PD3O and Condat-Vu, three launches
+per iteration) against the CPU oracle's restatement of the reference's m_step (pds.py:429-442,
+747-761) on the same seeded inputs, and against the generic rule-by-rule path.
+
+Tolerance (north_star): trajectories after 8 iterations <= 1e-5 norm-wise relative in fp32,
+<= 1e-10 in fp64.  Cases cover 2-D images, 3-D volumes, batch-as-axis volumes (directions (1, 2)),
+sizes smaller than the blur radius, ragged multi-tile planes, blur radii 2..8, anisotropic (L1) and
+isotropic (L21) TV, and g in {None, PositiveOrthant, lam L1}.
+"""
+import numpy as np
+import pytest
+
+import oracle as orc
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs an MI355X", allow_module_level=True)
+
+import pyxu_amd.operator as pxo  # noqa: E402
+import pyxu_amd.opt.solver as pxs  # noqa: E402
+import pyxu_amd.opt.stop as pxst  # noqa: E402
+import pyxu_amd.runtime as pxrt  # noqa: E402
+from pyxu_amd import _dev  # noqa: E402
+from pyxu_amd.util import to_device, to_NUMPY  # noqa: E402
+
+TOL = {np.float32: 1e-5, np.float64: 1e-10}
+ALGOS = {"pd3o": pxs.PD3O, "cv": pxs.CondatVu}
+
+
+def W(dt):
+    return pxrt.Width.SINGLE if np.dtype(dt) == np.float32 else pxrt.Width.DOUBLE
+
+
+def D(a):
+    return to_device(np.ascontiguousarray(a))
+
+
+def _problem(sh, sigma, h_kind, g_kind, dt, batch_axis=False, lam=0.05, seed=0):
+    """(f, g, h, K, host pieces for the oracle) of 1/2||S.-y||^2 + g + lam TV."""
+    rng = np.random.default_rng(seed)
+    N = int(np.prod(sh))
+    y = rng.standard_normal(N).astype(dt)
+    taps, c = orc.gaussian_taps(sigma, 3.0, dt)
+    if batch_axis:
+        kern = [np.array([1.0], dtype=dt), taps, taps]
+        cen = [0, c, c]
+        dirs = (1, 2)
+    else:
+        kern = [taps] * len(sh)
+        cen = [c] * len(sh)
+        dirs = tuple(range(len(sh)))
+    Dd = len(dirs)
+    S = pxo.Stencil(arg_shape=sh, kernel=kern, center=cen, mode="constant")
+    f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(D(y)) * S
+    f.diff_lipschitz = 1.0
+    K = pxo.Gradient(arg_shape=sh, directions=dirs)
+    h = lam * (pxo.L21Norm(arg_shape=(Dd, *sh)) if h_kind == "iso" else pxo.L1Norm(dim=Dd * N))
+    g = {"none": None, "pos": pxo.PositiveOrthant(dim=N), "l1": 0.01 * pxo.L1Norm(dim=N)}[g_kind]
+    host = dict(y=y, blur=dict(arg_shape=sh, kernel=kern, center=cen), dirs=dirs, Dd=Dd, lam=lam)
+    return f, g, h, K, host
+
+
+def _oracle(algo, host, g_kind, x0, tau, sigma, rho, n, h_kind, sh):
+    dt = x0.dtype.type
+    y, blur, dirs, Dd, lam = host["y"], host["blur"], host["dirs"], host["Dd"], host["lam"]
+    grad_f = lambda v: orc.deblur_tv_grad(v, blur, y, 0.0, 1.0, dict(arg_shape=sh))
+    Kf = lambda v: orc.gradient_apply(v, arg_shape=sh, directions=dirs)
+    KT = lambda v: orc.gradient_adjoint(v, arg_shape=sh, directions=dirs)
+    if h_kind == "iso":
+        hp = lambda v, t: orc.l21_prox(v, t * dt(lam), (Dd, *sh))
+    else:
+        hp = lambda v, t: orc.l1_prox(v, t * dt(lam))
+    fprox = lambda v, s: orc.fenchel_prox(hp, v, s)
+    pg = {"none": None, "pos": lambda v, t: orc.positive_orthant_prox(v), "l1": lambda v, t: orc.l1_prox(v, t * dt(0.01))}[g_kind]
+    if algo == "pd3o":
+        x, z, _ = orc.pd3o(x0, grad_f, pg, Kf, KT, fprox, tau, sigma, rho, n)
+    else:
+        x, z = orc.condat_vu(x0, grad_f, pg, Kf, KT, fprox, tau, sigma, rho, n)
+    return x, z
+
+
+CASES = [
+    # (shape, sigma, h, g, dtype, batch-as-axis)
+    ((5, 7), 0.8, "l1", "none", np.float32, False),
+    ((40, 68), 2.0, "iso", "pos", np.float32, False),
+    ((70, 131), 2.5, "l1", "l1", np.float64, False),
+    ((6, 9, 11), 0.8, "l1", "none", np.float32, False),
+    ((17, 40, 70), 2.0, "l1", "none", np.float32, False),
+    ((13, 33, 66), 1.0, "iso", "pos", np.float64, False),
+    ((4, 33, 66), 2.0, "l1", "none", np.float32, True),
+]
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{'x'.join(map(str, c[0]))}-s{c[1]}-{c[2]}-{c[3]}-{np.dtype(c[4]).name}{'-batch' if c[5] else ''}")
+def test_pds_fused_vs_oracle(algo, case):
+    sh, sigma, h_kind, g_kind, dt, batch = case
+    N = int(np.prod(sh))
+    x0 = np.random.default_rng(1).uniform(0, 1, N).astype(dt)
+    n = 8
+    with pxrt.Precision(W(dt)):
+        f, g, h, K, host = _problem(sh, sigma, h_kind, g_kind, dt, batch_axis=batch)
+        s = ALGOS[algo](f=f, g=g, h=h, K=K, show_progress=False)
+        s.fit(x0=D(x0), stop_crit=pxst.MaxIter(n))
+        assert s._plan is not None, "fused path not selected"
+        x, z = to_NUMPY(s._mstate["x"]), to_NUMPY(s._mstate["z"])
+        tau, sigma_, rho = s._mstate["tau"], s._mstate["sigma"], s._mstate["rho"]
+    xr, zr = _oracle(algo, host, g_kind, x0, tau, sigma_, rho, n, h_kind, sh)
+    assert rel_err(x, xr) <= TOL[dt], algo
+    assert rel_err(z, zr) <= TOL[dt], algo
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+def test_pds_fused_matches_generic(algo):
+    """Fused (3 launches) vs the generic rule-by-rule path (also HIP) on a multi-tile volume."""
+    sh = (24, 64, 200)
+    N = int(np.prod(sh))
+    x0 = np.random.default_rng(2).uniform(0, 1, N).astype(np.float32)
+    out = {}
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        f, g, h, K, _ = _problem(sh, 2.0, "l1", "none", np.float32)
+        for fused in (True, False):
+            s = ALGOS[algo](f=f, g=g, h=h, K=K, show_progress=False)
+            s.fit(x0=D(x0), stop_crit=pxst.MaxIter(10), fused=fused)
+            assert (s._plan is not None) == fused
+            out[fused] = (to_NUMPY(s._mstate["x"]), to_NUMPY(s._mstate["z"]))
+    assert rel_err(out[True][0], out[False][0]) <= 1e-5
+    assert rel_err(out[True][1], out[False][1]) <= 1e-5
+
+
+def test_pds_axis0_segments_bit_exact():
+    """Splitting the axis-0 march into segments recomputes the halo planes with the same arithmetic."""
+    sh = (37, 40, 64)
+    N = int(np.prod(sh))
+    x0 = np.random.default_rng(3).uniform(0, 1, N).astype(np.float32)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        f, g, h, K, _ = _problem(sh, 2.0, "iso", "pos", np.float32)
+        s = pxs.PD3O(f=f, g=g, h=h, K=K, show_progress=False)
+        s.fit(x0=D(x0), stop_crit=pxst.MaxIter(3))
+        p, m = s._plan, s._mstate
+        outs = []
+        for nseg in (1, 3, 37):
+            xo, uo, zo = _dev.empty_like(m["x"]), _dev.empty_like(m["u"]), _dev.empty_like(m["z"])
+            _dev.pds_step(0, p["pre"], None, m["u"], m["z"], p["hty"], xo, uo, zo, p["q"], p["w"], nseg=nseg)
+            outs.append([to_NUMPY(t) for t in (xo, uo, zo)])
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+def test_pds_fused_stacked_rows_and_no_input_mutation(algo):
+    """(2, N) stacked initial points = two single solves; a user-held z0 is never overwritten."""
+    sh = (9, 20, 36)
+    N = int(np.prod(sh))
+    rng = np.random.default_rng(4)
+    x0 = rng.uniform(0, 1, (2, N)).astype(np.float32)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        f, g, h, K, _ = _problem(sh, 1.0, "l1", "none", np.float32)
+        z0 = K(D(x0))
+        z0_host = to_NUMPY(z0).copy()
+        s = ALGOS[algo](f=f, g=g, h=h, K=K, show_progress=False)
+        s.fit(x0=D(x0), z0=z0, stop_crit=pxst.MaxIter(5))
+        assert s._plan is not None
+        xs = to_NUMPY(s._mstate["x"])
+        assert np.array_equal(to_NUMPY(z0), z0_host)
+        for r in range(2):
+            s1 = ALGOS[algo](f=f, g=g, h=h, K=K, show_progress=False)
+            s1.fit(x0=D(x0[r]), stop_crit=pxst.MaxIter(5))
+            assert rel_err(xs[r], to_NUMPY(s1._mstate["x"])) <= 1e-6
