@@ -43,8 +43,7 @@ template <typename T>
 struct PdsC {
   PdsGeom<T> g;
   T sigma, t, rho, omr;  // t = (1 / sigma) * lam, as pxa_fenchel_prox_* computes it
-  int64_t rows;          // stack * n0 * n1
-  int cblocks;           // column blocks per row
+  int seg;               // planes per axis-0 segment
 };
 
 template <typename T>
@@ -55,66 +54,79 @@ __device__ inline T soft_thr(T x, T tau) {  // L1Norm.prox (norm.py:47-52), as e
   return m * sg;
 }
 
-// One thread = NV consecutive voxels of a row; workgroups stride over (row, column block) items.
+template <typename T, int NV>
+__device__ inline void ldv(const T* p, T (&v)[NV]) {
+  if constexpr (NV == kVecN<T>)
+    *reinterpret_cast<typename Vec4<T>::type*>(v) = *reinterpret_cast<const typename Vec4<T>::type*>(p);
+  else
+    v[0] = p[0];
+}
+
+// Thread = NV consecutive in-plane positions of one row; it marches the planes of its segment, so the
+// axis-0 forward neighbour w(p + 1) is loaded once and carried to the next step.  The in-plane block
+// index is XCD-banded (tile2d::xcd_tile) so that the row+1 neighbour is usually read from the L2 of the
+// same XCD, where the neighbouring block marches in step.
 template <typename T, int NV, bool ISO, bool PD3O>
 __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __restrict__ w,
                                                           const T* __restrict__ z, T* __restrict__ zo) {
-  using VT = typename Vec4<T>::type;
-  const PdsGeom<T>& g = p.g;
+  const PdsGeom<T> g = p.g;
+  const T sigma = p.sigma, thr = p.t, rho = p.rho, omr = p.omr;
   const int n0 = g.n0, n1 = g.n1, n2 = g.n2, D = g.D;
   const int64_t M = (int64_t)n1 * n2, N = M * n0;
   const int a_first = 3 - D;
-  const int64_t items = p.rows * p.cblocks;
-  for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
-    const int64_t rowg = item / p.cblocks;
-    const int cb = (int)(item - rowg * p.cblocks);
-    const int c = (cb * kBlock + (int)threadIdx.x) * NV;
-    if (c >= n2) continue;
-    const int64_t vp = rowg / n1;  // volume-plane index s * n0 + plane
-    const int r = (int)(rowg - vp * n1);
-    const int64_t s = vp / n0;
-    const int plane = (int)(vp - s * n0);
-    const int64_t off = vp * M + (int64_t)r * n2 + c;  // in w
-    const int64_t zoff = s * (int64_t)D * N + (int64_t)plane * M + (int64_t)r * n2 + c;
-    T wc[NV];
-    if constexpr (NV == kVecN<T>)
-      *reinterpret_cast<VT*>(wc) = *reinterpret_cast<const VT*>(w + off);
-    else
-      wc[0] = w[off];
+  const unsigned blk = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t j0 = ((int64_t)blk * kBlock + threadIdx.x) * NV;
+  if (j0 >= M) return;  // no barriers below
+  const int r = (int)(j0 / n2), c = (int)(j0 - (int64_t)r * n2);
+  const int64_t s = blockIdx.z;
+  const int pb = blockIdx.y * p.seg;
+  const int pe = pb + p.seg < n0 ? pb + p.seg : n0;
+  const T* ws = w + s * N + j0;
+  const T* zs = z + s * (int64_t)D * N + j0;
+  T* zos = zo + s * (int64_t)D * N + j0;
+  const bool row_nb = r + 1 < n1, col_nb = c + NV < n2;
+  T wn0[NV];  // w at the current plane (carried from the previous step)
+  ldv<T, NV>(ws + (int64_t)pb * M, wn0);
+  for (int pl = pb; pl < pe; ++pl) {
+    const int64_t off = (int64_t)pl * M;
+    T wc[NV], wp[NV];
+#pragma unroll
+    for (int e = 0; e < NV; ++e) wc[e] = wn0[e];
+    if (pl + 1 < n0) {
+      ldv<T, NV>(ws + off + M, wp);
+    } else {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) wp[e] = T(0);
+    }
     T zin[3][NV], zc[3][NV];
 #pragma unroll
     for (int ax = 0; ax < 3; ++ax) {
       if (ax < a_first) continue;
-      const int d = ax - a_first;
       T wn[NV];
-      if (ax == 2) {
+      if (ax == 0) {
 #pragma unroll
-        for (int e = 0; e + 1 < NV; ++e) wn[e] = wc[e + 1];
-        wn[NV - 1] = (c + NV < n2) ? w[off + NV] : T(0);
-      } else {
-        const bool has = ax == 1 ? (r + 1 < n1) : (plane + 1 < n0);
-        const int64_t st = ax == 1 ? (int64_t)n2 : M;
-        if (has) {
-          if constexpr (NV == kVecN<T>)
-            *reinterpret_cast<VT*>(wn) = *reinterpret_cast<const VT*>(w + off + st);
-          else
-            wn[0] = w[off + st];
+        for (int e = 0; e < NV; ++e) wn[e] = wp[e];
+      } else if (ax == 1) {
+        if (row_nb) {
+          ldv<T, NV>(ws + off + n2, wn);
         } else {
 #pragma unroll
           for (int e = 0; e < NV; ++e) wn[e] = T(0);
         }
+      } else {
+#pragma unroll
+        for (int e = 0; e + 1 < NV; ++e) wn[e] = wc[e + 1];
+        wn[NV - 1] = col_nb ? ws[off + NV] : T(0);
       }
-      const T* zd = z + zoff + (int64_t)d * N;
-      if constexpr (NV == kVecN<T>)
-        *reinterpret_cast<VT*>(zc[ax]) = *reinterpret_cast<const VT*>(zd);
-      else
-        zc[ax][0] = zd[0];
+      ldv<T, NV>(zs + (int64_t)(ax - a_first) * N + off, zc[ax]);
 #pragma unroll
       for (int e = 0; e < NV; ++e) {
         const T kw = g.c0[ax] * wc[e] + g.c1[ax] * wn[e];  // forward difference (pxa_gradient2)
-        zin[ax][e] = T(1) * zc[ax][e] + p.sigma * kw;       // z + sigma K w
+        zin[ax][e] = T(1) * zc[ax][e] + sigma * kw;         // z + sigma K w
       }
     }
+#pragma unroll
+    for (int e = 0; e < NV; ++e) wn0[e] = wp[e];
     T zt[3][NV];
     if constexpr (ISO) {
       // fenchel_prox of lam L21 (groups over directions): pxa_fenchel_prox_l21
@@ -124,16 +136,16 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
 #pragma unroll
         for (int ax = 0; ax < 3; ++ax) {
           if (ax < a_first) continue;
-          const T v = zin[ax][e] / p.sigma;
+          const T v = zin[ax][e] / sigma;
           ss += v * v;
         }
         const T n = sqrt(ss);
-        const T f = T(1) - p.t / (n > p.t ? n : p.t);
+        const T f = T(1) - thr / (n > thr ? n : thr);
 #pragma unroll
         for (int ax = 0; ax < 3; ++ax) {
           if (ax < a_first) continue;
-          const T pr = (zin[ax][e] / p.sigma) * f;
-          zt[ax][e] = pr * (-p.sigma) + zin[ax][e];
+          const T pr = (zin[ax][e] / sigma) * f;
+          zt[ax][e] = pr * (-sigma) + zin[ax][e];
         }
       }
     } else {
@@ -142,8 +154,8 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
         if (ax < a_first) continue;
 #pragma unroll
         for (int e = 0; e < NV; ++e) {
-          const T pr = soft_thr<T>(zin[ax][e] / p.sigma, p.t);  // pxa_fenchel_prox_l1
-          zt[ax][e] = pr * (-p.sigma) + zin[ax][e];
+          const T pr = soft_thr<T>(zin[ax][e] / sigma, thr);  // pxa_fenchel_prox_l1
+          zt[ax][e] = pr * (-sigma) + zin[ax][e];
         }
       }
     }
@@ -153,26 +165,26 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
       T zn[NV];
 #pragma unroll
       for (int e = 0; e < NV; ++e)
-        zn[e] = PD3O ? p.omr * zc[ax][e] + p.rho * zt[ax][e] : p.rho * zt[ax][e] + p.omr * zc[ax][e];
-      T* zq = zo + zoff + (int64_t)(ax - a_first) * N;
+        zn[e] = PD3O ? omr * zc[ax][e] + rho * zt[ax][e] : rho * zt[ax][e] + omr * zc[ax][e];
+      T* zq = zos + (int64_t)(ax - a_first) * N + off;
       if constexpr (NV == kVecN<T>)
-        *reinterpret_cast<VT*>(zq) = *reinterpret_cast<const VT*>(zn);
+        *reinterpret_cast<typename Vec4<T>::type*>(zq) = *reinterpret_cast<const typename Vec4<T>::type*>(zn);
       else
         zq[0] = zn[0];
     }
   }
 }
 
-
 template <typename T, int NV, bool PD3O>
-int launch_c(const PdsC<T>& pc, bool iso, const void* w, const void* z, void* zo, hipStream_t st) {
-  const int64_t items = pc.rows * pc.cblocks;
-  const int grid = (int)(items < (int64_t)kMaxGrid ? items : (int64_t)kMaxGrid);
+int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, const void* z, void* zo,
+             hipStream_t st) {
+  const int64_t blocks = (M + (int64_t)kBlock * NV - 1) / ((int64_t)kBlock * NV);
+  dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pc.g.stack);
   if (iso)
-    hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O>), dim3(grid), dim3(kBlock), 0, st, pc, (const T*)w,
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
                        (const T*)z, (T*)zo);
   else
-    hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O>), dim3(grid), dim3(kBlock), 0, st, pc, (const T*)w,
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
                        (const T*)z, (T*)zo);
   return last_launch_status();
 }
@@ -243,7 +255,14 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
     pa.tau = tau;
     pa.pw = pw;
     pa.prox = prox;
-    if (nseg < 1) nseg = 1;
+    if (nseg < 1) {
+      // auto: about 4096 workgroups in flight, segments >= 4 rings deep (halo recompute <= 1/2)
+      const int64_t blocks = stack * ((M + 2 * kAThreads - 1) / (2 * kAThreads));
+      const int64_t want = (4096 + blocks - 1) / blocks;
+      const int64_t cap = R0 > 0 ? n0 / (4 * (2 * R0 + 1)) : n0;
+      nseg = (int)(want < cap ? want : cap);
+      if (nseg < 1) nseg = 1;
+    }
     if (nseg > n0) nseg = (int)n0;
     pa.seg = (int)((n0 + nseg - 1) / nseg);
     nseg = (int)((n0 + pa.seg - 1) / pa.seg);
@@ -304,16 +323,23 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
     pc.t = (T(1) / sigma) * lam;
     pc.rho = rho;
     pc.omr = omr;
-    pc.rows = stack * n0 * n1;
     const bool vec = (n2 % V == 0) && aligned16(work_w) && aligned16(z) && aligned16(z_out);
     const int nv = vec ? V : 1;
-    pc.cblocks = (int)((n2 + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
+    // enough workgroups for 256 CUs: split the march into segments (no halo: w(p + 1) is a plain load)
+    const int64_t blocks = stack * ((M + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
+    int cseg = (int)((4096 + blocks - 1) / blocks);
+    if (cseg > n0) cseg = (int)n0;
+    if (cseg < 1) cseg = 1;
+    pc.seg = (int)((n0 + cseg - 1) / cseg);
+    cseg = (int)((n0 + pc.seg - 1) / pc.seg);
     const bool iso = h_kind == 1;
     int e;
     if (vec)
-      e = pd3o ? launch_c<T, V, true>(pc, iso, work_w, z, z_out, st) : launch_c<T, V, false>(pc, iso, work_w, z, z_out, st);
+      e = pd3o ? launch_c<T, V, true>(pc, iso, M, cseg, work_w, z, z_out, st)
+               : launch_c<T, V, false>(pc, iso, M, cseg, work_w, z, z_out, st);
     else
-      e = pd3o ? launch_c<T, 1, true>(pc, iso, work_w, z, z_out, st) : launch_c<T, 1, false>(pc, iso, work_w, z, z_out, st);
+      e = pd3o ? launch_c<T, 1, true>(pc, iso, M, cseg, work_w, z, z_out, st)
+               : launch_c<T, 1, false>(pc, iso, M, cseg, work_w, z, z_out, st);
     if (e) return e;
   }
   return PXA_OK;

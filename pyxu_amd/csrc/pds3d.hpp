@@ -86,7 +86,8 @@ __global__ void __launch_bounds__(kAThreads) pds_axis0_kernel(PdsA<T> p, const T
 #pragma unroll
   for (int t = 0; t < RING; ++t) k0[t] = p.k0[t];
   const int64_t M = (int64_t)g.n1 * g.n2;
-  const int64_t j0 = ((int64_t)blockIdx.x * kAThreads + threadIdx.x) * NP;
+  // XCD-banded block index: the row-1 neighbour of K^T z is usually read from the same XCD's L2
+  const int64_t j0 = ((int64_t)xcd_tile(blockIdx.x, gridDim.x) * kAThreads + threadIdx.x) * NP;
   if (j0 >= M) return;  // no barriers below
   const int64_t s = blockIdx.z;
   const int64_t N = M * g.n0;

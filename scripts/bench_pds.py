@@ -9,6 +9,7 @@ bytes of the fused dataflow (PD3O 76 B/voxel, CV 68 B/voxel) and at SURVEY §8(d
 rule-by-rule comparison run, default 256; 0 skips it), PXA_NSEG (axis-0 segments, default 0 = auto)."""
 import json
 import os
+import shutil
 import sys
 import time
 
@@ -16,6 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import torch
 
+import pyxu_amd.abc as pxa
 import pyxu_amd.operator as pxo
 import pyxu_amd.opt.solver as pxs
 import pyxu_amd.opt.stop as pxst
@@ -53,7 +55,9 @@ def run(algo, n, steps, fused, nseg):
     klass = pxs.PD3O if algo == "pd3o" else pxs.CondatVu
     with pxrt.Precision(pxrt.Width.SINGLE):
         s = klass(f=f, g=None, h=h, K=K, show_progress=False)
-        s.fit(x0=torch.zeros(N, device="cuda", dtype=torch.float32), stop_crit=pxst.MaxIter(1), fused=fused)
+        # MANUAL mode: m_init only (no end-of-fit writeback of the multi-GB iterates to disk)
+        s.fit(x0=torch.zeros(N, device="cuda", dtype=torch.float32), stop_crit=pxst.MaxIter(1), fused=fused,
+              mode=pxa.Mode.MANUAL)
         if s._astate.get("exception") is not None:
             raise RuntimeError("solver init failed") from s._astate["exception"]
         if fused:
@@ -79,6 +83,7 @@ def run(algo, n, steps, fused, nseg):
         line["frac_survey_8tbs"] = round(b_survey * N / (ms * 1e-3) / 8e12, 3)
         line["nseg"] = nseg
     print(json.dumps(line), flush=True)
+    shutil.rmtree(s.workdir, ignore_errors=True)
     del s, f, K, h
     torch.cuda.empty_cache()
 
