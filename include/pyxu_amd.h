@@ -78,6 +78,10 @@ int pxa_axpby(int dtype, int64_t n, double a, const void* x, double b, const voi
  * arithmetic.py:580-652; AddRule range broadcasting :843-849). */
 int pxa_axpby_bcast(int dtype, int64_t n, double a, const void* x, double b, const void* y, int64_t ny, void* out,
                     void* stream);
+/* out[r, i] = y[r, i] + s * c[r] * x[r, i] over a (rows, n) stack, c a device vector of `rows` scalars
+ * (CG.m_step on stacked right-hand sides, opt/solver/cg.py:125-153: per-row alpha / beta). */
+int pxa_axpy_rows(int dtype, int64_t rows, int64_t n, const void* c, double s, const void* x, const void* y, void* out,
+                  void* stream);
 
 /* out = a*x + b*y + c*z. */
 int pxa_lincomb3(int dtype, int64_t n, double a, const void* x, double b, const void* y, double c, const void* z,

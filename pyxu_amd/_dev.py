@@ -178,6 +178,16 @@ def axpby_bcast(a, x, b, y, out=None):
     return out
 
 
+def axpy_rows(c, s, x, y, out=None):
+    """out[r] = y[r] + s * c[r] * x[r] for x, y of shape (rows, n); c a (rows,) device vector."""
+    x, y, c = require(x, "x"), require(y, "y"), require(c, "c")
+    rows = c.numel()
+    out = empty_like(y) if out is None else out
+    check(lib.pxa_axpy_rows(dtcode(x), rows, x.numel() // max(rows, 1), ptr(c), float(s), ptr(x), ptr(y), ptr(out), stream()),
+          "pxa_axpy_rows")
+    return out
+
+
 def lincomb3(a, x, b, y, c, z, out=None):
     x, y, z = require(x), require(y), require(z)
     out = empty_like(x) if out is None else out

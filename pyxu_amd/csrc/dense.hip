@@ -27,7 +27,29 @@ __global__ void __launch_bounds__(kBlock) gemv_rows_kernel(int64_t M, int64_t N,
 #pragma unroll
     for (int j = 0; j < kBC; ++j) acc[j] = 0.0;
     if (vec) {
-      for (int64_t k = (int64_t)lane * V; k < N; k += 64 * V) {
+      // kU independent 16-B loads of the A row in flight per lane (latency hiding: one wave per row)
+      constexpr int kU = 4;
+      int64_t k = (int64_t)lane * V;
+      for (; k + (kU - 1) * 64 * V < N; k += kU * 64 * V) {
+        T av[kU][V];
+#pragma unroll
+        for (int q = 0; q < kU; ++q) *reinterpret_cast<VT*>(av[q]) = *reinterpret_cast<const VT*>(a + k + q * 64 * V);
+#pragma unroll
+        for (int q = 0; q < kU; ++q) {
+#pragma unroll
+          for (int j = 0; j < kBC; ++j) {
+            if (j < nb) {
+              T xv[V];
+              *reinterpret_cast<VT*>(xv) = *reinterpret_cast<const VT*>(X + (b0 + j) * N + k + q * 64 * V);
+              T part = T(0);
+#pragma unroll
+              for (int v = 0; v < V; ++v) part += av[q][v] * xv[v];
+              acc[j] += (double)part;
+            }
+          }
+        }
+      }
+      for (; k < N; k += 64 * V) {
         T av[V];
         *reinterpret_cast<VT*>(av) = *reinterpret_cast<const VT*>(a + k);
 #pragma unroll
@@ -79,6 +101,7 @@ __global__ void __launch_bounds__(kBlock) gemv_cols_partial_kernel(int64_t M, in
   for (int j = 0; j < kBC; ++j)
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[j][v] = T(0);
+#pragma unroll 4
   for (int64_t m = m_lo; m < m_hi; ++m) {
     T av[V];
     if (vec && n0 + V <= N) {

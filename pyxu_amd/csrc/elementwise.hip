@@ -200,6 +200,19 @@ __global__ void __launch_bounds__(kBlock) bcast_kernel(int64_t n, int64_t ny, T 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = a * x[i] + b * y[i % ny];
 }
 
+// out[r, i] = y[r, i] + s * c[r] * x[r, i]   (per-row step of CG on stacked right-hand sides, cg.py:125-153)
+template <typename T>
+__global__ void __launch_bounds__(kBlock) axpy_rows_kernel(int64_t rows, int64_t n, const T* __restrict__ c, T s,
+                                                           const T* __restrict__ x, const T* __restrict__ y,
+                                                           T* __restrict__ out) {
+  const int64_t total = rows * n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const T a = s * c[i / n];
+    out[i] = a * x[i] + y[i];
+  }
+}
+
 }  // namespace
 }  // namespace pxa
 
@@ -222,6 +235,18 @@ int pxa_axpby_bcast(int dtype, int64_t n, double a, const void* x, double b, con
   PXA_DISPATCH(dtype, T, {
     hipLaunchKernelGGL((bcast_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, ny, (T)a,
                        (const T*)x, (T)b, (const T*)y, (T*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_axpy_rows(int dtype, int64_t rows, int64_t n, const void* c, double s, const void* x, const void* y, void* out,
+                  void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && n >= 0);
+  if (rows * n == 0) return PXA_OK;
+  PXA_CHECK_ARG(c && x && y && out);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((axpy_rows_kernel<T>), dim3(grid_for(rows * n)), dim3(kBlock), 0, as_stream(stream), rows, n,
+                       (const T*)c, (T)s, (const T*)x, (const T*)y, (T*)out);
     return last_launch_status();
   });
 }

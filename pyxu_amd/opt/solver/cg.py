@@ -79,18 +79,18 @@ class CG(pxa.Solver):
             _dev.axpby(beta, p, 1.0, r, out=p)
         else:
             # stacked right-hand sides: per-row coefficients
-            A_ = self._scale_rows(alpha, x)
-            x.add_(A_ * p) if False else _dev.axpby(1.0, x, 1.0, _dev.mul(p, A_.expand_as(p).contiguous()), out=x)
+            A_ = self._scale_rows(alpha, x).reshape(-1)
+            _dev.axpy_rows(A_, 1.0, p, x, out=x)  # x += alpha p (per row)
             if np.any(rr <= eps):
                 _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
             else:
-                _dev.axpby(1.0, r, -1.0, _dev.mul(Ap, A_.expand_as(Ap).contiguous()), out=r)
+                _dev.axpy_rows(A_, -1.0, Ap, r, out=r)  # r -= alpha A p
             if self._astate["idx"] % mst["restart_rate"] == 0:
                 _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
                 _dev.axpby(0.0, p, 1.0, r, out=p)
             else:
-                B_ = self._scale_rows(_rowsq(r) / rr, p)
-                _dev.axpby(1.0, _dev.mul(p, B_.expand_as(p).contiguous()), 1.0, r, out=p)
+                B_ = self._scale_rows(_rowsq(r) / rr, p).reshape(-1)
+                _dev.axpy_rows(B_, 1.0, p, r, out=p)  # p = r + beta p (per row)
         mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
 
     def default_stop_crit(self):

@@ -378,3 +378,22 @@ def test_xp_shim_numpy_semantics():
         ref = np.linalg.norm(a.astype(np.float64), ord=ord_, axis=-1, keepdims=True)
         assert rel_err(to_NUMPY(xp.linalg.norm(t, ord=ord_, axis=-1, keepdims=True)), ref) <= 1e-6
     assert NDArrayInfo.from_obj(t) is NDArrayInfo.MI355X
+
+
+@pytest.mark.parametrize("rows", [1, 3])
+def test_cg_stacked_vs_oracle(rows):
+    """CG (opt/solver/cg.py:72-165) on an SPD dense operator, single and stacked right-hand sides
+    (per-row alpha / beta through pxa_axpy_rows), fp64, against the oracle's restatement."""
+    rng = np.random.default_rng(7 + rows)
+    N = 96
+    Kh = rng.standard_normal((64, N))
+    Ah = Kh.T @ Kh + 0.5 * np.eye(N)
+    b = rng.standard_normal((rows, N)) if rows > 1 else rng.standard_normal(N)
+    with pxrt.Precision(pxrt.Width.DOUBLE):
+        A = pxa.LinOp.from_array(D(Ah))
+        s = pxs.CG(A=A, show_progress=False)
+        s.fit(b=D(b), stop_crit=pxst.MaxIter(200) | pxst.AbsError(eps=1e-4, var="residual", f=None, norm=2, satisfy_all=True))
+        x = to_NUMPY(s.solution())
+    ref, _ = orc.cg(lambda v: v @ Ah.T, b, eps=1e-4, max_iter=200)
+    assert rel_err(x, ref) <= 1e-7  # fp64; CG amplifies reduction-order rounding (kappa ~ 600)
+    assert rel_err(x, np.linalg.solve(Ah, b.T).T) <= 1e-3
