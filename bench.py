@@ -181,8 +181,6 @@ def main():
         _dev.set_launch_timer(None)
         kern_ms = timer.mean_ms() if fused else None
 
-        # ---- dominant-kernel duration: HIP events on the launch stream, kernel-only replay of the
-        # same fused step (same buffers, same parameters) back to back.
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -223,7 +221,7 @@ def main():
             "data": "synthetic (piecewise-constant phantom, Gaussian blur, 1% noise)",
             "config": {"workload": f"PGD {n0}x{n1} Gaussian(sigma=2) deblur + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
                        "image": [n0, n1], "images_per_gpu": 1, "stop_rate": args.stop_rate,
-                       "stop_crit": "MaxIter | RelError" + (" (global, RCCL all-reduce)" if world > 1 else ""), "fused_m_step": fused, "parallelism": f"independent-images x{world}"},
+                       "stop_crit": "MaxIter | RelError" + (" (global, RCCL all-reduce)" if world > 1 else ""), "fused_m_step": fused, "parallelism": f"batch-as-axis slabs x{world} (one image per rank)"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
