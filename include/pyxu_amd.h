@@ -248,6 +248,23 @@ int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, in
                       const void* x_prev, const void* hty, void* x_new, double* partials, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * FFT LinOp (operator/linop/fft/fft.py:257-379).  `stack` arrays of complex values (interleaved
+ * re/im, i.e. the reference's view_as_real layout, (stack, *shape, 2)), transformed over the
+ * `naxes` distinct `axes` of `shape`:
+ *   inverse = 0: apply   = fftn(x, axes, norm="backward")  (exp(-2 pi i jk/n), unnormalised)
+ *   inverse = 1: adjoint = ifftn(x, axes, norm="forward")  (exp(+2 pi i jk/n), unnormalised)
+ * `out` may alias `in`.  Lengths whose prime factors are in {2, 3, 5, 7} run a mixed-radix Stockham
+ * FFT in LDS (n <= 4096 in fp32, 2048 in fp64); other lengths an exact DFT (n <= 2048);
+ * PXA_ERR_UNSUPPORTED beyond that.
+ * ------------------------------------------------------------------------------------------- */
+int pxa_fft(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse,
+            const void* in, void* out, void* stream);
+/* z[i] = x[i] + 0j (FFT(real=True).apply input, fft.py:320-330); n complex elements. */
+int pxa_real_to_complex(int dtype, int64_t n, const void* x, void* z, void* stream);
+/* x[i] = Re z[i] (FFT(real=True).adjoint output, fft.py:370-379); n complex elements. */
+int pxa_complex_real_part(int dtype, int64_t n, const void* z, void* x, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Fused primal-dual splitting iteration (replaces PD3O.m_step, opt/solver/pds.py:747-761, algo 0, and
  * CondatVu.m_step, pds.py:429-442, algo 1) for f = 1/2 ||S . - y||^2, K = Gradient over the D trailing
  * axes (forward differences, zero boundary), h = lam L1 (h_kind 0, anisotropic TV) or lam L21 over

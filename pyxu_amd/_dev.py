@@ -502,3 +502,29 @@ def pds_step(algo, pre, x, u, z, hty, x_out, u_out, z_out, work_q, work_w, nseg=
                            p(work_q), p(work_w), int(nseg), stream()), "pxa_pds_step")
     if ev is not None:
         _TIMER.end(ev)
+
+
+# ------------------------------------------------------------------ FFT
+def fft(z, shape, axes, stack, inverse, out=None):
+    """Unnormalised DFT over `axes` of `stack` complex arrays of `shape`, interleaved (re, im) real
+    tensors (pxa_fft).  inverse=False: exp(-2 pi i ..) (fftn, norm="backward"); True: exp(+..)
+    (ifftn, norm="forward")."""
+    z = require(z, "z")
+    out = empty_like(z) if out is None else out
+    check(lib.pxa_fft(dtcode(z), len(shape), i64_array(shape), len(axes), int_array(axes), int(stack), int(bool(inverse)),
+                      ptr(z), ptr(out), stream()), "pxa_fft")
+    return out
+
+
+def real_to_complex(x):
+    x = require(x, "x")
+    z = empty((*x.shape[:-1], 2 * x.shape[-1]), x)
+    check(lib.pxa_real_to_complex(dtcode(x), x.numel(), ptr(x), ptr(z), stream()), "pxa_real_to_complex")
+    return z
+
+
+def complex_real_part(z):
+    z = require(z, "z")
+    x = empty((*z.shape[:-1], z.shape[-1] // 2), z)
+    check(lib.pxa_complex_real_part(dtcode(z), x.numel(), ptr(z), ptr(x), stream()), "pxa_complex_real_part")
+    return x
