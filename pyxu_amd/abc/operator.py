@@ -479,10 +479,10 @@ class QuadraticFunc(ProxDiffFunc):
         A = Q + HomothetyOp(cst=1 / tau, dim=Q.dim)
         b = _dev.div(arr, tau)
         b = _dev.axpby(1.0, b, -1.0, c.grad(arr), out=b)
-        slvr = CG(A=A, show_progress=False)
+        slvr = CG(A=A, show_progress=False, _internal=True)
         sentinel = MaxIter(n=2 * A.dim)
         stop_crit = slvr.default_stop_crit() | sentinel
-        slvr.fit(b=b, stop_crit=stop_crit)
+        slvr._solve_inline(b=b, stop_crit=stop_crit)  # = slvr.fit(b=b, stop_crit=stop_crit), no side files
         return slvr.solution()
 
     def asloss(self, data=None):

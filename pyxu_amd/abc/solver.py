@@ -64,17 +64,24 @@ class _StoppingCriteriaComposition(StoppingCriterion):
         self._rhs.clear()
 
 
+_NULL_LOGGER = logging.getLogger("pyxu_amd.internal_solver")
+_NULL_LOGGER.addHandler(logging.NullHandler())
+_NULL_LOGGER.propagate = False
+
+
 class Solver:
     """Base class of iterative solvers (solver.py:97-718)."""
 
     def __init__(self, *, folder=None, exist_ok=False, stop_rate=1, writeback_rate=None, verbosity=None,
-                 show_progress=True, log_var=frozenset()):
+                 show_progress=True, log_var=frozenset(), _internal=False):
         self._mstate = dict()
         self._astate = dict(history=None, idx=0, log_rate=None, log_var=None, logger=None, stdout=None, stop_crit=None,
                             stop_rate=None, track_objective=None, wb_rate=None, workdir=None, mode=None, active=None,
-                            worker=None)
+                            worker=None, internal=bool(_internal))
         try:
-            if folder is None:
+            if _internal:  # sub-solver of an operator method (QuadraticFunc.prox): no workdir / log / checkpoint
+                pass
+            elif folder is None:
                 folder = plib.Path(tempfile.mkdtemp(prefix="pyxu_amd_"))
             elif (folder := plib.Path(folder).expanduser().resolve()).exists() and (not exist_ok):
                 raise FileExistsError(f"{folder} already exists.")
@@ -175,6 +182,8 @@ class Solver:
 
     def writeback(self):
         """Checkpoint ``log_var`` + history to ``workdir/data.npz`` (solver.py:562-570)."""
+        if self._astate.get("internal"):
+            return
         data, history = self.stats()
         kwargs = {k: to_NUMPY(v) for (k, v) in dict(history=history, **data).items() if (v is not None)}
         np.savez(self.datafile, **kwargs)
@@ -184,6 +193,25 @@ class Solver:
 
     def objective_func(self):
         raise NotImplementedError("No objective function defined.")
+
+    def _solve_inline(self, stop_crit=None, **kwargs):
+        """Run m_init and the stop/m_step loop on the calling thread (the iterates, stop decisions and
+        history are those of ``fit()``).  Used for sub-solvers created inside operator methods
+        (QuadraticFunc.prox -> CG, operator.py:1273-1291), where the reference's per-fit temporary
+        folder, log file, worker thread and final checkpoint are side effects nobody reads: they cost
+        milliseconds per call against a sub-millisecond iteration on the device."""
+        self._mstate.clear()
+        if stop_crit is None:
+            stop_crit = self.default_stop_crit()
+        stop_crit.clear()
+        self._astate.update(history=[], idx=0, logger=_NULL_LOGGER, stop_crit=stop_crit, track_objective=False,
+                            mode=Mode.MANUAL, active=None, worker=None, exception=None)
+        self.m_init(**kwargs)
+        while self._step():
+            pass
+        self._astate["mode"] = None
+        if self._astate.get("exception") is not None:
+            raise self._astate["exception"]
 
     # ------------------------------------------------------------------ internals
     def _fit_init(self, mode, stop_crit, track_objective):
@@ -263,13 +291,14 @@ class Solver:
                 self._mstate["objective_func"] = self.objective_func().reshape(-1)
             if _ms and ast["stop_crit"].stop(self._mstate):
                 _update_history()
-                _log()
-                _log(msg=f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
+                if not ast.get("internal"):
+                    _log()
+                    _log(msg=f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
                 self.writeback()
                 return False
             if _ms:
                 _update_history()
-            if _ml:
+            if _ml and not ast.get("internal"):
                 _log()
             if _mw:
                 self.writeback()
@@ -278,6 +307,9 @@ class Solver:
             return True
         except Exception as e:
             msg = f"[{dt.datetime.now()}] Something went wrong -> EXCEPTION RAISED"
+            if ast.get("internal"):
+                ast["exception"] = e
+                return False
             print("\n".join([msg, f"More information: {self.logfile}."]), file=sys.stderr)
             if ast["wb_rate"] is not None:
                 _, r = divmod(ast["idx"], ast["wb_rate"])

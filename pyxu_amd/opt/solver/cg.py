@@ -19,6 +19,17 @@ def _rowdot(x, y):
     return r.cpu().numpy().reshape(*x.shape[:-1], 1)
 
 
+def _rowsq_rowdot(r, p, Ap):
+    """(||r||^2, <p, Ap>) per row with ONE host synchronisation (two reductions into one buffer)."""
+    rows = r.numel() // r.shape[-1]
+    buf = _dev.empty_f64((2, rows), r)
+    _dev.row_reduce(_dev.RED_SUMSQ, r.reshape(-1, r.shape[-1]), out=buf[0])
+    _dev.row_reduce(_dev.RED_DOT, p.reshape(-1, p.shape[-1]), Ap.reshape(-1, Ap.shape[-1]), out=buf[1])
+    h = buf.cpu().numpy()
+    sh = (*r.shape[:-1], 1)
+    return h[0].reshape(sh), h[1].reshape(sh)
+
+
 class CG(pxa.Solver):
     """Solve ``A x = b`` for positive-definite ``A`` (cg.py:14-187)."""
 
@@ -49,6 +60,7 @@ class CG(pxa.Solver):
             mst["b"], mst["x"] = bb.contiguous(), xx.contiguous()
         mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(mst["x"]))
         mst["conjugate_dir"] = _dev.copy(mst["residual"])
+        self._rr = None  # ||r||^2 of the current residual, carried from the previous step's beta
 
     def _scale_rows(self, coef, v):
         """coef (..., 1) host numpy -> device tensor broadcast multiplier."""
@@ -61,8 +73,14 @@ class CG(pxa.Solver):
         mst = self._mstate
         x, r, p = mst["x"], mst["residual"], mst["conjugate_dir"]
         Ap = self._A.apply(p)
-        rr = _rowsq(r)
-        alpha = rr / _rowdot(p, Ap)
+        # ||r||^2 is the previous step's beta numerator (same reduction of the same r: identical bits);
+        # otherwise it is computed together with <p, A p> behind one host synchronisation
+        if self._rr is not None and self._rr[1] is r:
+            rr, pAp = self._rr[0], _rowdot(p, Ap)
+        else:
+            rr, pAp = _rowsq_rowdot(r, p, Ap)
+        self._rr = None
+        alpha = rr / pAp
         eps = pxrt.Width(np.dtype(str(x.dtype).replace("torch.", ""))).eps()
         if x.ndim <= 1 or x.numel() == x.shape[-1]:
             a = float(np.asarray(alpha).reshape(-1)[0])
@@ -75,7 +93,9 @@ class CG(pxa.Solver):
                 beta = 0.0
                 _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
             else:
-                beta = float((_rowsq(r) / rr).reshape(-1)[0])
+                rr_new = _rowsq(r)
+                self._rr = (rr_new, r)
+                beta = float((rr_new / rr).reshape(-1)[0])
             _dev.axpby(beta, p, 1.0, r, out=p)
         else:
             # stacked right-hand sides: per-row coefficients
@@ -89,7 +109,9 @@ class CG(pxa.Solver):
                 _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
                 _dev.axpby(0.0, p, 1.0, r, out=p)
             else:
-                B_ = self._scale_rows(_rowsq(r) / rr, p).reshape(-1)
+                rr_new = _rowsq(r)
+                self._rr = (rr_new, r)
+                B_ = self._scale_rows(rr_new / rr, p).reshape(-1)
                 _dev.axpy_rows(B_, 1.0, p, r, out=p)  # p = r + beta p (per row)
         mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
 
