@@ -85,35 +85,44 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     KT[kKT + tid] = p.k1[tid];
   }
 
-  // ---- phase 0: yk = (x - x_prev) * a + x on A, zero outside the image
+  // ---- phase 0: yk = (x - x_prev) * a + x on A, zero outside the image.  All K0 vector pairs of a
+  // thread are loaded before the first LDS store, so their latencies overlap (one round trip, not K0).
   constexpr int K0 = cdiv(L::N0, kThreads);
+  T xv[K0][V], pv[K0][V];
 #pragma unroll
   for (int k = 0; k < K0; ++k) {
     const int it = tid + k * kThreads;
     if (it < L::N0) {
       const int r = it / L::NGA, g = it - r * L::NGA;
       const int gr = ty0 - 2 * R + r, gc = tx0 - CA + V * g;
-      T xv[V], pv[V], out[V];
       if (!EDGE) {
         const unsigned off = (unsigned)(gr * n1 + gc);
-        ld_vec<T, V>(xs + off, xv);
-        ld_vec<T, V>(xps + off, pv);
+        ld_vec<T, V>(xs + off, xv[k]);
+        ld_vec<T, V>(xps + off, pv[k]);
       } else if (gr >= 0 && gr < n0 && p.vec_ok && gc >= 0 && gc + V <= n1) {
-        ld_vec<T, V>(xs + (int64_t)gr * n1 + gc, xv);
-        ld_vec<T, V>(xps + (int64_t)gr * n1 + gc, pv);
+        ld_vec<T, V>(xs + (int64_t)gr * n1 + gc, xv[k]);
+        ld_vec<T, V>(xps + (int64_t)gr * n1 + gc, pv[k]);
       } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           const bool in = gr >= 0 && gr < n0 && gc + v >= 0 && gc + v < n1;
-          xv[v] = in ? xs[(int64_t)gr * n1 + gc + v] : T(0);
-          pv[v] = in ? xps[(int64_t)gr * n1 + gc + v] : T(0);
+          xv[k][v] = in ? xs[(int64_t)gr * n1 + gc + v] : T(0);
+          pv[k][v] = in ? xps[(int64_t)gr * n1 + gc + v] : T(0);
         }
       }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K0; ++k) {
+    const int it = tid + k * kThreads;
+    if (it < L::N0) {
+      const int r = it / L::NGA, g = it - r * L::NGA;
+      T out[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        T d = xv[v] - pv[v];
+        T d = xv[k][v] - pv[k][v];
         d = d * p.a;
-        out[v] = d + xv[v];
+        out[v] = d + xv[k][v];
       }
       st_vec<T, V>(A + r * L::AP + V * g, out);
     }
