@@ -22,6 +22,13 @@ __all__ = [
     "gradient_kernels",
     "gradient_apply",
     "gradient_adjoint",
+    "diff_kernels",
+    "divergence_apply",
+    "divergence_adjoint",
+    "hessian_components",
+    "hessian_apply",
+    "hessian_adjoint",
+    "laplacian_apply",
     "l1_prox",
     "l21_apply",
     "l21_prox",
@@ -330,6 +337,97 @@ def gradient_adjoint(z, arg_shape, directions=None, scheme="forward", accuracy=1
     for j, d in enumerate(directions):
         k, c = gradient_kernels(arg_shape, d, scheme, accuracy, sampling, z.dtype)
         out = out + stencil_adjoint(z[..., j * N:(j + 1) * N], arg_shape, k, c, mode)
+    return out
+
+
+# ----------------------------------------------------------------------------- divergence / hessian / laplacian
+def diff_kernels(arg_shape, order, scheme, accuracy=1, sampling=1.0, dtype=np.float64):
+    """Separable kernels of ``PartialDerivative.finite_difference`` for a full per-axis ``order`` tuple
+    (diff.py:140-155, 501-741): FD taps of ``order[a]`` on every axis with ``order[a] > 0``."""
+    D = len(arg_shape)
+    kernels, center = [np.array([1.0], dtype=dtype)] * D, [0] * D
+    kernels = list(kernels)
+    for a in range(D):
+        if order[a] > 0:
+            _, coefs, c = fd_taps(order[a], scheme, accuracy, sampling, dtype)
+            kernels[a], center[a] = coefs, c
+    return kernels, center
+
+
+def divergence_apply(z, arg_shape, directions=None, scheme="central"):
+    """``Divergence.apply`` = Sum(axis=0) o block_diag(Gradient(direction d)) with the scheme reversed
+    (diff.py:1540-1589): forward <-> backward, central unchanged."""
+    scheme = {"central": "central", "forward": "backward", "backward": "forward"}[scheme]
+    directions = tuple(range(len(arg_shape))) if directions is None else tuple(directions)
+    N = int(np.prod(arg_shape))
+    out = 0
+    for j, d in enumerate(directions):
+        order = [0] * len(arg_shape)
+        order[d] = 1
+        k, c = diff_kernels(arg_shape, order, scheme, dtype=z.dtype)
+        out = out + stencil_apply(z[..., j * N:(j + 1) * N], arg_shape, k, c)
+    return out
+
+
+def divergence_adjoint(x, arg_shape, directions=None, scheme="central"):
+    scheme = {"central": "central", "forward": "backward", "backward": "forward"}[scheme]
+    directions = tuple(range(len(arg_shape))) if directions is None else tuple(directions)
+    parts = []
+    for d in directions:
+        order = [0] * len(arg_shape)
+        order[d] = 1
+        k, c = diff_kernels(arg_shape, order, scheme, dtype=x.dtype)
+        parts.append(stencil_adjoint(x, arg_shape, k, c))
+    return np.concatenate(parts, axis=-1)
+
+
+def hessian_components(arg_shape, directions="all"):
+    """(axes, order) pairs of ``_StackDiffHelper._check_directions_and_order`` (diff.py:1060-1111)."""
+    import itertools
+
+    D = len(arg_shape)
+    if isinstance(directions, (int, np.integer)):
+        directions = [[int(directions)] * 2]
+    elif isinstance(directions, str):
+        directions = [list(c) for c in itertools.combinations_with_replacement(range(D), 2)]
+    elif not isinstance(directions[0], (list, tuple, np.ndarray)):
+        directions = [list(directions)]
+    comps = []
+    for ds in directions:
+        axes = sorted(set(int(v) for v in ds))
+        o = 3 - len(axes)
+        order = [0] * D
+        for a in axes:
+            order[a] = o
+        comps.append((order, "central" if o == 2 else "forward"))
+    return comps
+
+
+def hessian_apply(x, arg_shape, directions="all"):
+    """``Hessian.apply``: vstack of the second-order partial derivatives (diff.py:1591-1797)."""
+    parts = []
+    for order, scheme in hessian_components(arg_shape, directions):
+        k, c = diff_kernels(arg_shape, order, scheme, dtype=x.dtype)
+        parts.append(stencil_apply(x, arg_shape, k, c))
+    return np.concatenate(parts, axis=-1)
+
+
+def hessian_adjoint(z, arg_shape, directions="all"):
+    N = int(np.prod(arg_shape))
+    out = 0
+    for j, (order, scheme) in enumerate(hessian_components(arg_shape, directions)):
+        k, c = diff_kernels(arg_shape, order, scheme, dtype=z.dtype)
+        out = out + stencil_adjoint(z[..., j * N:(j + 1) * N], arg_shape, k, c)
+    return out
+
+
+def laplacian_apply(x, arg_shape):
+    """``Laplacian.apply`` = Sum(axis=0) o Hessian(diagonal directions) (diff.py:1923-1936)."""
+    N = int(np.prod(arg_shape))
+    h = hessian_apply(x, arg_shape, [[i, i] for i in range(len(arg_shape))])
+    out = 0
+    for j in range(len(arg_shape)):
+        out = out + h[..., j * N:(j + 1) * N]
     return out
 
 

@@ -17,7 +17,7 @@ import pyxu_amd.runtime as pxrt
 from pyxu_amd import _dev
 from pyxu_amd.operator.linop.stencil import Stencil
 
-__all__ = ["PartialDerivative", "Gradient", "fd_coefficients"]
+__all__ = ["PartialDerivative", "Gradient", "Hessian", "Laplacian", "Divergence", "fd_coefficients"]
 
 
 def fd_coefficients(order, scheme, accuracy, sampling, dtype):
@@ -179,4 +179,172 @@ def Gradient(arg_shape, directions=None, diff_method="fd", mode="constant", gpu=
     op = _DiffStack(arg_shape, stencils, directions)
     op._name = "Gradient"
     op.meta = dict(sampling=samp, scheme=sch, accuracy=acc)
+    return op
+
+
+def _fd_stencil(arg_shape, order, scheme, accuracy, mode, dtype, sampling):
+    return PartialDerivative.finite_difference(arg_shape=arg_shape, order=tuple(order), scheme=scheme, accuracy=accuracy,
+                                               mode=mode, dtype=dtype, sampling=sampling)
+
+
+class _Divergence(pxa.LinOp):
+    """Sum(axis=0) o block_diag(partial derivatives) (diff.py:1576-1589): (..., K*N) -> (..., N)."""
+
+    def __init__(self, arg_shape, stencils):
+        N = int(np.prod(arg_shape))
+        super().__init__(shape=(N, len(stencils) * N))
+        self.arg_shape = tuple(arg_shape)
+        self._stencils = stencils
+        self._N = N
+        self.lipschitz = float(np.sqrt(len(stencils)) * max(float(st.lipschitz) for st in stencils))
+
+    @pxrt.enforce_precision(i="arr")
+    def apply(self, arr):
+        z = _dev.require(arr)
+        sh, N, K = z.shape[:-1], self._N, len(self._stencils)
+        z2 = z.reshape(-1, K, N)
+        out = None
+        for k, st in enumerate(self._stencils):
+            part = st.apply(z2[:, k].contiguous())
+            out = part if out is None else _dev.axpby(1.0, out, 1.0, part, out=out)  # sum over axis 0, in order
+        return out.reshape(*sh, N)
+
+    @pxrt.enforce_precision(i="arr")
+    def adjoint(self, arr):
+        x = _dev.require(arr)
+        sh, N, K = x.shape[:-1], self._N, len(self._stencils)
+        x2 = x.reshape(-1, N)
+        out = _dev.empty((x2.shape[0], K, N), x2)
+        for k, st in enumerate(self._stencils):
+            out[:, k] = st.adjoint(x2)
+        return out.reshape(*sh, K * N)
+
+    def unravel(self, arr):
+        return arr.reshape(*arr.shape[:-1], *self.arg_shape)
+
+    def ravel(self, arr):
+        return arr.reshape(*arr.shape[: -len(self.arg_shape)], -1)
+
+
+class _StencilSum(pxa.SquareOp):
+    """Sum(axis=0) o vstack(stencils) (Laplacian, diff.py:1923-1936): (..., N) -> (..., N)."""
+
+    def __init__(self, arg_shape, stencils):
+        N = int(np.prod(arg_shape))
+        super().__init__(shape=(N, N))
+        self.arg_shape = tuple(arg_shape)
+        self._stencils = stencils
+        L2 = sum(float(st.lipschitz) ** 2 for st in stencils)
+        self.lipschitz = float(np.sqrt(len(stencils)) * np.sqrt(L2))
+
+    def _sum(self, arr, adjoint):
+        x = _dev.require(arr)
+        out = None
+        for st in self._stencils:
+            part = st.adjoint(x) if adjoint else st.apply(x)
+            out = part if out is None else _dev.axpby(1.0, out, 1.0, part, out=out)
+        return out
+
+    @pxrt.enforce_precision(i="arr")
+    def apply(self, arr):
+        return self._sum(arr, adjoint=False)
+
+    @pxrt.enforce_precision(i="arr")
+    def adjoint(self, arr):
+        return self._sum(arr, adjoint=True)
+
+    def unravel(self, arr):
+        return arr.reshape(*arr.shape[:-1], *self.arg_shape)
+
+    def ravel(self, arr):
+        return arr.reshape(*arr.shape[: -len(self.arg_shape)], -1)
+
+
+def _hessian_directions(arg_shape, directions):
+    """_StackDiffHelper._check_directions_and_order (diff.py:1060-1111): canonical (axes, order) pairs."""
+    import itertools
+
+    D = len(arg_shape)
+
+    def _check(ds):
+        assert all(0 <= d <= D - 1 for d in ds), "Direction values must be between 0 and the number of dimensions in `arg_shape`."
+
+    if isinstance(directions, (int, np.integer)):
+        directions = ([int(directions), int(directions)],)
+        _check(directions[0])
+    elif isinstance(directions, str):
+        assert directions == "all", "Value for `directions` not implemented. The accepted directions types are int, tuple or a str with the value `all`."
+        directions = tuple(list(c) for c in itertools.combinations_with_replacement(range(D), 2))
+    elif not isinstance(directions[0], (list, tuple, np.ndarray)):
+        assert len(directions) == 2, "If `directions` is a tuple, it should contain two elements, corresponding to the i-th an j-th elements (dx_i and dx_j)"
+        directions = (list(directions),)
+        _check(directions[0])
+    else:
+        for ds in directions:
+            _check(ds)
+    axes = [sorted(set(int(v) for v in ds)) for ds in directions]
+    order = [3 - len(a) for a in axes]
+    return axes, order
+
+
+def Hessian(arg_shape, directions="all", diff_method="fd", mode="constant", gpu=True, dtype=None, parallel=False,
+            **diff_kwargs):
+    """Hessian (diff.py:1591-1797): vstack of second-order partial derivatives, upper triangle for "all".
+    Diagonal components default to the central scheme, off-diagonal ones to `scheme` (forward)."""
+    if diff_method != "fd":
+        raise NotImplementedError("pyxu_amd: only diff_method='fd' (finite differences) is on the hot path.")
+    arg_shape = tuple(arg_shape)
+    D = len(arg_shape)
+    axes, order = _hessian_directions(arg_shape, directions)
+    user_scheme = diff_kwargs.get("scheme", None)
+    accuracy = diff_kwargs.get("accuracy", 1)
+    sampling = diff_kwargs.get("sampling", 1.0)
+    stencils = []
+    for ax, o in zip(axes, order):
+        full = [0] * D
+        for a in ax:
+            full[a] = o
+        scheme = user_scheme if user_scheme is not None else ("central" if o == 2 else "forward")
+        stencils.append(_fd_stencil(arg_shape, full, _tuple(scheme, D) if isinstance(scheme, str) else scheme,
+                                    _tuple(accuracy, D), mode, dtype, _tuple(sampling, D)))
+    op = _DiffStack(arg_shape, stencils, [a[0] for a in axes])
+    op._name = "Hessian"
+    return op
+
+
+def Laplacian(arg_shape, directions=None, diff_method="fd", mode="constant", gpu=True, dtype=None, parallel=False,
+              **diff_kwargs):
+    """Laplacian (diff.py:1799-1936): sum of the diagonal Hessian components (central scheme)."""
+    arg_shape = tuple(arg_shape)
+    D = len(arg_shape)
+    directions = tuple(range(D)) if directions is None else tuple(np.atleast_1d(directions).tolist())
+    H = Hessian(arg_shape, directions=[(i, i) for i in range(D) if i in directions], diff_method=diff_method,
+                mode=mode, gpu=gpu, dtype=dtype, parallel=parallel, **diff_kwargs)
+    op = _StencilSum(arg_shape, H._stencils)
+    op._name = "Laplacian"
+    return op
+
+
+def Divergence(arg_shape, directions=None, diff_method="fd", mode="constant", gpu=True, dtype=None, parallel=False,
+               **diff_kwargs):
+    """Divergence (diff.py:1418-1589): Sum(axis=0) o block_diag of per-direction first derivatives,
+    with the finite-difference scheme reversed (forward <-> backward; central stays, the default)."""
+    if diff_method != "fd":
+        raise NotImplementedError("pyxu_amd: only diff_method='fd' (finite differences) is on the hot path.")
+    arg_shape = tuple(arg_shape)
+    D = len(arg_shape)
+    change = {"central": "central", "forward": "backward", "backward": "forward"}
+    scheme = diff_kwargs.get("scheme", "central")
+    scheme = change[scheme] if isinstance(scheme, str) else [change[s] for s in scheme]
+    accuracy = diff_kwargs.get("accuracy", 1)
+    sampling = diff_kwargs.get("sampling", 1.0)
+    directions = tuple(range(D)) if directions is None else tuple(np.atleast_1d(directions).tolist())
+    stencils = []
+    for d in directions:
+        order = [0] * D
+        order[d] = 1
+        stencils.append(_fd_stencil(arg_shape, order, _tuple(scheme, D) if isinstance(scheme, str) else tuple(scheme),
+                                    _tuple(accuracy, D), mode, dtype, _tuple(sampling, D)))
+    op = _Divergence(arg_shape, stencils)
+    op._name = "Divergence"
     return op

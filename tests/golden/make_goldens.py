@@ -161,6 +161,46 @@ def gen_gradient():
             )
 
 
+def gen_diffops():
+    """Divergence (diff.py:1418-1589), Laplacian (:1799-1936), Hessian (:1591-1797)."""
+    rng = np.random.default_rng(9)
+    cases = [
+        ("divergence", dict(arg_shape=(13, 17))),
+        ("divergence", dict(arg_shape=(6, 7, 9))),
+        ("divergence", dict(arg_shape=(6, 7, 9), directions=(0, 2))),
+        ("divergence", dict(arg_shape=(13, 17), scheme="forward")),
+        ("laplacian", dict(arg_shape=(13, 17))),
+        # 3-D default Laplacian / Hessian raise in the reference itself: Hessian's default diagonal scheme
+        # is the 2-tuple ("central", "central") (diff.py:1776-1777), rejected for 3 axes at diff.py:118
+        ("hessian", dict(arg_shape=(13, 17))),
+        ("hessian", dict(arg_shape=(13, 17), directions=(0, 1))),
+        ("hessian", dict(arg_shape=(13, 17), directions=1)),
+    ]
+    for w, width in WIDTHS.items():
+        dt = width.value
+        for ci, (kind, kw) in enumerate(cases):
+            arg_shape = kw["arg_shape"]
+            N = int(np.prod(arg_shape))
+            extra = {k: v for k, v in kw.items() if k in ("scheme",)}
+            with pxrt.Precision(width):
+                if kind == "divergence":
+                    op = pxo.Divergence(arg_shape=arg_shape, directions=kw.get("directions"), **extra)
+                elif kind == "laplacian":
+                    op = pxo.Laplacian(arg_shape=arg_shape)
+                else:
+                    op = pxo.Hessian(arg_shape=arg_shape, directions=kw.get("directions", "all"))
+                x = rng.standard_normal((2, op.dim)).astype(dt)
+                z = rng.standard_normal((2, op.codim)).astype(dt)
+                y, a = op.apply(x), op.adjoint(z)
+            d = kw.get("directions")
+            save(
+                f"diffop_{w}_c{ci}",
+                kind=kind, arg_shape=np.array(arg_shape),
+                directions=np.array(-1 if d is None else d), scheme=kw.get("scheme", ""),
+                x=x, y=y, z=z, adj=a,
+            )
+
+
 def gen_norms():
     rng = np.random.default_rng(3)
     for w, width in WIDTHS.items():
@@ -316,9 +356,14 @@ def gen_admm():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # e.g. `make_goldens.py diffops`: regenerate only the named families
+        for name in sys.argv[1:]:
+            globals()[f"gen_{name}"]()
+        sys.exit(0)
     gen_stencil()
     gen_convolve_gaussian()
     gen_gradient()
+    gen_diffops()
     gen_norms()
     gen_dense()
     gen_pgd()

@@ -397,3 +397,26 @@ def test_cg_stacked_vs_oracle(rows):
     ref, _ = orc.cg(lambda v: v @ Ah.T, b, eps=1e-4, max_iter=200)
     assert rel_err(x, ref) <= 1e-7  # fp64; CG amplifies reduction-order rounding (kappa ~ 600)
     assert rel_err(x, np.linalg.solve(Ah, b.T).T) <= 1e-3
+
+
+@pytest.mark.parametrize("name", golden_names("diffop_"))
+def test_diffop_golden(name):
+    """Divergence / Laplacian / Hessian (diff.py:1418-1936) through the HIP stencil path vs the
+    reference's own outputs (tests/golden/make_goldens.py gen_diffops)."""
+    g = load_golden(name)
+    dt = g["x"].dtype.type
+    kind = str(g["kind"])
+    sh = tuple(int(v) for v in g["arg_shape"])
+    d = g["directions"]
+    directions = None if (d.ndim == 0 and int(d) == -1) else (int(d) if d.ndim == 0 else tuple(int(v) for v in d))
+    with pxrt.Precision(W(dt)):
+        if kind == "divergence":
+            kw = {"scheme": str(g["scheme"])} if str(g["scheme"]) else {}
+            op = pxo.Divergence(arg_shape=sh, directions=directions, **kw)
+        elif kind == "laplacian":
+            op = pxo.Laplacian(arg_shape=sh)
+        else:
+            op = pxo.Hessian(arg_shape=sh, directions="all" if directions is None else directions)
+        assert op.shape == (g["y"].shape[-1], g["x"].shape[-1])
+        assert rel_err(to_NUMPY(op.apply(D(g["x"]))), g["y"]) <= OP_TOL[dt]
+        assert rel_err(to_NUMPY(op.adjoint(D(g["z"]))), g["adj"]) <= OP_TOL[dt]

@@ -178,3 +178,27 @@ def test_admm_trajectory(name):
         x, u, z, _ = orc.admm_dense_l1(g["A"], g["y"], float(g["lam"]), g["x0"], float(g["tau"]), n)
         assert rel_err(x, g[f"x_{n}"]) <= tol, n
         assert rel_err(u, g[f"u_{n}"]) <= tol, n
+
+
+def _diffop_args(g):
+    d = g["directions"]
+    directions = None if (d.ndim == 0 and int(d) == -1) else (int(d) if d.ndim == 0 else tuple(int(v) for v in d))
+    return str(g["kind"]), tuple(int(v) for v in g["arg_shape"]), directions, str(g["scheme"]) or None
+
+
+@pytest.mark.parametrize("name", golden_names("diffop_"))
+def test_diffops(name):
+    """Divergence / Laplacian / Hessian restatements vs the reference's own outputs (diff.py:1418-1936)."""
+    g = load_golden(name)
+    kind, sh, directions, scheme = _diffop_args(g)
+    if kind == "divergence":
+        kw = dict(directions=directions, scheme=scheme or "central")
+        y, a = orc.divergence_apply(g["x"], sh, **kw), orc.divergence_adjoint(g["z"], sh, **kw)
+    elif kind == "laplacian":
+        y = orc.laplacian_apply(g["x"], sh)
+        a = orc.laplacian_apply(g["z"], sh)  # the central second differences are symmetric
+    else:
+        dirs = "all" if directions is None else directions
+        y, a = orc.hessian_apply(g["x"], sh, dirs), orc.hessian_adjoint(g["z"], sh, dirs)
+    assert rel_err(y, g["y"]) <= _tol(y)
+    assert rel_err(a, g["adj"]) <= _tol(a)
