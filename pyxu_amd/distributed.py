@@ -19,8 +19,17 @@ steps the hot path has, and nothing else:
   ``abc/operator.py:1273-1291``) therefore costs one all-reduce per CG iteration, and the CG
   vectors (x, r, p) and their dot products stay replicated — no further communication.
 
-Message sizes are a few doubles (stop checks) or ``4·N·B`` bytes (C4: 256 KiB per right-hand side at
-N = 65 536): latency-bound on xGMI, so RCCL's default (LL/one-shot) protocols are the right choice.
+* **Halo-exchanged volume slabs** (volumes larger than one GPU; the analogue
+  of the reference's Dask ``map_overlap``, ``stencil.py:578-606``).  A volume is split along axis 0;
+  :class:`SlabLinOp` applies a rank-local operator (Stencil / Gaussian / Gradient / ...) to the
+  rank's slab padded with ``halo`` planes received from its two neighbours (point-to-point
+  send/recv, zeros beyond the volume) and crops the result; the adjoint sends the halo part of the
+  local adjoint back to the neighbours, which add it to their edge planes.  Both are exact: the
+  global operator restricted to the slab is Crop o S_local o HaloPad.
+
+Message sizes are a few doubles (stop checks), ``4·N·B`` bytes (C4: 256 KiB per right-hand side at
+N = 65 536) or a few planes (halos: R planes of n1·n2 values per neighbour): latency-bound on xGMI,
+so RCCL's default (LL/one-shot) protocols are the right choice.
 """
 import numpy as np
 
@@ -36,6 +45,9 @@ __all__ = [
     "ShardedRelError",
     "ShardedAbsError",
     "RowShardedLinOp",
+    "halo_pad",
+    "halo_reduce",
+    "SlabLinOp",
 ]
 
 
@@ -174,3 +186,150 @@ def RowShardedLinOp(mat_local, M, group=None, enable_warnings=True):
         adjoint=op_adjoint,
     )
     return op
+
+
+# ------------------------------------------------------------------ halo-exchanged slabs
+def _p2p(sends, recvs, group=None):
+    """Point-to-point exchange: sends = [(tensor, peer)], recvs = [(buffer, peer)].  Device tensors
+    go through RCCL directly; with gloo they are staged through the host."""
+    dist = _dist()
+    if not sends and not recvs:
+        return
+    host = _host_backend(group)
+    stage = lambda t: t.cpu().contiguous() if (host and t.is_cuda) else t.contiguous()  # noqa: E731
+    s_bufs = [(stage(t), peer) for t, peer in sends]
+    r_bufs = [(stage(b) if (host and b.is_cuda) else b, b, peer) for b, peer in recvs]
+    ops = [dist.P2POp(dist.isend, t, _global_rank(peer, group), group) for t, peer in s_bufs]
+    ops += [dist.P2POp(dist.irecv, h, _global_rank(peer, group), group) for h, _, peer in r_bufs]
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    for h, b, _ in r_bufs:
+        if h is not b:
+            b.copy_(h)
+
+
+def _global_rank(r, group):
+    if group is None:
+        return r
+    return _dist().get_global_rank(group, r)
+
+
+def _accumulate(dst, src):
+    """dst += src (contiguous views).  Device tensors: the HIP element-wise kernel; host tensors only
+    occur in the gloo CPU tests of this exchange logic."""
+    if dst.is_cuda:
+        from pyxu_amd import _dev
+
+        _dev.axpby(1.0, dst, 1.0, src, out=dst)
+    else:
+        dst.add_(src)
+
+
+def halo_pad(x, lo, hi, group=None):
+    """x: (S, nl, M) slab of axis-0 planes owned by this rank -> (S, lo + nl + hi, M) with the last
+    `lo` planes of rank-1 in front, the first `hi` planes of rank+1 behind (zeros beyond the volume)."""
+    import torch
+
+    rank, w = world(group)
+    S, nl, M = x.shape
+    if nl < max(lo, hi) and w > 1:
+        raise ValueError(f"slab of {nl} planes is thinner than the halo ({lo}, {hi})")
+    left = torch.zeros((S, lo, M), dtype=x.dtype, device=x.device)
+    right = torch.zeros((S, hi, M), dtype=x.dtype, device=x.device)
+    sends, recvs = [], []
+    if rank > 0:
+        if hi:
+            sends.append((x[:, :hi], rank - 1))
+        if lo:
+            recvs.append((left, rank - 1))
+    if rank < w - 1:
+        if lo:
+            sends.append((x[:, nl - lo:], rank + 1))
+        if hi:
+            recvs.append((right, rank + 1))
+    _p2p(sends, recvs, group)
+    return torch.cat([left, x, right], dim=1)
+
+
+def halo_reduce(xp, lo, hi, group=None):
+    """Adjoint of halo_pad: xp (S, lo + nl + hi, M) -> (S, nl, M), the halo planes sent back to the
+    neighbours that own them and added to their edge planes (dropped beyond the volume)."""
+    import torch
+
+    rank, w = world(group)
+    S, pl, M = xp.shape
+    nl = pl - lo - hi
+    out = xp[:, lo:lo + nl].contiguous()
+    from_left = torch.empty((S, hi, M), dtype=xp.dtype, device=xp.device) if (rank > 0 and hi) else None
+    from_right = torch.empty((S, lo, M), dtype=xp.dtype, device=xp.device) if (rank < w - 1 and lo) else None
+    sends, recvs = [], []
+    if rank > 0:
+        if lo:
+            sends.append((xp[:, :lo], rank - 1))  # my left halo = rank-1's last lo planes
+        if hi:
+            recvs.append((from_left, rank - 1))  # rank-1's right halo = my first hi planes
+    if rank < w - 1:
+        if hi:
+            sends.append((xp[:, lo + nl:], rank + 1))
+        if lo:
+            recvs.append((from_right, rank + 1))
+    _p2p(sends, recvs, group)
+    for s in range(S):  # per stack row: contiguous plane ranges
+        if from_left is not None:
+            _accumulate(out[s, :hi], from_left[s])
+        if from_right is not None:
+            _accumulate(out[s, nl - lo:], from_right[s])
+    return out
+
+
+class SlabLinOp(pxa.LinOp):
+    """This rank's slab (axis 0, :func:`shard_range`) of a linear operator on a volume of
+    ``global_shape``, evaluated with halo exchange (module docstring).
+
+    ``make_local(padded_shape)`` builds the rank-local operator on the padded slab
+    ``(lo + nl + hi, *global_shape[1:])`` with zero-boundary semantics (e.g.
+    ``lambda sh: pyxu_amd.operator.Gaussian(sh, sigma=2)`` or ``Gradient(sh)``); its output may hold
+    K blocks of the padded shape (Gradient: K = D, direction-major).  ``halo = (lo, hi)`` must cover
+    the operator's reach along axis 0 (planes before / after the output plane).  Input: the rank's
+    ``(..., nl * M)`` slab; output ``(..., K * nl * M)``, direction-major like the local operator.
+    """
+
+    def __init__(self, make_local, global_shape, halo, group=None):
+        global_shape = tuple(int(v) for v in global_shape)
+        rank, w = world(group)
+        a, b = shard_range(global_shape[0], rank, w)
+        self._nl, self._M = b - a, int(np.prod(global_shape[1:]))
+        self._halo = (int(halo[0]), int(halo[1]))
+        self._group = group
+        self._rows = (a, b)
+        pshape = (self._halo[0] + self._nl + self._halo[1], *global_shape[1:])
+        self._local = make_local(pshape)
+        pdim = int(np.prod(pshape))
+        if self._local.dim != pdim or self._local.codim % pdim != 0:
+            raise ValueError("make_local must return an operator on the padded slab with K * padded outputs")
+        self._K = self._local.codim // pdim
+        super().__init__(shape=(self._K * self._nl * self._M, self._nl * self._M))
+        self.lipschitz = getattr(self._local, "lipschitz", np.inf)
+
+    def _stack(self, arr):
+        sh = arr.shape[:-1]
+        return sh, int(np.prod(sh)) if len(sh) else 1
+
+    @pxrt.enforce_precision(i="arr")
+    def apply(self, arr):
+        (lo, hi), nl, M, K = self._halo, self._nl, self._M, self._K
+        sh, S = self._stack(arr)
+        xp = halo_pad(arr.reshape(S, nl, M), lo, hi, self._group)
+        y = self._local.apply(xp.reshape(S, -1)).reshape(S, K, lo + nl + hi, M)
+        return y[:, :, lo:lo + nl].contiguous().reshape(*sh, K * nl * M)
+
+    @pxrt.enforce_precision(i="arr")
+    def adjoint(self, arr):
+        import torch
+
+        (lo, hi), nl, M, K = self._halo, self._nl, self._M, self._K
+        sh, S = self._stack(arr)
+        yp = torch.zeros((S, K, lo + nl + hi, M), dtype=arr.dtype, device=arr.device)
+        yp[:, :, lo:lo + nl] = arr.reshape(S, K, nl, M)
+        xp = self._local.adjoint(yp.reshape(S, -1)).reshape(S, lo + nl + hi, M)
+        return halo_reduce(xp, lo, hi, self._group).reshape(*sh, nl * M)

@@ -113,7 +113,99 @@ def row_sharded_normal_cg(rank, world, M, N, iters):
     return dict(x=x, n=n)
 
 
+class _OracleVolumeOp:
+    """Host stand-in for a pyxu_amd volume operator (the HIP kernels need a GPU): Gaussian blur on all
+    axes ("blur") or the forward-difference Gradient ("grad") through the CPU oracle."""
+
+    def __init__(self, shape, kind, sigma=1.0):
+        import oracle as orc
+
+        self.shape, self.kind = tuple(shape), kind
+        n = int(np.prod(shape))
+        self.dim = n
+        self.codim = n * (len(shape) if kind == "grad" else 1)
+        taps, c = orc.gaussian_taps(sigma, 3.0, np.float64)
+        self._blur = dict(kernel=[taps] * len(shape), center=[c] * len(shape))
+
+    def apply(self, x):
+        import torch
+
+        import oracle as orc
+
+        a = x.numpy()
+        y = orc.gradient_apply(a, self.shape) if self.kind == "grad" else orc.stencil_apply(a, self.shape, **self._blur)
+        return torch.from_numpy(np.ascontiguousarray(y))
+
+    def adjoint(self, z):
+        import torch
+
+        import oracle as orc
+
+        a = z.numpy()
+        x = orc.gradient_adjoint(a, self.shape) if self.kind == "grad" else orc.stencil_adjoint(a, self.shape, **self._blur)
+        return torch.from_numpy(np.ascontiguousarray(x))
+
+
+def slab_halo_oracle(rank, world, shape, kind, halo, sigma=1.0):
+    """SlabLinOp exchange logic on the host: apply / adjoint of this rank's slab (halo-padded local
+    operator, cropped / halo-reduced), gathered along axis 0."""
+    import torch
+
+    import pyxu_amd.distributed as pd
+    import pyxu_amd.runtime as pxrt
+
+    rng = np.random.default_rng(21)
+    N = int(np.prod(shape))
+    K = len(shape) if kind == "grad" else 1
+    x = rng.standard_normal((2, N))
+    y = rng.standard_normal((2, K * N))
+    lo, hi = pd.shard_range(shape[0])
+    M = N // shape[0]
+    with pxrt.Precision(pxrt.Width.DOUBLE):
+        op = pd.SlabLinOp(lambda sh: _OracleVolumeOp(sh, kind, sigma), shape, halo)
+        xl = torch.from_numpy(x.reshape(2, shape[0], M)[:, lo:hi].reshape(2, -1).copy())
+        yl = torch.from_numpy(y.reshape(2, K, shape[0], M)[:, :, lo:hi].reshape(2, -1).copy())
+        ya = op.apply(xl).reshape(2, K, hi - lo, M)
+        xa = op.adjoint(yl).reshape(2, hi - lo, M)
+    Y = pd.gather_slabs(ya.permute(2, 0, 1, 3).contiguous(), shape[0]).permute(1, 2, 0, 3).reshape(2, K * N)
+    X = pd.gather_slabs(xa.permute(1, 0, 2).contiguous(), shape[0]).permute(1, 0, 2).reshape(2, N)
+    return dict(apply=Y.numpy(), adjoint=X.numpy(), x=x, y=y)
+
+
 # ------------------------------------------------------------------ GPU scenarios (real HIP path)
+def gpu_slab_ops(rank, world, shape):
+    """SlabLinOp on the MI355X with the real HIP Gaussian / Gradient vs the unsharded operators."""
+    import torch
+
+    torch.cuda.set_device(0)
+    import pyxu_amd.distributed as pd
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd.util import to_device, to_NUMPY
+
+    rng = np.random.default_rng(23)
+    N = int(np.prod(shape))
+    M = N // shape[0]
+    lo, hi = pd.shard_range(shape[0])
+    out = {}
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        cases = {"blur": (lambda sh: pxo.Gaussian(arg_shape=sh, sigma=1.5), (5, 5), 1),
+                 "grad": (lambda sh: pxo.Gradient(arg_shape=sh), (0, 1), len(shape))}
+        for name, (make, halo, K) in cases.items():
+            x = rng.standard_normal((2, N)).astype(np.float32)
+            y = rng.standard_normal((2, K * N)).astype(np.float32)
+            op = pd.SlabLinOp(make, shape, halo)
+            xl = to_device(x.reshape(2, shape[0], M)[:, lo:hi].reshape(2, -1).copy())
+            yl = to_device(y.reshape(2, K, shape[0], M)[:, :, lo:hi].reshape(2, -1).copy())
+            ya = op.apply(xl).reshape(2, K, hi - lo, M)
+            xa = op.adjoint(yl).reshape(2, hi - lo, M)
+            Y = pd.gather_slabs(ya.permute(2, 0, 1, 3).contiguous(), shape[0]).permute(1, 2, 0, 3).reshape(2, K * N)
+            X = pd.gather_slabs(xa.permute(1, 0, 2).contiguous(), shape[0]).permute(1, 0, 2).reshape(2, N)
+            full = make(shape)
+            out[name] = dict(apply=to_NUMPY(Y), adjoint=to_NUMPY(X), apply_ref=to_NUMPY(full.apply(to_device(x))),
+                             adjoint_ref=to_NUMPY(full.adjoint(to_device(y))))
+    return out
+
 def gpu_batched_pgd(rank, world, B, sh, iters, eps):
     """C5 on the MI355X: each rank solves its slab with the fused kernel; ShardedRelError."""
     import torch
