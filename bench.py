@@ -137,10 +137,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    # one rank per GPU; the modulo only matters for rehearsals with more ranks than GPUs (gloo)
+    dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     distributed = world > 1
     if distributed:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+        backend = os.environ.get("PXA_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI; gloo for rehearsals
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend=backend)
     if not pyxu_amd.native_loaded():
         raise RuntimeError("libpyxu_amd.so not loaded")
 
