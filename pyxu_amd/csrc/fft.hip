@@ -84,12 +84,29 @@ __device__ inline void dft8(Cx<T>* v) {
     v[k + 4] = csub(e[k], p[k]);
   }
 }
+// e^{-+2 pi i m / R} for the odd radices, as literal constants (no sincos per butterfly)
+template <typename T, bool INV, int R>
+__device__ inline Cx<T> root(int m) {
+  constexpr double c3[2] = {-0.5, 0.86602540378443864676};
+  constexpr double c5[4] = {0.30901699437494742410, 0.95105651629515357212, -0.80901699437494742410,
+                            0.58778525229247312917};
+  constexpr double c7[6] = {0.62348980185873353053, 0.78183148246802980871, -0.22252093395631440429,
+                            0.97492791218182360702, -0.90096886790241912624, 0.43388373911755812048};
+  if (m == 0) return Cx<T>{T(1), T(0)};
+  const int h = m <= R / 2 ? m : R - m;  // cos symmetric, sin antisymmetric
+  const double* t = R == 3 ? c3 : (R == 5 ? c5 : c7);
+  const T c = (T)t[2 * (h - 1)];
+  T sn = (T)t[2 * (h - 1) + 1];
+  if (m > R / 2) sn = -sn;
+  return Cx<T>{c, INV ? sn : -sn};
+}
+
 // odd prime radix: direct DFT with the R roots of unity
 template <typename T, bool INV, int R>
 __device__ inline void dft_odd(Cx<T>* v) {
   Cx<T> w[R];
 #pragma unroll
-  for (int m = 0; m < R; ++m) w[m] = twiddle<T, INV>(m, R);
+  for (int m = 0; m < R; ++m) w[m] = root<T, INV, R>(m);
   Cx<T> out[R];
 #pragma unroll
   for (int q = 0; q < R; ++q) {
@@ -124,9 +141,15 @@ __device__ inline void stage(const Cx<T>* src, Cx<T>* dst, int n, int ns, int lp
     Cx<T>* d = dst + l * n;
     Cx<T> v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      v[r] = s[j + r * nr];
-      if (r > 0 && ns > 1) v[r] = cmul(v[r], twiddle<T, INV>(r * k, ns * R));
+    for (int r = 0; r < R; ++r) v[r] = s[j + r * nr];
+    if (ns > 1) {  // w^r from one sincospi: w^1, then successive products (error ~ r ulp)
+      const Cx<T> w1 = twiddle<T, INV>(k, ns * R);
+      Cx<T> w = w1;
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        v[r] = cmul(v[r], w);
+        if (r + 1 < R) w = cmul(w, w1);
+      }
     }
     if constexpr (R == 2) dft2<T, INV>(v);
     else if constexpr (R == 4) dft4<T, INV>(v);
