@@ -161,57 +161,68 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     if (it < L::NPB) {
       const int a = it % L::NA, cb = it / L::NA;
       const int c0 = CW * cb;  // first output column of the item (tile-relative)
-      // yk window: rows V a - 1 .. V a + V (V + 2), cols c0 - 1 .. c0 + CW (CW + 2)
-      T Y[V + 2][CW + 2];
-#pragma unroll
-      for (int r = 0; r < V + 2; ++r) {
+      // yk window rows V a - 1 .. V a + V, cols c0 - 1 .. c0 + CW, streamed two rows at a time so
+      // that the TV stencil keeps ~20 values live instead of the whole (V+2) x (CW+2) window
+      auto yrow = [&](int r, T(&y)[CW + 2]) {
         const T* arow = A + (V * a - 1 + r + 2 * R) * L::AP + CA + c0;
         if constexpr (CW == 2) {
           T lo[2], mid[2], hi[2];
           ld_pair<T>(arow - 2, lo);
           ld_pair<T>(arow, mid);
           ld_pair<T>(arow + 2, hi);
-          Y[r][0] = lo[1];
-          Y[r][1] = mid[0];
-          Y[r][2] = mid[1];
-          Y[r][3] = hi[0];
+          y[0] = lo[1];
+          y[1] = mid[0];
+          y[2] = mid[1];
+          y[3] = hi[0];
         } else {
 #pragma unroll
-          for (int c = 0; c < CW + 2; ++c) Y[r][c] = arow[c - 1];
+          for (int c = 0; c < CW + 2; ++c) y[c] = arow[c - 1];
         }
-      }
+      };
+      // q = w v at window row r (0..V), cols c = 0..CW, from yk rows r (yr) and r + 1 (yn)
+      auto qrow = [&](int r, const T(&yr)[CW + 2], const T(&yn)[CW + 2], T(&q0)[CW + 1], T(&q1)[CW + 1]) {
+#pragma unroll
+        for (int c = 0; c <= CW; ++c) {
+          const T v0 = p.g0a * yr[c] + p.g0b * yn[c];
+          const T v1 = p.g1a * yr[c] + p.g1b * yr[c + 1];
+          T w = tv_weight<T>(v0 * v0 + v1 * v1, p.lam, p.mu, p.inv_mu);
+          if (EDGE) {
+            const int gr = ty0 + V * a - 1 + r, gc = tx0 + c0 - 1 + c;
+            if (!(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) w = T(0);
+          }
+          q0[c] = v0 * w;
+          q1[c] = v1 * w;
+        }
+      };
       T yc[V][CW];  // yk at the item's own pixels
-#pragma unroll
-      for (int u = 0; u < V; ++u)
-#pragma unroll
-        for (int w = 0; w < CW; ++w) yc[u][w] = Y[u + 1][w + 1];
       T tv[V][CW];
-      if (p.tv) {
-        // q at rows V a - 1 .. V a + V - 1 (index r = 0..V), cols c0 - 1 .. c0 + CW - 1 (index c = 0..CW)
-        T q0[V + 1][CW + 1], q1[V + 1][CW + 1];
+      {
+        T yr[CW + 2], yn[CW + 2];
+        yrow(0, yr);
+        yrow(1, yn);
+        T qp0[CW + 1], qp1[CW + 1];
+        if (p.tv) qrow(0, yr, yn, qp0, qp1);
 #pragma unroll
-        for (int r = 0; r <= V; ++r)
+        for (int u = 0; u < V; ++u) {
 #pragma unroll
-          for (int c = 0; c <= CW; ++c) {
-            const T v0 = p.g0a * Y[r][c] + p.g0b * Y[r + 1][c];
-            const T v1 = p.g1a * Y[r][c] + p.g1b * Y[r][c + 1];
-            T w = tv_weight<T>(v0 * v0 + v1 * v1, p.lam, p.mu, p.inv_mu);
-            if (EDGE) {
-              const int gr = ty0 + V * a - 1 + r, gc = tx0 + c0 - 1 + c;
-              if (!(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) w = T(0);
+          for (int c = 0; c < CW + 2; ++c) yr[c] = yn[c];  // window row u + 1
+          yrow(u + 2, yn);
+#pragma unroll
+          for (int w = 0; w < CW; ++w) yc[u][w] = yr[w + 1];
+          if (p.tv) {
+            T qc0[CW + 1], qc1[CW + 1];
+            qrow(u + 1, yr, yn, qc0, qc1);
+            // Grad^T q: flipped 2-tap adjoints, (+1/h tap at i - e_d) then (-1/h tap at i), summed over d
+#pragma unroll
+            for (int w = 0; w < CW; ++w) {
+              const T t0 = p.g0b * qp0[w + 1] + p.g0a * qc0[w + 1];
+              const T t1 = p.g1b * qc1[w] + p.g1a * qc1[w + 1];
+              tv[u][w] = t0 + t1;
             }
-            q0[r][c] = v0 * w;
-            q1[r][c] = v1 * w;
-          }
-        // Grad^T q: flipped 2-tap adjoints, (+1/h tap at i - e_d) then (-1/h tap at i), summed over d
 #pragma unroll
-        for (int u = 0; u < V; ++u)
-#pragma unroll
-          for (int w = 0; w < CW; ++w) {
-            const T t0 = p.g0b * q0[u][w + 1] + p.g0a * q0[u + 1][w + 1];
-            const T t1 = p.g1b * q1[u + 1][w] + p.g1a * q1[u + 1][w + 1];
-            tv[u][w] = t0 + t1;
+            for (int c = 0; c <= CW; ++c) qp0[c] = qc0[c];
           }
+        }
       }
       T acc[CW][V];            // acc[w][u]: column c0 + w, row V a + u
       sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g1, acc);
