@@ -319,7 +319,8 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
   for (int k = 0; k < KB; ++k) {
     const int it = tid + k * kThreads;
     if (it < L::NPB) {
-      const int a = it % L::NA, cb = it / L::NA;
+      int a, cb;
+      L::pass_b_item(it, a, cb);
       const int c0 = CW * cb;
       T acc[CW][V];
       sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g2, acc);

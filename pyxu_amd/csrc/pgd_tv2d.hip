@@ -159,7 +159,8 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   for (int k = 0; k < KB; ++k) {
     const int it = tid + k * kThreads;
     if (it < L::NPB) {
-      const int a = it % L::NA, cb = it / L::NA;
+      int a, cb;
+      L::pass_b_item(it, a, cb);
       const int c0 = CW * cb;  // first output column of the item (tile-relative)
       // yk window rows V a - 1 .. V a + V, cols c0 - 1 .. c0 + CW, streamed two rows at a time so
       // that the TV stencil keeps ~20 values live instead of the whole (V+2) x (CW+2) window

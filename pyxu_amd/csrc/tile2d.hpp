@@ -35,7 +35,20 @@ struct Layout {
     return p;
   }
   static constexpr int AP = pad_to(AC, 32, 28);   // A pitch (elements)
-  static constexpr int PTP = F32 ? TY + 16 : TY;  // PT pitch (elements)
+  static constexpr int PTP = F32 ? TY + 8 : TY;  // PT pitch (elements): conflict-free with pass_b_item
+  // pass B item of linear index `it`: row group a, column item cb.  fp32: each 32-lane half of a wave
+  // takes 4 row groups x 8 column items, so that both the G1 sweep (ds_read_b128 of PT) and the yk
+  // window reads of the TV stencil (ds_read_b64 of A, row groups 4 apart collide mod 64 banks) are
+  // conflict-free under the MI355X_MICROARCH.md bank model (scripts/ldsbank.py)
+  __device__ static inline void pass_b_item(int it, int& a, int& cb) {
+    if constexpr (F32 && NA == 8) {
+      a = (it & 3) + 4 * ((it >> 5) & 1);
+      cb = ((it >> 2) & 7) + 8 * (it >> 6);
+    } else {
+      a = it % NA;
+      cb = it / NA;
+    }
+  }
   static constexpr int N0 = AR * NGA, NPA = NA * NB, NPB = NA * NCB;
   static constexpr size_t BYTES = (size_t)(AR * AP + AC * PTP + 2 * kKT) * sizeof(T);
 };
