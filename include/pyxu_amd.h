@@ -259,6 +259,10 @@ int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, in
  * ------------------------------------------------------------------------------------------- */
 int pxa_fft(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse,
             const void* in, void* out, void* stream);
+/* out[i] = a[i] * b[i % nb] over n complex elements (b conjugated if conj_b): the spectrum product of
+ * the FFT path of large zero-boundary stencils (Stencil.apply/adjoint, stencil.py:441-461). */
+int pxa_complex_mul(int dtype, int64_t n, int64_t nb, const void* a, const void* b, int conj_b, void* out,
+                    void* stream);
 /* z[i] = x[i] + 0j (FFT(real=True).apply input, fft.py:320-330); n complex elements. */
 int pxa_real_to_complex(int dtype, int64_t n, const void* x, void* z, void* stream);
 /* x[i] = Re z[i] (FFT(real=True).adjoint output, fft.py:370-379); n complex elements. */

@@ -528,3 +528,12 @@ def complex_real_part(z):
     x = empty((*z.shape[:-1], z.shape[-1] // 2), z)
     check(lib.pxa_complex_real_part(dtcode(z), x.numel(), ptr(z), ptr(x), stream()), "pxa_complex_real_part")
     return x
+
+
+def complex_mul(a, b, conj_b=False, out=None):
+    """out = a * b (b broadcast over a's leading stack) for interleaved complex tensors."""
+    a, b = require(a, "a"), require(b, "b")
+    out = empty_like(a) if out is None else out
+    check(lib.pxa_complex_mul(dtcode(a), a.numel() // 2, b.numel() // 2, ptr(a), ptr(b), int(bool(conj_b)), ptr(out),
+                              stream()), "pxa_complex_mul")
+    return out

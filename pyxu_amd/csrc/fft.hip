@@ -319,6 +319,18 @@ __global__ void __launch_bounds__(kBlock) complex_real_kernel(int64_t n, const C
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = z[i].re;
 }
 
+// out[i] = a[i] * b[i % nb] (b conjugated if CONJ): spectrum product of an FFT convolution
+template <typename T, bool CONJ>
+__global__ void __launch_bounds__(kBlock) cmul_kernel(int64_t n, int64_t nb, const Cx<T>* __restrict__ a,
+                                                      const Cx<T>* __restrict__ b, Cx<T>* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    Cx<T> w = b[i % nb];
+    if (CONJ) w.im = -w.im;
+    out[i] = cmul(a[i], w);
+  }
+}
+
 }  // namespace
 }  // namespace pxa
 
@@ -329,6 +341,22 @@ extern "C" {
 int pxa_fft(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse,
             const void* in, void* out, void* stream) {
   PXA_DISPATCH(dtype, T, return fft_entry<T>(ndim, shape, naxes, axes, stack, inverse, in, out, as_stream(stream)));
+}
+
+int pxa_complex_mul(int dtype, int64_t n, int64_t nb, const void* a, const void* b, int conj_b, void* out,
+                    void* stream) {
+  PXA_CHECK_ARG(n >= 0 && nb >= 1);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(a && b && out);
+  PXA_DISPATCH(dtype, T, {
+    if (conj_b)
+      hipLaunchKernelGGL((cmul_kernel<T, true>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, nb,
+                         (const Cx<T>*)a, (const Cx<T>*)b, (Cx<T>*)out);
+    else
+      hipLaunchKernelGGL((cmul_kernel<T, false>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, nb,
+                         (const Cx<T>*)a, (const Cx<T>*)b, (Cx<T>*)out);
+    return last_launch_status();
+  });
 }
 
 int pxa_real_to_complex(int dtype, int64_t n, const void* x, void* z, void* stream) {

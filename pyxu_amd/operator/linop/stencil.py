@@ -164,12 +164,74 @@ class Stencil(pxa.SquareOp):
             warnings.warn("Computation may not be performed at the requested precision.", PrecisionWarning)
         return arr.to(pxrt.Width(self._dtype).torch)
 
+    # ------------------------------------------------------------------ FFT path (large N-D kernels)
+    FFT_MIN_TAPS = 256  # non-separable constant-mode kernels with at least this many taps go through the FFT
+
+    @staticmethod
+    def _smooth(n):
+        """Smallest 2^a 3^b 5^c 7^d >= n (lengths the mixed-radix FFT kernel runs in LDS)."""
+        m = n
+        while True:
+            k = m
+            for p in (2, 3, 5, 7):
+                while k % p == 0:
+                    k //= p
+            if k == 1:
+                return m
+            m += 1
+
+    def _fft_plan(self, x):
+        """Linear correlation through an FFT of the zero-padded signal (no wrap-around: L >= n + K - 1):
+        y = Crop_[0,n)( IFFT( FFT(Pad(x)) * FFT(k_circ) ) / prod(L) ) with k_circ[(c - j) mod L] = k[j];
+        the adjoint multiplies by the conjugate spectrum.  Returns the cached plan or None."""
+        cache = getattr(self, "_fft_cache", None)
+        key = str(x.dtype)
+        if cache is not None and key in cache:
+            return cache[key]
+        plan = None
+        st = self._st_fw[0]
+        K = st.kernel.shape
+        if (not self._separable and all(m == "constant" for m in self._mode) and int(np.prod(K)) >= self.FFT_MIN_TAPS):
+            L = tuple(self._smooth(n + k - 1) for n, k in zip(self._arg_shape, K))
+            lim = 4096 if x.dtype == pxrt.Width.SINGLE.torch else 2048
+            if max(L) <= lim and len(L) <= 8:
+                import torch
+
+                k = np.asarray(st.kernel, dtype=np.float64)
+                c = np.asarray(st.center, dtype=int)
+                kc = np.zeros(L, dtype=np.float64)
+                idx = np.indices(K).reshape(len(K), -1)
+                tgt = tuple(((c[:, None] - idx) % np.array(L)[:, None]))
+                np.add.at(kc, tgt, k.reshape(-1))
+                kc /= float(np.prod(L))  # the unnormalised inverse FFT's 1/prod(L), folded into the spectrum
+                kd = torch.from_numpy(kc.reshape(-1)).to(device=x.device, dtype=x.dtype)
+                spec = _dev.fft(_dev.real_to_complex(kd), L, tuple(range(len(L))), 1, inverse=False)
+                plan = dict(L=L, spec=spec)
+        if cache is None:
+            cache = self._fft_cache = {}
+        cache[key] = plan
+        return plan
+
+    def _run_fft(self, x, S, plan, adjoint):
+        L, n = plan["L"], self._arg_shape
+        D = len(L)
+        hi = [l - m for l, m in zip(L, n)]
+        xp = _dev.pad(x, S, n, [0] * D, hi, ("constant",) * D).reshape(S, -1)
+        z = _dev.fft(_dev.real_to_complex(xp), L, tuple(range(D)), S, inverse=False)
+        z = _dev.complex_mul(z, plan["spec"], conj_b=adjoint, out=z)
+        z = _dev.fft(z, L, tuple(range(D)), S, inverse=True, out=z)
+        yp = _dev.complex_real_part(z)
+        return _dev.trim(yp, S, L, [0] * D, hi, embed=False).reshape(S, -1)
+
     def _run(self, arr, specs, adjoint):
         x = _dev.require(self._cast_warn(arr))
         sh = x.shape[:-1]
         S = int(np.prod(sh)) if len(sh) else 1
         N = self.dim
         x = x.reshape(S, N)
+        plan = self._fft_plan(x)
+        if plan is not None:
+            return self._run_fft(x, S, plan, adjoint).reshape(*sh, N)
         y = _dev.empty((S, N), x)
         if all(m == "constant" for m in self._mode):
             if self._separable:

@@ -56,6 +56,18 @@ def main():
                         "gbs": round(8 * D * N / (ms * 1e-3) / 1e9, 1)})
             del z, x
             torch.cuda.empty_cache()
+    with pxrt.Precision(pxrt.Width.SINGLE):  # large non-separable zero-boundary stencil: FFT path vs direct taps
+        for sh, K in [((2048, 2048), (31, 31)), ((2048, 2048), (15, 15)), ((256, 256, 256), (9, 9, 9))]:
+            N = int(np.prod(sh))
+            k = np.random.default_rng(0).standard_normal(K)
+            x = torch.randn(N, device="cuda", dtype=torch.float32, generator=g)
+            for path in ("fft", "direct"):
+                op = pxo.Stencil(arg_shape=sh, kernel=k, center=tuple(s // 2 for s in K))
+                if path == "direct":
+                    op.FFT_MIN_TAPS = 1 << 60
+                ms = timed(lambda: op.apply(x), reps=5 if path == "direct" and N * k.size > 1e10 else 20)
+                out.append({"op": f"Stencil.apply[{path}]", "shape": sh, "kernel": list(K), "ms": round(ms, 4),
+                            "gbs": round(8 * N / (ms * 1e-3) / 1e9, 1)})
     for line in out:
         line["shape"] = list(line["shape"])
         print(json.dumps(line), flush=True)
