@@ -174,12 +174,16 @@ def main():
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
-        timer = _dev.LaunchTimer(window=10)
+        # one HIP-event window per run of back-to-back fused launches, closed only where other device work
+        # (the stop check) is enqueued: an event record between two launches costs a ~11 us bubble
+        # (rocprofv3 trace, r01c), so per-10-launch windows would tax the timed step by ~1 us
+        timer = _dev.LaunchTimer(window=10**9)
         if not args.no_kernel_timer:
             _dev.set_launch_timer(timer)  # HIP-event windows around the fused-step launches, on their stream
         t0 = time.perf_counter()
         for _ in range(args.steps):
             next(gen)
+        timer.interrupt()  # close the last window right behind the last launch (before the host sync)
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()

@@ -148,6 +148,7 @@ class Solver:
                 return
 
     def stats(self):
+        self._flush_records()
         history = self._astate["history"]
         if history is not None:
             history = np.concatenate(history, dtype=history[0].dtype, axis=0) if len(history) > 0 else None
@@ -204,8 +205,8 @@ class Solver:
         if stop_crit is None:
             stop_crit = self.default_stop_crit()
         stop_crit.clear()
-        self._astate.update(history=[], idx=0, logger=_NULL_LOGGER, stop_crit=stop_crit, track_objective=False,
-                            mode=Mode.MANUAL, active=None, worker=None, exception=None)
+        self._astate.update(history=[], pending=[], idx=0, logger=_NULL_LOGGER, stop_crit=stop_crit,
+                            track_objective=False, mode=Mode.MANUAL, active=None, worker=None, exception=None)
         self.m_init(**kwargs)
         while self._step():
             pass
@@ -238,7 +239,7 @@ class Solver:
             from pyxu_amd.opt.stop import Memorize
 
             stop_crit |= Memorize(var="objective_func")
-        self._astate.update(history=[], idx=0, logger=_init_logger(), stop_crit=stop_crit,
+        self._astate.update(history=[], pending=[], idx=0, logger=_init_logger(), stop_crit=stop_crit,
                             track_objective=track_objective, mode=mode, active=None, worker=None)
 
     def _fit_run(self):
@@ -267,45 +268,42 @@ class Solver:
         _ml = idx % ast["log_rate"] == 0
         _mw = (ast["wb_rate"] is not None) and (idx % ast["wb_rate"] == 0)
 
-        def _log(msg=None):
-            if msg is None:
-                h = ast["history"][-1][0]
-                lines = [f"[{dt.datetime.now()}] Iteration {ast['idx']:>_d}"]
-                for field, value in zip(h.dtype.names, h):
-                    lines.append(f"\t{field}: {value}")
-                msg = "\n".join(lines)
-            ast["logger"].info(msg)
-
-        def _update_history():
-            data = ast["stop_crit"].info()
-            ftype = pxrt.getPrecision().value
-            dtype = np.dtype([("iteration", np.int64)] + [(k, ftype) for k in data])
-            rec = np.zeros(1, dtype=dtype)
-            rec["iteration"] = ast["idx"]
-            for k, v in data.items():
-                rec[k] = v
-            ast["history"].append(rec)
+        log_on = not ast.get("internal")
+        if ast["pending"] and (_ms or _ml or _mw or idx - ast["pending"][0][0] >= self._RECORD_LAG):
+            self._flush_records()
 
         try:
             if _ms and ast["track_objective"]:
                 self._mstate["objective_func"] = self.objective_func().reshape(-1)
             if _ms and ast["stop_crit"].stop(self._mstate):
-                _update_history()
-                if not ast.get("internal"):
-                    _log()
-                    _log(msg=f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
+                self._record(idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, log_on)
+                if log_on:
+                    ast["logger"].info(f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
                 self.writeback()
                 return False
-            if _ms:
-                _update_history()
-            if _ml and not ast.get("internal"):
-                _log()
-            if _mw:
+            if _mw:  # the checkpoint saves the pre-step state: keep the reference order (solver.py:626-652)
+                self._record(idx, ast["stop_crit"].info() if _ms else None, dt.datetime.now(),
+                             pxrt.getPrecision().value, _ml and log_on)
                 self.writeback()
+                ast["idx"] += 1
+                self.m_step()
+                return True
+            # m_step is enqueued first, so the device starts on it right after the stop decision.  This
+            # iteration's history record and log line (solver.py:604-624) are captured after the launch
+            # (info() reads only the stop criterion, which m_step does not touch; the log time stamp is
+            # taken here) and written a few steps later, when the device queue holds enough work to hide
+            # them (_flush_records: before the next stop check / log / checkpoint and in stats()).  The
+            # records are the reference's, also when m_step raises.
             ast["idx"] += 1
-            self.m_step()
+            try:
+                self.m_step()
+            finally:
+                if _ms or (_ml and log_on):
+                    ast["pending"].append((idx, ast["stop_crit"].info() if _ms else None,
+                                           dt.datetime.now(), pxrt.getPrecision().value, _ml and log_on))
             return True
         except Exception as e:
+            self._flush_records()
             msg = f"[{dt.datetime.now()}] Something went wrong -> EXCEPTION RAISED"
             if ast.get("internal"):
                 ast["exception"] = e
@@ -317,6 +315,38 @@ class Solver:
             ast["logger"].exception(msg, exc_info=e)
             ast["exception"] = e
             return False
+
+    _RECORD_LAG = 8  # steps between an iteration and the write of its deferred history record / log line
+
+    def _record(self, it, data, stamp, ftype, log):
+        """Append the history record of iteration `it` (stop-criterion info `data`, None = no record) and
+        write its log line (solver.py:604-624)."""
+        ast = self._astate
+        if data is not None:
+            key = (ftype, tuple(data))
+            cache = ast.setdefault("_hist_dtype", {})
+            dtype = cache.get(key)
+            if dtype is None:
+                dtype = cache[key] = np.dtype([("iteration", np.int64)] + [(k, ftype) for k in data])
+            rec = np.zeros(1, dtype=dtype)
+            rec["iteration"] = it
+            for k, v in data.items():
+                rec[k] = v
+            ast["history"].append(rec)
+        if log:
+            h = ast["history"][-1][0]
+            lines = [f"[{stamp}] Iteration {it:>_d}"]
+            for field, value in zip(h.dtype.names, h):
+                lines.append(f"\t{field}: {value}")
+            ast["logger"].info("\n".join(lines))
+
+    def _flush_records(self):
+        ast = self._astate
+        items = ast.get("pending")
+        if items:
+            ast["pending"] = []
+            for e in items:
+                self._record(*e)
 
     def _cleanup_logger(self):
         logger = logging.getLogger(str(self.workdir))

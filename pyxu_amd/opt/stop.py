@@ -6,7 +6,6 @@ scalars cross to the host — the single device->host sync of a stop check (stop
 """
 import datetime as dt
 import numbers
-import warnings
 
 import numpy as np
 
@@ -203,6 +202,9 @@ class RelError(pxa.StoppingCriterion):
         st = _dev.empty_f64((2, max(rows, 1)), fx)
         _rowstat(fx, self._norm, fx_prev, out=st[0])
         _rowstat(fx_prev, self._norm, out=st[1])
+        # the reference copies x after the decision (stop.py:381); the copy is decision-independent, so it
+        # is enqueued here and runs while the host waits on the statistics instead of after the sync
+        x_copy = _dev.copy(x)
         if self._reduce is not None:
             st = self._reduce(st, "max" if self._norm == np.inf else "sum")
         st = _finish(st.cpu().numpy(), self._norm)
@@ -210,11 +212,10 @@ class RelError(pxa.StoppingCriterion):
         den = st[1].reshape(*fx.shape[:-1], 1)
         rule = np.all if self._satisfy_all else np.any
         decision = bool(rule(num <= self._eps * den))
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore")
+        with np.errstate(divide="ignore", invalid="ignore"):  # 0/0 -> nan -> 0 below (stop.py:375-379)
             self._val = num / den
             self._val[np.isnan(self._val)] = 0
-        self._x_prev = _dev.copy(x)
+        self._x_prev = x_copy
         return decision
 
     # hook: combine a device row statistic across shards (identity on one process)
