@@ -141,6 +141,14 @@ size_t pxa_row_reduce_workspace_bytes(int64_t rows, int64_t n);
 int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, const void* y, double* out, void* work,
                    void* stream);
 
+/* RelError.stop in one pass (opt/stop.py:353-382, norm=2): out[0:rows] = sum (x - x_prev)^2 and
+ * out[rows:2 rows] = sum x_prev^2 per row (same bits as pxa_row_reduce DIFFSQ / SUMSQ), and, when
+ * x_copy is not NULL, x_copy = x (the `x.copy()` the criterion keeps, stop.py:381).
+ * `work` must hold pxa_relerr_stats_workspace_bytes(rows, n) bytes of device memory. */
+size_t pxa_relerr_stats_workspace_bytes(int64_t rows, int64_t n);
+int pxa_relerr_stats(int dtype, int64_t rows, int64_t n, const void* x, const void* x_prev, void* x_copy, double* out,
+                     void* work, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Stencils (operator/linop/stencil/stencil.py:356-627, _stencil.py:232-476; pad.py; select.py).
  *

@@ -297,6 +297,26 @@ def group_norm(x, outer, group, inner):
 
 
 # ------------------------------------------------------------------ reductions
+def relerr_stats(x, x_prev, out, copy=True):
+    """RelError statistics in one pass (pxa_relerr_stats): out[0] = sum (x - x_prev)^2 and
+    out[1] = sum x_prev^2 per row (out: contiguous float64 (2, rows) device buffer); returns the copy
+    of x the criterion keeps (or None with copy=False)."""
+    torch = _torch()
+    x = require(x)
+    x_prev = require(x_prev)
+    assert x_prev.shape == x.shape and x_prev.dtype == x.dtype
+    n = x.shape[-1] if x.ndim > 0 else 1
+    rows = x.numel() // max(n, 1) if x.numel() else 0
+    assert out.dtype == torch.float64 and out.is_contiguous() and out.numel() == 2 * max(rows, 1)
+    assert 0 < rows <= 65535, "relerr_stats: rows out of range (use row_reduce)"
+    xc = empty_like(x) if copy else None
+    wsz = int(lib.pxa_relerr_stats_workspace_bytes(rows, n))
+    work = torch.empty((max(wsz // 8, 1),), dtype=torch.float64, device=x.device)
+    check(lib.pxa_relerr_stats(dtcode(x), rows, n, ptr(x), ptr(x_prev), ptr(xc) if copy else None, out.data_ptr(),
+                               ptr(work), stream()), "pxa_relerr_stats")
+    return xc
+
+
 def row_reduce(op, x, y=None, out=None):
     """Per-row reduction over the last axis -> float64 device tensor of shape x.shape[:-1] (or (1,)).
     `out`: optional contiguous float64 device buffer of max(rows, 1) elements to write into."""

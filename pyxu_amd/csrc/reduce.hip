@@ -98,6 +98,61 @@ int launch_reduce(int64_t rows, int64_t n, const void* x, const void* y, double*
   return last_launch_status();
 }
 
+
+// RelError statistics in one pass (stop.py:353-382): per row, num = sum (x - p)^2 and den = sum p^2,
+// plus (optionally) the copy of x the criterion keeps for its next check.  Same partition, per-thread
+// order and fold as row_partial_kernel<DIFFSQ> / <SUMSQ> (identical bits), with x and p read once.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) relerr_partial_kernel(int64_t n, int nb, const T* __restrict__ x,
+                                                                const T* __restrict__ p, T* __restrict__ xcopy,
+                                                                double* __restrict__ part) {
+  const int64_t row = blockIdx.y;
+  const T* xr = x + row * n;
+  const T* pr = p + row * n;
+  T* cr = xcopy ? xcopy + row * n : nullptr;
+  int64_t chunk = (n + nb - 1) / nb;
+  int64_t lo = (int64_t)blockIdx.x * chunk;
+  int64_t hi = lo + chunk < n ? lo + chunk : n;
+  double a0 = 0.0, a1 = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const T xv = xr[i], pv = pr[i];
+    a0 = combine<PXA_RED_DIFFSQ>(a0, elem<T, PXA_RED_DIFFSQ>(xv, pv));
+    a1 = combine<PXA_RED_SUMSQ>(a1, elem<T, PXA_RED_SUMSQ>(pv, T(0)));
+    if (cr) cr[i] = xv;
+  }
+  a0 = wave_reduce<PXA_RED_SUMSQ>(a0);
+  a1 = wave_reduce<PXA_RED_SUMSQ>(a1);
+  __shared__ double sw[2][kBlock / kWave];
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    sw[0][w] = a0;
+    sw[1][w] = a1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double r = sw[threadIdx.x][0];
+    for (int k = 1; k < kBlock / kWave; ++k) r = r + sw[threadIdx.x][k];
+    part[(int64_t)threadIdx.x * gridDim.y * nb + row * nb + blockIdx.x] = r;
+  }
+}
+
+template <typename T>
+int launch_relerr(int64_t rows, int64_t n, const void* x, const void* p, void* xcopy, double* out, void* work,
+                  void* stream) {
+  int nb = blocks_per_row(rows, n);
+  double* part = (double*)work;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL((relerr_partial_kernel<T>), dim3(nb, (unsigned)rows), dim3(kBlock), 0, s, n, nb, (const T*)x,
+                     (const T*)p, (T*)xcopy, part);
+  int e = last_launch_status();
+  if (e) return e;
+  // both statistic rows folded by one launch of the row_final kernel (2 * rows rows of nb partials)
+  const int64_t rows_per_block = kBlock / kWave;
+  hipLaunchKernelGGL((row_final_kernel<PXA_RED_SUMSQ>), dim3((unsigned)((2 * rows + rows_per_block - 1) / rows_per_block)),
+                     dim3(kBlock), 0, s, 2 * rows, nb, part, out);
+  return last_launch_status();
+}
+
 }  // namespace
 }  // namespace pxa
 
@@ -133,6 +188,19 @@ int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, co
       return PXA_ERR_ARG;
   }
 #undef PXA_RED_CASE
+}
+
+size_t pxa_relerr_stats_workspace_bytes(int64_t rows, int64_t n) { return 2 * pxa_row_reduce_workspace_bytes(rows, n); }
+
+int pxa_relerr_stats(int dtype, int64_t rows, int64_t n, const void* x, const void* x_prev, void* x_copy, double* out,
+                     void* work, void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && n >= 0);
+  if (rows == 0) return PXA_OK;
+  PXA_CHECK_ARG(rows <= 65535);  // grid.y limit
+  PXA_CHECK_ARG(x != nullptr && x_prev != nullptr && out != nullptr && work != nullptr);
+  PXA_CHECK_ARG(x_copy != x && x_copy != x_prev);
+  if (n == 0) return (int)hipMemsetAsync(out, 0, 2 * rows * sizeof(double), as_stream(stream));
+  PXA_DISPATCH(dtype, T, return launch_relerr<T>(rows, n, x, x_prev, x_copy, out, work, stream));
 }
 
 }  // extern "C"

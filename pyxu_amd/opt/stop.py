@@ -46,6 +46,10 @@ def _rownorm(x, norm, reduce=None):
     return _finish(st.cpu().numpy(), norm).reshape(*x.shape[:-1], 1)
 
 
+def _identity(x):
+    return x
+
+
 def _as_vec(x):
     if isinstance(x, numbers.Real):
         return None
@@ -177,7 +181,7 @@ class RelError(pxa.StoppingCriterion):
         except Exception:
             raise ValueError(f"eps: expected positive threshold, got {eps}.")
         self._var = var
-        self._f = f if (f is not None) else (lambda _: _)
+        self._f = f if (f is not None) else _identity
         try:
             assert norm >= 0
             self._norm = norm
@@ -200,11 +204,15 @@ class RelError(pxa.StoppingCriterion):
         # numerator and denominator row statistics in one device tensor -> one host sync
         rows = fx.numel() // fx.shape[-1]
         st = _dev.empty_f64((2, max(rows, 1)), fx)
-        _rowstat(fx, self._norm, fx_prev, out=st[0])
-        _rowstat(fx_prev, self._norm, out=st[1])
         # the reference copies x after the decision (stop.py:381); the copy is decision-independent, so it
-        # is enqueued here and runs while the host waits on the statistics instead of after the sync
-        x_copy = _dev.copy(x)
+        # is made here, before the host sync.  Identity f and the 2-norm (the default): both statistics
+        # and the copy in one pass over x and x_prev (pxa_relerr_stats).
+        if self._f is _identity and self._norm == 2 and 0 < rows <= 65535 and fx.dtype == fx_prev.dtype:
+            x_copy = _dev.relerr_stats(fx, fx_prev, st)
+        else:
+            _rowstat(fx, self._norm, fx_prev, out=st[0])
+            _rowstat(fx_prev, self._norm, out=st[1])
+            x_copy = _dev.copy(x)
         if self._reduce is not None:
             st = self._reduce(st, "max" if self._norm == np.inf else "sum")
         st = _finish(st.cpu().numpy(), self._norm)

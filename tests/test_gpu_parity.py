@@ -420,3 +420,27 @@ def test_diffop_golden(name):
         assert op.shape == (g["y"].shape[-1], g["x"].shape[-1])
         assert rel_err(to_NUMPY(op.apply(D(g["x"]))), g["y"]) <= OP_TOL[dt]
         assert rel_err(to_NUMPY(op.adjoint(D(g["z"]))), g["adj"]) <= OP_TOL[dt]
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("shape", [(1,), (7,), (4096 * 3 + 5,), (3, 1000), (2, 1, 2048 * 2048 // 64)])
+def test_relerr_stats_one_pass(shape, dtype):
+    """pxa_relerr_stats == (row_reduce DIFFSQ, row_reduce SUMSQ) bit for bit, the copy == x, and the
+    statistics match an fp64 NumPy restatement of RelError (stop.py:365-371)."""
+    from pyxu_amd import _dev
+
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal(shape).astype(dtype)
+    p = rng.standard_normal(shape).astype(dtype)
+    xd, pd = to_device(x), to_device(p)
+    rows = int(np.prod(shape[:-1])) if len(shape) > 1 else 1
+    st = _dev.empty_f64((2, rows), xd)
+    xc = _dev.relerr_stats(xd, pd, st)
+    a = _dev.row_reduce(_dev.RED_DIFFSQ, xd.reshape(-1, shape[-1]), pd.reshape(-1, shape[-1]))
+    b = _dev.row_reduce(_dev.RED_SUMSQ, pd.reshape(-1, shape[-1]))
+    got = to_NUMPY(st)
+    assert np.array_equal(got[0], to_NUMPY(a).reshape(-1)) and np.array_equal(got[1], to_NUMPY(b).reshape(-1))
+    assert np.array_equal(to_NUMPY(xc), x) and xc.data_ptr() != xd.data_ptr()
+    x2, p2 = x.reshape(rows, -1).astype(np.float64), p.reshape(rows, -1).astype(np.float64)
+    assert np.allclose(got[0], ((x2 - p2) ** 2).sum(-1), rtol=1e-12)
+    assert np.allclose(got[1], (p2**2).sum(-1), rtol=1e-12)
