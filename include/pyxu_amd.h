@@ -82,6 +82,10 @@ int pxa_axpby_bcast(int dtype, int64_t n, double a, const void* x, double b, con
  * (CG.m_step on stacked right-hand sides, opt/solver/cg.py:125-153: per-row alpha / beta). */
 int pxa_axpy_rows(int dtype, int64_t rows, int64_t n, const void* c, double s, const void* x, const void* y, void* out,
                   void* stream);
+/* out[r] = (dtype)(num[r] / den[r]) for float64 device vectors num, den of `rows` entries: the CG step
+ * coefficients alpha / beta (opt/solver/cg.py:125-153) formed on the device, so the step needs no host
+ * round trip for <p, A p>. */
+int pxa_row_ratio(int dtype, int64_t rows, const double* num, const double* den, void* out, void* stream);
 
 /* out = a*x + b*y + c*z. */
 int pxa_lincomb3(int dtype, int64_t n, double a, const void* x, double b, const void* y, double c, const void* z,

@@ -188,6 +188,16 @@ def axpy_rows(c, s, x, y, out=None):
     return out
 
 
+def row_ratio(num, den, like, out=None):
+    """out[r] = num[r] / den[r] (float64 device vectors) cast to like's dtype, on the device."""
+    num, den = require(num, "num"), require(den, "den")
+    torch = _torch()
+    assert num.dtype == torch.float64 and den.dtype == torch.float64 and num.numel() == den.numel()
+    out = torch.empty((num.numel(),), dtype=like.dtype, device=like.device) if out is None else out
+    check(lib.pxa_row_ratio(dtcode(like), num.numel(), ptr(num), ptr(den), ptr(out), stream()), "pxa_row_ratio")
+    return out
+
+
 def lincomb3(a, x, b, y, c, z, out=None):
     x, y, z = require(x), require(y), require(z)
     out = empty_like(x) if out is None else out

@@ -26,6 +26,7 @@ EXPORTS = {
     "pxa_axpby": (i32, [i32, i64, f64, vp, f64, vp, vp, vp]),
     "pxa_axpby_bcast": (i32, [i32, i64, f64, vp, f64, vp, i64, vp, vp]),
     "pxa_axpy_rows": (i32, [i32, i64, i64, vp, f64, vp, vp, vp, vp]),
+    "pxa_row_ratio": (i32, [i32, i64, vp, vp, vp, vp]),
     "pxa_lincomb3": (i32, [i32, i64, f64, vp, f64, vp, f64, vp, vp, vp]),
     "pxa_extrapolate": (i32, [i32, i64, f64, vp, vp, vp, vp]),
     "pxa_div": (i32, [i32, i64, vp, f64, vp, vp]),

@@ -213,6 +213,15 @@ __global__ void __launch_bounds__(kBlock) axpy_rows_kernel(int64_t rows, int64_t
   }
 }
 
+// out[r] = (T)(num[r] / den[r]) in float64 (CG alpha = ||r||^2 / <p, A p>, beta = ||r'||^2 / ||r||^2,
+// cg.py:125-153): the same IEEE division the host would do, so the coefficient bits do not change.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) row_ratio_kernel(int64_t rows, const double* __restrict__ num,
+                                                           const double* __restrict__ den, T* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += stride) out[i] = (T)(num[i] / den[i]);
+}
+
 }  // namespace
 }  // namespace pxa
 
@@ -247,6 +256,17 @@ int pxa_axpy_rows(int dtype, int64_t rows, int64_t n, const void* c, double s, c
   PXA_DISPATCH(dtype, T, {
     hipLaunchKernelGGL((axpy_rows_kernel<T>), dim3(grid_for(rows * n)), dim3(kBlock), 0, as_stream(stream), rows, n,
                        (const T*)c, (T)s, (const T*)x, (const T*)y, (T*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_row_ratio(int dtype, int64_t rows, const double* num, const double* den, void* out, void* stream) {
+  PXA_CHECK_ARG(rows >= 0);
+  if (rows == 0) return PXA_OK;
+  PXA_CHECK_ARG(num && den && out);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((row_ratio_kernel<T>), dim3(grid_for(rows)), dim3(kBlock), 0, as_stream(stream), rows, num, den,
+                       (T*)out);
     return last_launch_status();
   });
 }

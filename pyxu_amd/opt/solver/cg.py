@@ -8,26 +8,27 @@ from pyxu_amd import _dev
 __all__ = ["CG"]
 
 
-def _rowsq(x):
-    """||x||^2 per row -> host float64 (..., 1)."""
-    r = _dev.row_reduce(_dev.RED_SUMSQ, x.reshape(-1, x.shape[-1]))
-    return r.cpu().numpy().reshape(*x.shape[:-1], 1)
+def _rows2d(x):
+    return x.reshape(-1, x.shape[-1])
 
 
-def _rowdot(x, y):
-    r = _dev.row_reduce(_dev.RED_DOT, x.reshape(-1, x.shape[-1]), y.reshape(-1, y.shape[-1]))
-    return r.cpu().numpy().reshape(*x.shape[:-1], 1)
+class _HostRows:
+    """Device float64 row vector plus its host copy, fetched with a non-blocking copy into pinned memory
+    behind an event: the host waits for it only where it branches on the value (the ||r||^2 <= eps test
+    of the next step), by which time that step's A p, <p, A p> and x update are already queued."""
 
+    def __init__(self, dev):
+        import torch
 
-def _rowsq_rowdot(r, p, Ap):
-    """(||r||^2, <p, Ap>) per row with ONE host synchronisation (two reductions into one buffer)."""
-    rows = r.numel() // r.shape[-1]
-    buf = _dev.empty_f64((2, rows), r)
-    _dev.row_reduce(_dev.RED_SUMSQ, r.reshape(-1, r.shape[-1]), out=buf[0])
-    _dev.row_reduce(_dev.RED_DOT, p.reshape(-1, p.shape[-1]), Ap.reshape(-1, Ap.shape[-1]), out=buf[1])
-    h = buf.cpu().numpy()
-    sh = (*r.shape[:-1], 1)
-    return h[0].reshape(sh), h[1].reshape(sh)
+        self.dev = dev
+        self._h = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True)
+        self._h.copy_(dev, non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record()
+
+    def host(self):
+        self._ev.synchronize()
+        return self._h.numpy()
 
 
 class CG(pxa.Solver):
@@ -62,57 +63,35 @@ class CG(pxa.Solver):
         mst["conjugate_dir"] = _dev.copy(mst["residual"])
         self._rr = None  # ||r||^2 of the current residual, carried from the previous step's beta
 
-    def _scale_rows(self, coef, v):
-        """coef (..., 1) host numpy -> device tensor broadcast multiplier."""
-        import torch
-
-        c = torch.from_numpy(np.ascontiguousarray(coef, dtype=np.float64)).to(device=v.device, dtype=v.dtype)
-        return c
-
     def m_step(self):
+        """cg.py:125-153.  alpha = ||r||^2 / <p, A p> and beta = ||r'||^2 / ||r||^2 are formed on the
+        device (pxa_row_ratio, float64 division then the cast the host path would do) and applied per
+        row (pxa_axpy_rows), so a step has ONE host read: ||r||^2 for the eps test, issued as an async
+        copy at the end of the previous step."""
         mst = self._mstate
         x, r, p = mst["x"], mst["residual"], mst["conjugate_dir"]
         Ap = self._A.apply(p)
-        # ||r||^2 is the previous step's beta numerator (same reduction of the same r: identical bits);
-        # otherwise it is computed together with <p, A p> behind one host synchronisation
+        pAp = _dev.row_reduce(_dev.RED_DOT, _rows2d(p), _rows2d(Ap))
         if self._rr is not None and self._rr[1] is r:
-            rr, pAp = self._rr[0], _rowdot(p, Ap)
+            rr = self._rr[0]  # ||r||^2 of this r: the previous step's beta numerator (identical bits)
         else:
-            rr, pAp = _rowsq_rowdot(r, p, Ap)
+            rr = _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)))
         self._rr = None
-        alpha = rr / pAp
+        alpha = _dev.row_ratio(rr.dev, pAp, x)
+        _dev.axpy_rows(alpha, 1.0, _rows2d(p), _rows2d(x), out=_rows2d(x))  # x += alpha p
         eps = pxrt.Width(np.dtype(str(x.dtype).replace("torch.", ""))).eps()
-        if x.ndim <= 1 or x.numel() == x.shape[-1]:
-            a = float(np.asarray(alpha).reshape(-1)[0])
-            _dev.axpby(1.0, x, a, p, out=x)
-            if np.any(rr <= eps):
-                _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
-            else:
-                _dev.axpby(1.0, r, -a, Ap, out=r)
-            if self._astate["idx"] % mst["restart_rate"] == 0:
-                beta = 0.0
-                _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
-            else:
-                rr_new = _rowsq(r)
-                self._rr = (rr_new, r)
-                beta = float((rr_new / rr).reshape(-1)[0])
-            _dev.axpby(beta, p, 1.0, r, out=p)
+        if np.any(rr.host() <= eps):
+            _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
         else:
-            # stacked right-hand sides: per-row coefficients
-            A_ = self._scale_rows(alpha, x).reshape(-1)
-            _dev.axpy_rows(A_, 1.0, p, x, out=x)  # x += alpha p (per row)
-            if np.any(rr <= eps):
-                _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
-            else:
-                _dev.axpy_rows(A_, -1.0, Ap, r, out=r)  # r -= alpha A p
-            if self._astate["idx"] % mst["restart_rate"] == 0:
-                _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
-                _dev.axpby(0.0, p, 1.0, r, out=p)
-            else:
-                rr_new = _rowsq(r)
-                self._rr = (rr_new, r)
-                B_ = self._scale_rows(rr_new / rr, p).reshape(-1)
-                _dev.axpy_rows(B_, 1.0, p, r, out=p)  # p = r + beta p (per row)
+            _dev.axpy_rows(alpha, -1.0, _rows2d(Ap), _rows2d(r), out=_rows2d(r))  # r -= alpha A p
+        if self._astate["idx"] % mst["restart_rate"] == 0:
+            _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
+            _dev.axpby(0.0, p, 1.0, r, out=p)  # beta = 0
+        else:
+            rr_new = _dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r))
+            beta = _dev.row_ratio(rr_new, rr.dev, p)
+            _dev.axpy_rows(beta, 1.0, _rows2d(p), _rows2d(r), out=_rows2d(p))  # p = r + beta p
+            self._rr = (_HostRows(rr_new), r)
         mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
 
     def default_stop_crit(self):

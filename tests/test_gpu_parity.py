@@ -380,6 +380,23 @@ def test_xp_shim_numpy_semantics():
     assert NDArrayInfo.from_obj(t) is NDArrayInfo.MI355X
 
 
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_row_ratio_bits(dt):
+    """pxa_row_ratio: (dtype)(num / den) in float64 on the device == the host's numpy division + cast
+    (the CG alpha / beta of cg.py:125-153), bit for bit, incl. a zero denominator."""
+    from pyxu_amd import _dev
+
+    rng = np.random.default_rng(3)
+    num = np.abs(rng.standard_normal(1000)) * 10.0 ** rng.integers(-30, 30, 1000)
+    den = np.abs(rng.standard_normal(1000)) * 10.0 ** rng.integers(-30, 30, 1000)
+    den[7] = 0.0
+    like = D(np.zeros(1, dtype=dt))
+    out = to_NUMPY(_dev.row_ratio(D(num), D(den), like))
+    with np.errstate(divide="ignore", over="ignore"):  # f32 overflow -> inf on both sides
+        ref = (num / den).astype(dt)
+    np.testing.assert_array_equal(out, ref)
+
+
 @pytest.mark.parametrize("rows", [1, 3])
 def test_cg_stacked_vs_oracle(rows):
     """CG (opt/solver/cg.py:72-165) on an SPD dense operator, single and stacked right-hand sides
