@@ -231,7 +231,7 @@ def main():
             "data": "synthetic (piecewise-constant phantom, Gaussian blur, 1% noise)",
             "config": {"workload": f"PGD {n0}x{n1} Gaussian(sigma=2) deblur + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
                        "image": [n0, n1], "images_per_gpu": 1, "stop_rate": args.stop_rate,
-                       "stop_crit": "MaxIter | RelError" + (" (global, RCCL all-reduce)" if world > 1 else ""), "fused_m_step": fused, "parallelism": f"batch-as-axis slabs x{world} (one image per rank)"},
+                       "stop_crit": "MaxIter | RelError" + (f" (global, {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} all-reduce)" if world > 1 else ""), "fused_m_step": fused, "parallelism": f"batch-as-axis slabs x{world} (one image per rank)"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
