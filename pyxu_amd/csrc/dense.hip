@@ -28,7 +28,7 @@ __global__ void __launch_bounds__(kBlock) gemv_rows_kernel(int64_t M, int64_t N,
     for (int j = 0; j < kBC; ++j) acc[j] = 0.0;
     if (vec) {
       // kU independent 16-B loads of the A row in flight per lane (latency hiding: one wave per row)
-      constexpr int kU = 4;
+      constexpr int kU = 8;
       int64_t k = (int64_t)lane * V;
       for (; k + (kU - 1) * 64 * V < N; k += kU * 64 * V) {
         T av[kU][V];
