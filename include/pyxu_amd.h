@@ -145,6 +145,12 @@ size_t pxa_row_reduce_workspace_bytes(int64_t rows, int64_t n);
 int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, const void* y, double* out, void* work,
                    void* stream);
 
+/* General Ln statistic of AbsError / RelError with any norm >= 0 (opt/stop.py:222-297, 300-396:
+ * xp.linalg.norm(ord=p)): out[r] = sum |x - y|^p over row r (p > 0; y may be NULL), or the count of
+ * non-zero entries of x - y (p == 0, NumPy's ord=0).  Same workspace as pxa_row_reduce. */
+int pxa_row_reduce_pow(int dtype, int64_t rows, int64_t n, double p, const void* x, const void* y, double* out,
+                       void* work, void* stream);
+
 /* RelError.stop in one pass (opt/stop.py:353-382, norm=2): out[0:rows] = sum (x - x_prev)^2 and
  * out[rows:2 rows] = sum x_prev^2 per row (same bits as pxa_row_reduce DIFFSQ / SUMSQ), and, when
  * x_copy is not NULL, x_copy = x (the `x.copy()` the criterion keeps, stop.py:381).

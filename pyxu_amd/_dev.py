@@ -132,6 +132,23 @@ def set_launch_timer(timer):
     _TIMER = timer
 
 
+_USE_COUNT = None
+
+
+def storage_exclusive(t) -> bool:
+    """True iff no other tensor shares `t`'s storage.  Solvers overwrite a buffer in place only when
+    the Python reference count of the tensor object says nobody else holds it AND this holds: views
+    such as ``img.reshape(-1)`` or ``batch[i]`` passed as x0 / z0 keep the storage's use count above
+    that of a lone tensor.  The reference allocates fresh arrays every step, so anything a user can
+    still reach must never be written."""
+    global _USE_COUNT
+    if _USE_COUNT is None:
+        torch = _torch()
+        _USE_COUNT = getattr(torch._C, "_storage_Use_Count", None) or (lambda _c: 1 << 30)
+    # a lone tensor: its TensorImpl + the temporary storage wrapper created here
+    return _USE_COUNT(t.untyped_storage()._cdata) <= 2
+
+
 def empty(shape, like):
     return _torch().empty(shape, dtype=like.dtype, device=like.device)
 
@@ -358,6 +375,31 @@ def row_reduce(op, x, y=None, out=None):
             "pxa_row_reduce",
         )
     return out.reshape(x.shape[:-1]) if x.ndim > 1 else out
+
+
+def row_reduce_pow(p, x, y=None, out=None):
+    """Per-row sum |x - y|^p (p > 0) or non-zero count (p == 0) -> float64 device (rows,) tensor."""
+    torch = _torch()
+    x = require(x)
+    n = x.shape[-1] if x.ndim > 0 else 1
+    rows = x.numel() // max(n, 1) if x.numel() else 0
+    if y is not None:
+        y = require(y)
+        assert y.shape == x.shape
+    if out is None:
+        out = torch.empty((max(rows, 1),), dtype=torch.float64, device=x.device)
+    if rows == 0:
+        return out.zero_()
+    step = 65535
+    es = x.element_size()
+    for r0 in range(0, rows, step):
+        r1 = min(rows, r0 + step)
+        wsz = int(lib.pxa_row_reduce_workspace_bytes(r1 - r0, n))
+        work = torch.empty((max(wsz // 8, 1),), dtype=torch.float64, device=x.device)
+        check(lib.pxa_row_reduce_pow(dtcode(x), r1 - r0, n, float(p), ptr(x) + r0 * n * es,
+                                     (ptr(y) + r0 * n * es) if y is not None else None, out.data_ptr() + r0 * 8,
+                                     ptr(work), stream()), "pxa_row_reduce_pow")
+    return out
 
 
 # ------------------------------------------------------------------ stencils

@@ -43,6 +43,7 @@ EXPORTS = {
     "pxa_group_norm": (i32, [i32, i64, i64, i64, vp, vp, vp]),
     "pxa_row_reduce_workspace_bytes": (sz, [i64, i64]),
     "pxa_row_reduce": (i32, [i32, i32, i64, i64, vp, vp, vp, vp, vp]),
+    "pxa_row_reduce_pow": (i32, [i32, i64, i64, f64, vp, vp, vp, vp, vp]),
     "pxa_relerr_stats_workspace_bytes": (sz, [i64, i64]),
     "pxa_relerr_stats": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp]),
     "pxa_stencil_axis": (i32, [i32, i64, i32, P_i64, i32, i32, P_i32, P_f64, i32, vp, i64, vp, i64, f64, vp]),

@@ -77,7 +77,7 @@ class Solver:
         self._mstate = dict()
         self._astate = dict(history=None, idx=0, log_rate=None, log_var=None, logger=None, stdout=None, stop_crit=None,
                             stop_rate=None, track_objective=None, wb_rate=None, workdir=None, mode=None, active=None,
-                            worker=None, internal=bool(_internal))
+                            worker=None, internal=bool(_internal), lock=threading.RLock())
         try:
             if _internal:  # sub-solver of an operator method (QuadraticFunc.prox): no workdir / log / checkpoint
                 pass
@@ -148,10 +148,13 @@ class Solver:
                 return
 
     def stats(self):
-        self._flush_records()
-        history = self._astate["history"]
-        if history is not None:
-            history = np.concatenate(history, dtype=history[0].dtype, axis=0) if len(history) > 0 else None
+        # ASYNC: the worker thread appends and flushes records concurrently; the records lock keeps
+        # pending -> history moves atomic, so no record is dropped, duplicated or reordered
+        with self._astate["lock"]:
+            self._flush_records()
+            history = self._astate["history"]
+            if history is not None:
+                history = np.concatenate(history, dtype=history[0].dtype, axis=0) if len(history) > 0 else None
         data = {k: self._mstate.get(k) for k in self._astate["log_var"]}
         return data, history
 
@@ -276,14 +279,16 @@ class Solver:
             if _ms and ast["track_objective"]:
                 self._mstate["objective_func"] = self.objective_func().reshape(-1)
             if _ms and ast["stop_crit"].stop(self._mstate):
-                self._record(idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, log_on)
+                with ast["lock"]:
+                    self._record(idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, log_on)
                 if log_on:
                     ast["logger"].info(f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
                 self.writeback()
                 return False
             if _mw:  # the checkpoint saves the pre-step state: keep the reference order (solver.py:626-652)
-                self._record(idx, ast["stop_crit"].info() if _ms else None, dt.datetime.now(),
-                             pxrt.getPrecision().value, _ml and log_on)
+                with ast["lock"]:
+                    self._record(idx, ast["stop_crit"].info() if _ms else None, dt.datetime.now(),
+                                 pxrt.getPrecision().value, _ml and log_on)
                 self.writeback()
                 ast["idx"] += 1
                 self.m_step()
@@ -299,8 +304,10 @@ class Solver:
                 self.m_step()
             finally:
                 if _ms or (_ml and log_on):
-                    ast["pending"].append((idx, ast["stop_crit"].info() if _ms else None,
-                                           dt.datetime.now(), pxrt.getPrecision().value, _ml and log_on))
+                    rec = (idx, ast["stop_crit"].info() if _ms else None, dt.datetime.now(),
+                           pxrt.getPrecision().value, _ml and log_on)
+                    with ast["lock"]:
+                        ast["pending"].append(rec)
             return True
         except Exception as e:
             self._flush_records()
@@ -342,11 +349,11 @@ class Solver:
 
     def _flush_records(self):
         ast = self._astate
-        items = ast.get("pending")
-        if items:
-            ast["pending"] = []
-            for e in items:
-                self._record(*e)
+        if ast.get("pending"):
+            with ast["lock"]:
+                items, ast["pending"] = ast["pending"], []
+                for e in items:
+                    self._record(*e)
 
     def _cleanup_logger(self):
         logger = logging.getLogger(str(self.workdir))

@@ -11,9 +11,10 @@ namespace {
 // Op::operator()(T* v[NIN], T& out) style is awkward in device code; use per-element functors
 // that receive the element index so each kernel reads exactly what it needs.
 template <typename T, int NIN, typename Op>
-__global__ void __launch_bounds__(kBlock) map_kernel(int64_t n, Op op, const T* __restrict__ a,
-                                                     const T* __restrict__ b, const T* __restrict__ c,
-                                                     T* __restrict__ out, bool vec) {
+// `out` may alias an input (solver updates written in place): element i is read and written by the
+// same thread only, so no __restrict__ on the operands.
+__global__ void __launch_bounds__(kBlock) map_kernel(int64_t n, Op op, const T* a, const T* b, const T* c, T* out,
+                                                     bool vec) {
   constexpr int V = kVecN<T>;
   using VT = typename Vec4<T>::type;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -142,8 +143,7 @@ enum GroupMode { kProx = 0, kFenchel = 1, kMoreau = 2, kNorm = 3 };
 
 template <typename T, int MODE>
 __global__ void __launch_bounds__(kBlock) group_kernel(int64_t outer, int64_t group, int64_t inner,
-                                                       const T* __restrict__ x, T* __restrict__ out, T p0, T p1,
-                                                       T p2) {
+                                                       const T* x, T* out, T p0, T p1, T p2) {  // out may alias x
   const int64_t total = outer * inner;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
@@ -194,17 +194,18 @@ int launch_group(int64_t outer, int64_t group, int64_t inner, const void* x, voi
 
 // out[i] = a*x[i] + b*y[i % ny]   (stack broadcast of a (ny,) vector; ArgShiftRule / AddRule)
 template <typename T>
-__global__ void __launch_bounds__(kBlock) bcast_kernel(int64_t n, int64_t ny, T a, const T* __restrict__ x, T b,
-                                                       const T* __restrict__ y, T* __restrict__ out) {
+__global__ void __launch_bounds__(kBlock) bcast_kernel(int64_t n, int64_t ny, T a, const T* x, T b,
+                                                       const T* __restrict__ y, T* out) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = a * x[i] + b * y[i % ny];
 }
 
 // out[r, i] = y[r, i] + s * c[r] * x[r, i]   (per-row step of CG on stacked right-hand sides, cg.py:125-153)
+// out may alias x or y (CG: x += a p, r -= a A p, p = r + b p): no __restrict__ on those three; each
+// element is read and written by the same thread only.
 template <typename T>
 __global__ void __launch_bounds__(kBlock) axpy_rows_kernel(int64_t rows, int64_t n, const T* __restrict__ c, T s,
-                                                           const T* __restrict__ x, const T* __restrict__ y,
-                                                           T* __restrict__ out) {
+                                                           const T* x, const T* y, T* out) {
   const int64_t total = rows * n;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {

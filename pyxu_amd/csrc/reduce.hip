@@ -153,12 +153,66 @@ int launch_relerr(int64_t rows, int64_t n, const void* x, const void* p, void* x
   return last_launch_status();
 }
 
+// General Ln row statistic for the stop criteria (stop.py:222-297 -> pxlg.norm(ord=p)):
+// sum |x - y|^p (p > 0), or the count of non-zero entries (p == 0, NumPy's ord=0).  Same partition
+// and fold as row_partial_kernel (deterministic).
+template <typename T>
+__global__ void __launch_bounds__(kBlock) row_pow_kernel(int64_t n, int nb, double p, const T* __restrict__ x,
+                                                         const T* __restrict__ y, double* __restrict__ part) {
+  const int64_t row = blockIdx.y;
+  const T* xr = x + row * n;
+  const T* yr = y ? y + row * n : nullptr;
+  int64_t chunk = (n + nb - 1) / nb;
+  int64_t lo = (int64_t)blockIdx.x * chunk;
+  int64_t hi = lo + chunk < n ? lo + chunk : n;
+  double acc = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const double d = fabs((double)xr[i] - (yr ? (double)yr[i] : 0.0));
+    acc += p == 0.0 ? (d != 0.0 ? 1.0 : 0.0) : pow(d, p);
+  }
+  acc = wave_reduce<PXA_RED_SUM>(acc);
+  __shared__ double sw[kBlock / kWave];
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) sw[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = sw[0];
+    for (int k = 1; k < kBlock / kWave; ++k) r = r + sw[k];
+    part[row * nb + blockIdx.x] = r;
+  }
+}
+
+template <typename T>
+int launch_pow(int64_t rows, int64_t n, double p, const void* x, const void* y, double* out, void* work, void* stream) {
+  int nb = blocks_per_row(rows, n);
+  double* part = (double*)work;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL((row_pow_kernel<T>), dim3(nb, (unsigned)rows), dim3(kBlock), 0, s, n, nb, p, (const T*)x,
+                     (const T*)y, part);
+  int e = last_launch_status();
+  if (e) return e;
+  const int64_t rows_per_block = kBlock / kWave;
+  hipLaunchKernelGGL((row_final_kernel<PXA_RED_SUM>), dim3((unsigned)((rows + rows_per_block - 1) / rows_per_block)),
+                     dim3(kBlock), 0, s, rows, nb, part, out);
+  return last_launch_status();
+}
+
 }  // namespace
 }  // namespace pxa
 
 using namespace pxa;
 
 extern "C" {
+
+int pxa_row_reduce_pow(int dtype, int64_t rows, int64_t n, double p, const void* x, const void* y, double* out,
+                       void* work, void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && n >= 0 && p >= 0.0);
+  if (rows == 0) return PXA_OK;
+  PXA_CHECK_ARG(rows <= 65535);
+  PXA_CHECK_ARG(x != nullptr && out != nullptr && work != nullptr);
+  if (n == 0) return (int)hipMemsetAsync(out, 0, rows * sizeof(double), as_stream(stream));
+  PXA_DISPATCH(dtype, T, return launch_pow<T>(rows, n, p, x, y, out, work, stream));
+}
 
 size_t pxa_row_reduce_workspace_bytes(int64_t rows, int64_t n) {
   if (rows <= 0) return 0;

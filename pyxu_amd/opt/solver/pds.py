@@ -104,8 +104,8 @@ class _PrimalDualSplitting(pxa.Solver):
     def _owned(t, extra=0):
         """True iff `t` is referenced only by the solver state (+ `extra` caller locals): it may be
         overwritten in place.  The reference allocates fresh arrays each step, so arrays a user holds
-        (z0, logged iterates) are never modified."""
-        return sys.getrefcount(t) <= 3 + extra
+        (z0, logged iterates, and views of user arrays such as ``batch[i]``) are never modified."""
+        return sys.getrefcount(t) <= 3 + extra and _dev.storage_exclusive(t)
 
     def m_step(self):
         raise NotImplementedError
@@ -190,7 +190,7 @@ class CondatVu(_PrimalDualSplitting):
             z_out = z if self._owned(z, extra=1) else _dev.empty_like(z)
             _dev.pds_step(1, p["pre"], x, None, z, p["hty"], out, None, z_out, p["q"], p["w"], nseg=p["nseg"])
             mst["x"], mst["z"] = out, z_out
-            self._spare = x if sys.getrefcount(x) == 2 else None
+            self._spare = x if (sys.getrefcount(x) == 2 and _dev.storage_exclusive(x)) else None
             return
         x = mst["x"]
         tau = mst["tau"]

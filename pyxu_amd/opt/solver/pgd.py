@@ -90,7 +90,8 @@ class PGD(pxa.Solver):
             mst["x_prev"], mst["x"] = x, out
             # recycle the old x_prev as the next output buffer iff nobody else holds it (the reference
             # allocates fresh arrays, so user-held results must never be overwritten)
-            self._spare = xp if (sys.getrefcount(xp) == 2 and xp.data_ptr() != x.data_ptr()) else None
+            self._spare = xp if (sys.getrefcount(xp) == 2 and xp.data_ptr() != x.data_ptr()
+                                 and _dev.storage_exclusive(xp)) else None
             return
         # generic path: y = (x - x_prev) * a + x ; z = y - tau * grad(y) ; x+ = prox_g(z, tau)
         y = _dev.extrapolate(a, mst["x"], mst["x_prev"])

@@ -22,9 +22,10 @@ def _rowstat(x, norm, y=None, out=None):
     """(..., N) device tensor(s) -> float64 DEVICE (rows,) row statistic of (x - y) for the Ln norm:
     sum of squares (2), sum of |.| (1) or max |.| (inf).  Stays on the device so that sharded
     criteria can all-reduce it before the single host sync (pyxu_amd.distributed)."""
-    if norm not in _RED:
-        raise NotImplementedError(f"pyxu_amd: norm={norm} not supported on device (1, 2, inf).")
     x2 = x.reshape(-1, x.shape[-1])
+    if norm not in _RED:  # any other Ln, norm >= 0 (stop.py:258, numpy ord=p): sum |x - y|^p or nnz count
+        y2 = y.reshape(-1, y.shape[-1]) if y is not None else None
+        return _dev.row_reduce_pow(float(norm), x2, y2, out=out)
     if y is not None:
         y2 = y.reshape(-1, y.shape[-1])
         if norm == 2:
@@ -34,8 +35,12 @@ def _rowstat(x, norm, y=None, out=None):
 
 
 def _finish(stat, norm):
-    """host row statistic -> Ln norm."""
-    return stat**0.5 if norm == 2 else stat
+    """host row statistic -> Ln norm (numpy.linalg.norm(ord=norm) semantics)."""
+    if norm == 2:
+        return stat**0.5
+    if norm in (1, np.inf, 0):
+        return stat
+    return stat ** (1.0 / norm)
 
 
 def _rownorm(x, norm, reduce=None):
