@@ -2,19 +2,33 @@
 """
 Benchmark: PGD solver iterations/s on TV-regularised deblurring (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): 2048 x 2048 image, H = Gaussian(sigma=2) blur (13 taps/axis,
-zero boundary), f = 1/2||H x - y||^2 + lam * env_mu(L21) o Gradient, g = PositiveOrthant,
-lam = mu = 0.01, fp32, synthetic piecewise-constant phantom + 1% noise.
-One "step" = one PGD iteration (Solver._step: stop check every `stop_rate` iterations + m_step)
-driven through the pyxu_amd Solver API in MANUAL mode.
+Headline workload (BASELINE.json configs[1], C2): 2048 x 2048 image, H = Gaussian(sigma=2) blur (13
+taps/axis, zero boundary), f = 1/2||H x - y||^2 + lam * env_mu(L21) o Gradient, g = PositiveOrthant,
+lam = mu = 0.01, fp32, synthetic piecewise-constant phantom + 1% noise.  One
+"step" = one PGD iteration (Solver._step: stop check every `stop_rate` iterations + m_step) driven
+through the pyxu_amd Solver API in MANUAL mode.  `stop_rate` defaults to the largest divisor of
+--steps that is <= 50, so the timed window holds exactly steps/stop_rate stop checks and
+`ms_per_step` carries their amortised cost.
 
-Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): every rank solves its own image
-(independent problems shard with no data-path collective) -> weak scaling; value = total
-image-iterations/s over all ranks = ranks * K / max_rank(elapsed).
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` (no WORLD_SIZE in the environment)
+launches N child ranks itself before touching the GPU (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT set per child); under torch.distributed.run each process is one
+rank.  Every rank solves its own 2048^2 image (independent problems, no data-path collective; the
+ranks' images form one batch-as-axis problem for the GLOBAL RelError: one RCCL all-reduce of 2
+doubles per stop check) -> weak scaling; value = total image-iterations/s = ranks * K / max_rank(t).
+
+Sub-records on the same line (north_star):
+  "stop_rate_1": the headline workload at the reference's default stop_rate = 1;
+  "c5": configs[4], 512 independent 512^2 TV-deblur images as ONE (512, 512, 512) batch-as-axis
+        problem sharded over the ranks (512 / N images each: strong scaling), global RelError;
+  "c4": configs[3], ADMM with a dense 8192 x 65536 K (MFMA/GEMV dense path) + lam L1; K row-sharded
+        over the ranks (one RCCL all-reduce of the 65536-vector per CG iteration).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,9 +40,56 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 KERNEL = "pgd_tv2d_kernel"
 ALG_BYTES_PER_PIXEL = 48  # 8 reads + 4 writes of fp32 per pixel per PGD iteration
-FUSED_BYTES_PER_PIXEL = 16  # compulsory traffic of the one-launch step: x, x_prev, y read + x_new write
+FUSED_BYTES_PER_PIXEL = 16  # compulsory traffic of the one-launch step: x, x_prev, H^T y read + x_new write
+CPU_THREADS_MAX = 16  # the GPU box's CPU share per GPU (gpurun: 16)
 
 
+# ----------------------------------------------------------------------------- launcher (no GPU here)
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, port, base=None):
+    """Per-child environments of the self-launch (one rank per GPU, rendezvous on 127.0.0.1)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PXA_BENCH_CHILD="1")
+        envs.append(e)
+    return envs
+
+
+def launch(argv, n, script=None):
+    """Start `n` ranks of this script as child processes and wait for them; rank 0's stdout is ours.
+    The parent never initialises the GPU (so no exec-after-GPU-init hazard) and forwards the worst
+    exit status; if one rank fails, the others are stopped (they would block in a collective)."""
+    envs = rank_envs(n, _free_port())
+    cmd = [sys.executable, script or os.path.abspath(__file__), *argv]
+    procs = [subprocess.Popen(cmd, env=e, stdout=None if r == 0 else subprocess.DEVNULL) for r, e in enumerate(envs)]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+# ----------------------------------------------------------------------------- workloads
 def phantom(shape, rng):
     x = np.zeros(shape, dtype=np.float32)
     for _ in range(12):
@@ -39,8 +100,10 @@ def phantom(shape, rng):
 
 
 def build_problem(n0, n1, seed, lam=0.01, mu=0.01, sigma=2.0):
+    """C2: f = 1/2||H.-y||^2 + lam env_mu(L21) o Grad, g = PositiveOrthant on one n0 x n1 image."""
     import pyxu_amd.operator as pxo
     import pyxu_amd.runtime as pxrt
+    from pyxu_amd import _dev
     from pyxu_amd.util import to_device
 
     sh = (n0, n1)
@@ -51,14 +114,46 @@ def build_problem(n0, n1, seed, lam=0.01, mu=0.01, sigma=2.0):
         x_gt = to_device(phantom(sh, rng).reshape(-1))
         y = H.apply(x_gt)
         noise = to_device((0.01 * rng.standard_normal(N)).astype(np.float32))
-        from pyxu_amd import _dev
-
         y = _dev.axpby(1.0, y, 1.0, noise)
         G = pxo.Gradient(arg_shape=sh)
         f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H + lam * pxo.L21Norm(arg_shape=(2, *sh)).moreau_envelope(mu) * G
         f.diff_lipschitz = 1.0 + (lam / mu) * 8.0  # ||H||^2 + lam/mu ||Grad||^2, set analytically (§8(d))
         g = pxo.PositiveOrthant(dim=N)
     return f, g, y
+
+
+def build_batch_problem(B, n, first, seed, lam=0.01, mu=0.01, sigma=2.0):
+    """C5 slab: images [first, first + B) of the global batch as one (B, n, n) batch-as-axis problem
+    (size-1 taps on axis 0, Gradient(directions=(1, 2)), distinct y per image; SURVEY App. A #12)."""
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd import _dev
+    from pyxu_amd.util import to_device
+
+    sh = (B, n, n)
+    N = B * n * n
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        H = pxo.Gaussian(arg_shape=sh, sigma=(0, sigma, sigma), truncate=3.0)
+        x_gt = np.empty((B, n, n), dtype=np.float32)
+        for b in range(B):  # image i's phantom depends only on (seed, i): identical for every N
+            x_gt[b] = phantom((n, n), np.random.default_rng((seed, first + b)))
+        y = H.apply(to_device(x_gt.reshape(-1)))
+        noise = np.random.default_rng((seed, first, 1)).standard_normal(N, dtype=np.float32) * np.float32(0.01)
+        y = _dev.axpby(1.0, y, 1.0, to_device(noise))
+        G = pxo.Gradient(arg_shape=sh, directions=(1, 2))
+        f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H + lam * pxo.L21Norm(arg_shape=(2, *sh)).moreau_envelope(mu) * G
+        f.diff_lipschitz = 1.0 + (lam / mu) * 8.0
+        g = pxo.PositiveOrthant(dim=N)
+    return f, g
+
+
+def auto_stop_rate(steps, cap=50):
+    """Largest divisor of `steps` that is <= cap: a window of `steps` consecutive iterations then holds
+    exactly steps / stop_rate stop checks wherever it starts."""
+    for r in range(min(cap, max(steps, 1)), 0, -1):
+        if steps % r == 0:
+            return r
+    return 1
 
 
 def cpu_model():
@@ -71,7 +166,7 @@ def cpu_model():
     return "unknown CPU"
 
 
-def measured_traffic(kernel, n0, n1):
+def measured_traffic(kernel, key):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic.json,
     written by scripts/pmc_traffic.py: (2 * FETCH_SIZE + WRITE_SIZE) * 1024, the gfx950 correction of
     MI355X_MICROARCH.md §HBM), or None when no profile of this workload exists."""
@@ -81,14 +176,17 @@ def measured_traffic(kernel, n0, n1):
             tab = json.load(fh)
     except (OSError, ValueError):
         return None
-    ent = tab.get(f"{kernel}@{n0}x{n1}")
+    ent = tab.get(f"{kernel}@{key}")
     return None if ent is None else ent.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(n0, n1, seed, budget_s, lam=0.01, mu=0.01, sigma=2.0):
-    """Oracle (NumPy restatement of the reference path) on the host: same problem; as many PGD
-    iterations as fit in about `budget_s` seconds (bounded sample; at least 2)."""
+def cpu_baseline(n0, n1, seed, budget_s, threads, lam=0.01, mu=0.01, sigma=2.0):
+    """Oracle (NumPy restatement of the reference PGD path) on the host: same problem; as many PGD
+    iterations as fit in about `budget_s` seconds (bounded sample; at least 2).  threads = 1: the
+    single-thread oracle (oracle.pgd); threads > 1: its slab-parallel form (oracle.parallel, the
+    Dask-map_overlap-style split of the reference, bit-identical results)."""
     import oracle as orc
+    from oracle.parallel import pgd_tv_threaded
 
     sh = (n0, n1)
     N = n0 * n1
@@ -98,41 +196,241 @@ def cpu_baseline(n0, n1, seed, budget_s, lam=0.01, mu=0.01, sigma=2.0):
     x_gt = phantom(sh, rng).reshape(-1)
     y = orc.stencil_apply(x_gt, sh, [taps, taps], [c, c])
     y = (y + (0.01 * rng.standard_normal(N)).astype(np.float32)).astype(np.float32)
-    grad = lambda v: orc.deblur_tv_grad(v, blur, y, lam, mu, dict(arg_shape=sh))
-    prox = lambda z, t: orc.positive_orthant_prox(z)
     tau = np.float32(1 / np.float32(1.0 + (lam / mu) * 8.0))
     x0 = np.zeros(N, dtype=np.float32)
+    if threads == 1:
+        grad = lambda v: orc.deblur_tv_grad(v, blur, y, lam, mu, dict(arg_shape=sh))
+        prox = lambda z, t: orc.positive_orthant_prox(z)
+        run = lambda k: orc.pgd(x0, grad, prox, tau, k)
+    else:
+        run = lambda k: pgd_tv_threaded(x0, blur, y, lam, mu, orc.positive_orthant_prox, tau, k, threads)
     t0 = time.perf_counter()
-    orc.pgd(x0, grad, prox, tau, 1)  # warm-up (page-in, allocator) and per-iteration estimate
+    run(1)  # warm-up (page-in, allocator) and per-iteration estimate
     t1 = time.perf_counter() - t0
-    iters = int(max(2, min(500, budget_s / max(t1, 1e-3))))
+    iters = int(max(2, min(2000, budget_s / max(t1, 1e-3))))
     t0 = time.perf_counter()
-    orc.pgd(x0, grad, prox, tau, iters)
+    run(iters)
     dt = time.perf_counter() - t0
     return iters / dt, iters, dt
 
 
+# ----------------------------------------------------------------------------- timing helpers
+class Ctx:
+    def __init__(self, world, rank, dist):
+        self.world, self.rank, self.dist = world, rank, dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, v):
+        import torch
+
+        t = torch.tensor([float(v)], dtype=torch.float64, device="cuda")
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(self, v):
+        import torch
+
+        t = torch.tensor([float(v)], dtype=torch.float64, device="cuda")
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def timed_steps(ctx, gen, warmup, steps, timer=None):
+    """W untimed steps, then exactly `steps` steps bracketed by barrier + synchronize on both sides;
+    returns the max-over-ranks elapsed seconds."""
+    import torch
+
+    from pyxu_amd import _dev
+
+    for _ in range(warmup):
+        next(gen)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    if timer is not None:
+        _dev.set_launch_timer(timer)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        next(gen)
+    if timer is not None:
+        timer.interrupt()  # close the last window right behind the last launch (before the host sync)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    _dev.set_launch_timer(None)
+    return ctx.max_over_ranks(elapsed)
+
+
+def run_pgd(ctx, f, g, stop_rate, warmup, steps, fused, prime_s=0.0, kernel_timer=True):
+    """Build a PGD solver in MANUAL mode on (f, g), prime the device, time `steps` steps."""
+    import torch
+
+    import pyxu_amd.abc as pxa
+    import pyxu_amd.distributed as pdist
+    import pyxu_amd.opt.solver as pxs
+    import pyxu_amd.opt.stop as pxst
+    from pyxu_amd import _dev
+
+    like = torch.empty((1,), dtype=torch.float32, device="cuda")
+
+    def new_solver():
+        s = pxs.PGD(f=f, g=g, show_progress=False, stop_rate=stop_rate)
+        rel = pdist.ShardedRelError(eps=1e-30) if ctx.world > 1 else pxst.RelError(eps=1e-30)
+        s.fit(x0=_dev.zeros((f.dim,), like), stop_crit=pxst.MaxIter(10**9) | rel, mode=pxa.Mode.MANUAL, fused=fused)
+        return s, rel
+
+    if prime_s > 0:
+        # untimed device priming on a throwaway solver of the same problem: code objects loaded, clocks
+        # and caches at steady state before the measured solver's W + K steps (which it does not change)
+        s, _ = new_solver()
+        gen = s.steps()
+        t_end = time.perf_counter() + prime_s
+        while time.perf_counter() < t_end:
+            for _ in range(200):
+                next(gen)
+            torch.cuda.synchronize()
+        del s, gen
+    slvr, rel = new_solver()
+    # prime the stop-check path once (loads its kernels' code objects) so that a warmup shorter than
+    # stop_rate does not leave one-time module loading inside the timed region
+    rel.stop({"x": slvr._mstate["x"]})
+    rel.stop({"x": slvr._mstate["x"]})
+    rel.clear()
+    fused_on = slvr._plan is not None
+    timer = _dev.LaunchTimer(window=10**9) if (kernel_timer and fused_on) else None
+    elapsed = timed_steps(ctx, slvr.steps(), warmup, steps, timer)
+    kern_ms = timer.mean_ms() if timer is not None else None
+    return elapsed, kern_ms, slvr, (timer.launches if timer is not None else 0)
+
+
+def roofline(pixels, kern_ms, traffic):
+    alg_bytes = ALG_BYTES_PER_PIXEL * pixels  # SURVEY.md §8(d): 48 B/pixel/iteration
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    comp = FUSED_BYTES_PER_PIXEL * pixels
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": KERNEL,
+            "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes, "fused_compulsory_bytes_per_launch": comp,
+            "frac_vs_fused_compulsory": round(comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def bench_c5(ctx, args):
+    """configs[4]: 512 x 512^2 batched TV-deblur, images sharded over the ranks (strong scaling)."""
+    import pyxu_amd.distributed as pdist
+    import pyxu_amd.runtime as pxrt
+
+    total, n = args.c5_images, args.c5_n
+    lo, hi = pdist.shard_range(total, ctx.rank, ctx.world)
+    f, g = build_batch_problem(hi - lo, n, lo, seed=77)
+    K = args.c5_steps
+    sr = auto_stop_rate(K)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        elapsed, kern_ms, slvr, launches = run_pgd(ctx, f, g, sr, args.c5_warmup, K, True)
+    kern_ms = ctx.max_over_ranks(kern_ms if kern_ms is not None else 0.0)
+    rec = {"workload": f"PGD {total} x {n}x{n} batch-as-axis Gaussian(sigma=2) + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
+           "images": total, "images_per_rank": hi - lo, "scaling": "strong", "steps": K, "warmup": args.c5_warmup,
+           "stop_rate": sr, "value": round(total * K / elapsed, 1), "unit": "image-iterations/s",
+           "ms_per_step": round(1e3 * elapsed / K, 4), "stop_crit": "MaxIter | RelError (global all-reduce)"}
+    if kern_ms > 0:
+        rec["roofline"] = roofline((hi - lo) * n * n, kern_ms, measured_traffic(KERNEL, f"{hi - lo}x{n}x{n}"))
+        rec["roofline"]["note"] = "per rank (slowest rank's kernel time)"
+    del slvr
+    return rec
+
+
+def bench_c4(ctx, args):
+    """configs[3]: ADMM + lam L1 on a dense M x N K (QuadraticFunc.prox -> CG on K^T K + I/tau);
+    K row-sharded over the ranks: K p local, K^T z = one all-reduce of the N-vector per CG step."""
+    import torch
+
+    import pyxu_amd.abc as pxa
+    import pyxu_amd.distributed as pdist
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.opt.solver as pxs
+    import pyxu_amd.opt.stop as pxst
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd.opt.solver.cg import CG
+
+    M, N = args.c4_m, args.c4_n
+    lo, hi = pdist.shard_range(M, ctx.rank, ctx.world)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1000 + ctx.rank)
+    # synthetic data (torch RNG only creates the inputs; every solver operation is a HIP kernel)
+    Kr = torch.randn((hi - lo, N), generator=gen, device="cuda", dtype=torch.float32)
+    Kr.mul_(1.0 / np.sqrt(M))
+    rng = np.random.default_rng(5)
+    xs = np.zeros(N, np.float32)
+    xs[rng.choice(N, 64, replace=False)] = rng.standard_normal(64).astype(np.float32)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        K = pdist.RowShardedLinOp(Kr, M) if ctx.world > 1 else pxa.LinOp.from_array(Kr)
+        from pyxu_amd.util import to_device
+
+        from pyxu_amd import _dev
+
+        y = K.apply(to_device(xs))
+        y = _dev.axpby(1.0, y, 0.01, torch.randn(y.shape, generator=gen, device="cuda", dtype=torch.float32))
+        f = 0.5 * pxo.SquaredL2Norm(dim=hi - lo).asloss(y) * K
+        h = args.c4_lam * pxo.L1Norm(dim=N)
+        s = pxs.ADMM(f=f, h=h, show_progress=False)
+        s.fit(x0=torch.zeros((N,), device="cuda", dtype=torch.float32), tau=1.0,
+              stop_crit=pxst.MaxIter(10**9), mode=pxa.Mode.MANUAL)
+        it = s.steps()
+        for _ in range(args.c4_warmup):
+            next(it)
+        c0 = CG.steps_taken
+        elapsed = timed_steps(ctx, it, 0, args.c4_steps)
+        cg_steps = CG.steps_taken - c0  # inner CG iterations of the timed outer iterations
+    per_outer = cg_steps / max(1, args.c4_steps)
+    cg_ms = 1e3 * elapsed / max(1.0, per_outer * args.c4_steps)
+    pair_bytes = 2 * (hi - lo) * N * 4  # one K p + one K^T z pass over the local K per CG iteration
+    rec = {"workload": f"ADMM dense {M}x{N} K + lam*L1 (x-update: QuadraticFunc.prox -> CG), tau=1",
+           "rows_per_rank": hi - lo, "scaling": "strong", "steps": args.c4_steps, "warmup": args.c4_warmup,
+           "value": round(args.c4_steps / elapsed, 3), "unit": "ADMM outer iterations/s",
+           "ms_per_step": round(1e3 * elapsed / args.c4_steps, 3), "cg_iters_per_outer": round(per_outer, 2),
+           "ms_per_cg_iter": round(cg_ms, 4),
+           "roofline": {"bound": "hbm", "achieved": round(pair_bytes / (cg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(pair_bytes / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "note": "whole CG iteration vs the two compulsory passes over this rank's K (SURVEY §8(d) C4)"}}
+    del s, K, Kr
+    torch.cuda.empty_cache()
+    return rec
+
+
+# ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=2048, help="image side (configs[1]: 2048)")
-    ap.add_argument("--stop-rate", type=int, default=50, help="stop-criterion evaluation rate (reference default 1)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget in s (0 = skip)")
+    ap.add_argument("--stop-rate", type=int, default=0, help="stop-criterion rate (0: largest divisor of --steps <= 50)")
+    ap.add_argument("--prime-seconds", type=float, default=0.4, help="untimed device priming before the warmup")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget per leg in s (0 = skip)")
     ap.add_argument("--generic", action="store_true", help="disable the fused m_step (rule-by-rule HIP path)")
     ap.add_argument("--no-kernel-timer", action="store_true", help="skip the in-region HIP-event kernel timing (A/B)")
+    ap.add_argument("--no-sub", action="store_true", help="headline line only (no stop_rate_1 / c5 / c4 records)")
+    ap.add_argument("--c5-images", type=int, default=512)
+    ap.add_argument("--c5-n", type=int, default=512)
+    ap.add_argument("--c5-steps", type=int, default=20)
+    ap.add_argument("--c5-warmup", type=int, default=5)
+    ap.add_argument("--c4-m", type=int, default=8192)
+    ap.add_argument("--c4-n", type=int, default=65536)
+    ap.add_argument("--c4-steps", type=int, default=4)
+    ap.add_argument("--c4-warmup", type=int, default=1)
+    ap.add_argument("--c4-lam", type=float, default=0.01)
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(sys.argv[1:], args.gpus))
 
     import torch
     import torch.distributed as dist
 
     import pyxu_amd
-    import pyxu_amd.abc as pxa
-    import pyxu_amd.opt.solver as pxs
-    import pyxu_amd.opt.stop as pxst
     import pyxu_amd.runtime as pxrt
-    from pyxu_amd import _dev
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -141,6 +439,7 @@ def main():
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
     distributed = world > 1
+    backend = None
     if distributed:
         backend = os.environ.get("PXA_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI; gloo for rehearsals
         if backend == "nccl":
@@ -149,73 +448,48 @@ def main():
             dist.init_process_group(backend=backend)
     if not pyxu_amd.native_loaded():
         raise RuntimeError("libpyxu_amd.so not loaded")
+    ctx = Ctx(world, rank, dist)
 
     n0 = n1 = args.n
     N = n0 * n1
-    f, g, y = build_problem(n0, n1, seed=1234 + rank)
+    sr = args.stop_rate or auto_stop_rate(args.steps)
+    f, g, _ = build_problem(n0, n1, seed=1234 + rank)
     with pxrt.Precision(pxrt.Width.SINGLE):
-        slvr = pxs.PGD(f=f, g=g, show_progress=False, stop_rate=args.stop_rate)
-        # N>1: the ranks' images form one batch-as-axis problem (C5 semantics): the stop check is the
-        # GLOBAL RelError, one RCCL all-reduce of 2 doubles per check (pyxu_amd.distributed)
-        import pyxu_amd.distributed as pdist
+        elapsed_max, kern_ms, slvr, launches = run_pgd(ctx, f, g, sr, args.warmup, args.steps, not args.generic,
+                                                       prime_s=args.prime_seconds, kernel_timer=not args.no_kernel_timer)
+    fused = slvr._plan is not None
+    stack = slvr._plan["stack"] if fused else 1
+    del slvr
 
-        rel = pdist.ShardedRelError(eps=1e-30) if distributed else pxst.RelError(eps=1e-30)
-        stop = pxst.MaxIter(10**9) | rel
-        slvr.fit(x0=_dev.zeros((N,), y), stop_crit=stop, mode=pxa.Mode.MANUAL, fused=not args.generic)
-        fused = slvr._plan is not None
-        # prime the stop-check path once (loads its kernels' code objects) so that a warmup shorter
-        # than stop_rate does not leave one-time module loading inside the timed region
-        rel.stop({"x": slvr._mstate["x"]})
-        rel.stop({"x": slvr._mstate["x"]})
-        rel.clear()
-        gen = slvr.steps()
-        for _ in range(args.warmup):
-            next(gen)
-        torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        # one HIP-event window per run of back-to-back fused launches, closed only where other device work
-        # (the stop check) is enqueued: an event record between two launches costs a ~11 us bubble
-        # (rocprofv3 trace, r01c), so per-10-launch windows would tax the timed step by ~1 us
-        timer = _dev.LaunchTimer(window=10**9)
-        if not args.no_kernel_timer:
-            _dev.set_launch_timer(timer)  # HIP-event windows around the fused-step launches, on their stream
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            next(gen)
-        timer.interrupt()  # close the last window right behind the last launch (before the host sync)
-        torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        _dev.set_launch_timer(None)
-        kern_ms = timer.mean_ms() if fused else None
-
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
+    sub = {}
+    if not args.no_sub:
+        with pxrt.Precision(pxrt.Width.SINGLE):
+            e1, _, s1, _ = run_pgd(ctx, f, g, 1, args.warmup, args.steps, not args.generic, kernel_timer=False)
+            del s1
+        sub["stop_rate_1"] = {"value": round(world * args.steps / e1, 2), "unit": "image-iterations/s",
+                              "ms_per_step": round(1e3 * e1 / args.steps, 4), "stop_rate": 1, "steps": args.steps}
+        del f, g
+        torch.cuda.empty_cache()
+        sub["c5"] = bench_c5(ctx, args)
+        torch.cuda.empty_cache()
+        sub["c4"] = bench_c4(ctx, args)
 
     if rank == 0:
         value = world * args.steps / elapsed_max
         roof = None
         if kern_ms is not None:
-            pix = N * slvr._plan["stack"]
-            alg_bytes = ALG_BYTES_PER_PIXEL * pix  # 48 B/pixel/iteration
-            achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-            traffic = measured_traffic(KERNEL, n0, n1)
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": KERNEL,
-                    "kernel_ms": round(kern_ms, 5), "launches_timed": timer.launches,
-                    "alg_bytes_per_launch": alg_bytes,
-                    "fused_compulsory_bytes_per_launch": FUSED_BYTES_PER_PIXEL * pix,
-                    "frac_vs_fused_compulsory": round(FUSED_BYTES_PER_PIXEL * pix / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            roof = roofline(N * stack, kern_ms, measured_traffic(KERNEL, f"{n0}x{n1}"))
+            roof["launches_timed"] = launches
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
-            v, it, dt = cpu_baseline(n0, n1, seed=1234, budget_s=args.cpu_seconds)
-            cpu = {"value": round(v, 4), "unit": "image-iterations/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle/ NumPy restatement of the reference PGD path (single thread), same {n0}x{n1} "
-                             f"TV-deblur problem, {it} iterations in {dt:.1f} s on {cpu_model()}"}
+            v1, it1, dt1 = cpu_baseline(n0, n1, seed=1234, budget_s=args.cpu_seconds, threads=1)
+            th = max(1, min(CPU_THREADS_MAX, os.cpu_count() or 1))
+            vn, itn, dtn = cpu_baseline(n0, n1, seed=1234, budget_s=args.cpu_seconds, threads=th)
+            cpu = {"value": round(vn, 4), "unit": "image-iterations/s", "cores": th, "kind": "port",
+                   "sample": f"oracle/ NumPy restatement of the reference PGD path, same {n0}x{n1} TV-deblur problem, "
+                             f"slab-parallel over {th} threads (oracle/parallel.py, bit-identical to the 1-thread oracle): "
+                             f"{itn} iterations in {dtn:.1f} s on {cpu_model()}",
+                   "single_core": {"value": round(v1, 4), "cores": 1, "sample": f"{it1} iterations in {dt1:.1f} s"}}
         line = {
             "metric": "solver iterations/s (PGD, TV-regularised deblur)",
             "value": round(value, 2),
@@ -228,12 +502,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (piecewise-constant phantom, Gaussian blur, 1% noise)",
+            "data": "synthetic (piecewise-constant phantom, Gaussian blur, 1% noise; random dense K for c4)",
             "config": {"workload": f"PGD {n0}x{n1} Gaussian(sigma=2) deblur + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
-                       "image": [n0, n1], "images_per_gpu": 1, "stop_rate": args.stop_rate,
-                       "stop_crit": "MaxIter | RelError" + (f" (global, {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} all-reduce)" if world > 1 else ""), "fused_m_step": fused, "parallelism": f"batch-as-axis slabs x{world} (one image per rank)"},
+                       "image": [n0, n1], "images_per_gpu": 1, "stop_rate": sr,
+                       "stop_crit": "MaxIter | RelError" + (f" (global, {'RCCL' if backend == 'nccl' else backend} all-reduce)" if world > 1 else ""),
+                       "fused_m_step": fused, "parallelism": f"independent images x{world} (one per rank)"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            **sub,
         }
         print(json.dumps(line), flush=True)
     if distributed:

@@ -34,6 +34,8 @@ class _HostRows:
 class CG(pxa.Solver):
     """Solve ``A x = b`` for positive-definite ``A`` (cg.py:14-187)."""
 
+    steps_taken = 0  # process-wide count of CG iterations (diagnostic: inner iterations of ADMM / prox)
+
     def __init__(self, A, **kwargs):
         kwargs.update(log_var=kwargs.get("log_var", ("x",)))
         super().__init__(**kwargs)
@@ -69,6 +71,7 @@ class CG(pxa.Solver):
         row (pxa_axpy_rows), so a step has ONE host read: ||r||^2 for the eps test, issued as an async
         copy at the end of the previous step."""
         mst = self._mstate
+        CG.steps_taken += 1
         x, r, p = mst["x"], mst["residual"], mst["conjugate_dir"]
         Ap = self._A.apply(p)
         pAp = _dev.row_reduce(_dev.RED_DOT, _rows2d(p), _rows2d(Ap))

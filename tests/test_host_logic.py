@@ -211,3 +211,65 @@ def test_host_arrays_are_rejected_loudly():
         op.prox(np.ones(4), 0.1)
     with pytest.raises(TypeError):
         op.prox(torch.ones(4, dtype=torch.float64), 0.1)  # CPU tensor: no CPU compute path
+
+
+# ----------------------------------------------------------------------------- bench harness (no GPU)
+def test_bench_auto_stop_rate():
+    import bench
+
+    assert bench.auto_stop_rate(20) == 20
+    assert bench.auto_stop_rate(200) == 50
+    assert bench.auto_stop_rate(60) == 30
+    assert bench.auto_stop_rate(97) == 1
+    assert bench.auto_stop_rate(7) == 7
+
+
+def test_bench_launcher_rank_envs_and_argv(tmp_path):
+    """`bench.py --gpus N` self-launch: N children, each with its RANK / LOCAL_RANK / WORLD_SIZE and a
+    127.0.0.1 rendezvous, started with the parent's argv (no GPU is touched by the parent)."""
+    import sys
+
+    import bench
+
+    envs = bench.rank_envs(3, 29555, base={"PATH": "/bin"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2"]
+    assert all(e["WORLD_SIZE"] == "3" and e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29555" for e in envs)
+    # run the real launcher on a stand-in script that records its env and argv
+    script = tmp_path / "child.py"
+    script.write_text(
+        "import os, sys, json\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'r' + os.environ['RANK'] + '.json'), 'w').write(json.dumps("
+        "{'argv': sys.argv[1:], 'world': os.environ['WORLD_SIZE'], 'local': os.environ['LOCAL_RANK'], "
+        "'addr': os.environ['MASTER_ADDR']}))\n")
+    rc = bench.launch(["--gpus", "2", "--steps", "20"], 2, script=str(script))
+    assert rc == 0
+    import json
+
+    for r in range(2):
+        rec = json.loads((tmp_path / f"r{r}.json").read_text())
+        assert rec == {"argv": ["--gpus", "2", "--steps", "20"], "world": "2", "local": str(r), "addr": "127.0.0.1"}
+    # a failing rank makes the launcher fail (and stops the others)
+    bad = tmp_path / "bad.py"
+    bad.write_text("import os, sys, time\nif os.environ['RANK'] == '1': sys.exit(3)\ntime.sleep(30)\n")
+    assert bench.launch([], 2, script=str(bad)) == 3
+
+
+def test_threaded_cpu_baseline_is_the_oracle():
+    """bench.py's all-core CPU baseline (oracle/parallel.py) computes the single-thread oracle's PGD
+    iterates bit for bit."""
+    from oracle.parallel import pgd_tv_threaded
+
+    sh = (97, 130)
+    rng = np.random.default_rng(0)
+    y = rng.standard_normal(sh[0] * sh[1]).astype(np.float32)
+    taps, c = orc.gaussian_taps(2.0, 3.0, np.float32)
+    blur = dict(arg_shape=sh, kernel=[taps, taps], center=[c, c])
+    lam = mu = 0.01
+    tau = np.float32(1 / np.float32(1 + 8 * lam / mu))
+    x0 = rng.uniform(0, 1, sh[0] * sh[1]).astype(np.float32)
+    grad = lambda v: orc.deblur_tv_grad(v, blur, y, lam, mu, dict(arg_shape=sh))
+    ref, _ = orc.pgd(x0, grad, lambda z, t: orc.positive_orthant_prox(z), tau, 4)
+    for th in (1, 4, 9):
+        out, _ = pgd_tv_threaded(x0, blur, y, lam, mu, orc.positive_orthant_prox, tau, 4, th)
+        assert np.array_equal(out, ref)
