@@ -412,6 +412,7 @@ def main():
     ap.add_argument("--generic", action="store_true", help="disable the fused m_step (rule-by-rule HIP path)")
     ap.add_argument("--no-kernel-timer", action="store_true", help="skip the in-region HIP-event kernel timing (A/B)")
     ap.add_argument("--no-sub", action="store_true", help="headline line only (no stop_rate_1 / c5 / c4 records)")
+    ap.add_argument("--pgd-kernel", type=int, default=0, help="PXA_TUNE_PGD_KERNEL (0 auto = tile kernel, 5 persistent LDS-DMA)")
     ap.add_argument("--c5-images", type=int, default=512)
     ap.add_argument("--c5-n", type=int, default=512)
     ap.add_argument("--c5-steps", type=int, default=20)
@@ -448,6 +449,9 @@ def main():
             dist.init_process_group(backend=backend)
     if not pyxu_amd.native_loaded():
         raise RuntimeError("libpyxu_amd.so not loaded")
+    from pyxu_amd import _dev
+
+    _dev.tuning(_dev.TUNE_PGD_KERNEL, args.pgd_kernel)
     ctx = Ctx(world, rank, dist)
 
     n0 = n1 = args.n
@@ -506,7 +510,8 @@ def main():
             "config": {"workload": f"PGD {n0}x{n1} Gaussian(sigma=2) deblur + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
                        "image": [n0, n1], "images_per_gpu": 1, "stop_rate": sr,
                        "stop_crit": "MaxIter | RelError" + (f" (global, {'RCCL' if backend == 'nccl' else backend} all-reduce)" if world > 1 else ""),
-                       "fused_m_step": fused, "parallelism": f"independent images x{world} (one per rank)"},
+                       "fused_m_step": fused, "pgd_kernel": "persistent LDS-DMA" if args.pgd_kernel == 5 else "tile",
+                       "parallelism": f"independent images x{world} (one per rank)"},
             "roofline": roof,
             "cpu_baseline": cpu,
             **sub,

@@ -47,6 +47,10 @@ extern "C" {
 #define PXA_MODE_SYMMETRIC 3
 #define PXA_MODE_EDGE 4
 
+/* Kernel-selection knobs (pxa_tuning). */
+#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 auto (= 4, the tile kernel), 5 persistent LDS-DMA kernel (fp32) */
+#define PXA_TUNE_COUNT 8
+
 /* Row reductions (pxa_row_reduce). */
 #define PXA_RED_SUMSQ 0  /* sum x^2            : SquaredL2Norm.apply, norm(ord=2)^2   (norm.py:91-94) */
 #define PXA_RED_DIFFSQ 1 /* sum (x-y)^2        : RelError numerator (opt/stop.py:365-371) */
@@ -63,6 +67,11 @@ const char* pxa_version(void);
 const char* pxa_error_string(int code);
 /* Number of exported compute entry points (for the loader's self-check). */
 int pxa_abi_version(void);
+
+/* Process-wide kernel-selection knob `key` (PXA_TUNE_*): sets it to `value` when value >= 0 and
+ * returns the previous value (PXA_ERR_ARG for an unknown key).  Defaults (0) pick the fastest
+ * kernel; the other values exist for A/B measurements and the parity tests between variants. */
+int pxa_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------------
  * Element-wise kernels: the arithmetic glue of the operator algebra
@@ -238,6 +247,60 @@ int pxa_gradient2_adjoint(int dtype, int64_t stack, int ndim, const int64_t* sha
 size_t pxa_dense_workspace_bytes(int dtype, int trans, int64_t M, int64_t N, int64_t B);
 int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, const void* A, const void* X, void* Y,
                      void* work, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Array primitives: the data movement of the operator algebra and the NumPy-named functions of the
+ * backend's array module (SURVEY.md §8(b) `xp` list), so that no array arithmetic of the product path
+ * runs outside this library.
+ * ------------------------------------------------------------------------------------------- */
+
+/* dst[r*ldd + i] = src[r*lds + i]  (+ dst[r*ldd + i] when accumulate != 0), r < rows, i < n.
+ * Block operators (operator/blocks.py:660-679, 838-860: slicing arr[..., off:off+dim], the row sums
+ * of hstack.apply / vstack.adjoint, concatenate), lds = 0 broadcasts one row (CG x0 broadcast,
+ * opt/solver/cg.py:96-110), diagonal extraction (lds = n + 1). */
+int pxa_copy2d(int dtype, int64_t rows, int64_t n, const void* src, int64_t lds, void* dst, int64_t ldd, int accumulate,
+               void* stream);
+
+/* out = f(x): op 0 sqrt, 1 sign (numpy.sign), 2 fabs, 3 negative, 4 square, 5 reciprocal. */
+#define PXA_UN_SQRT 0
+#define PXA_UN_SIGN 1
+#define PXA_UN_ABS 2
+#define PXA_UN_NEG 3
+#define PXA_UN_SQUARE 4
+#define PXA_UN_RECIP 5
+int pxa_unary(int dtype, int op, int64_t n, const void* x, void* out, void* stream);
+
+/* out = f(x, y) with x / y arrays of n elements or NULL for the broadcast scalars xs / ys:
+ * op 0 fmax, 1 fmin (NaN-ignoring, numpy.fmax/fmin), 2 add, 3 subtract, 4 multiply, 5 divide,
+ * 6 maximum, 7 minimum (NaN-propagating), 8 power. */
+#define PXA_BIN_FMAX 0
+#define PXA_BIN_FMIN 1
+#define PXA_BIN_ADD 2
+#define PXA_BIN_SUB 3
+#define PXA_BIN_MUL 4
+#define PXA_BIN_DIV 5
+#define PXA_BIN_MAXIMUM 6
+#define PXA_BIN_MINIMUM 7
+#define PXA_BIN_POW 8
+int pxa_binary(int dtype, int op, int64_t n, const void* x, double xs, const void* y, double ys, void* out,
+               void* stream);
+
+/* numpy.where(cond, x, y): cond is n bytes (bool), x / y arrays or NULL for scalars xs / ys. */
+int pxa_where(int dtype, int64_t n, const void* cond, const void* x, double xs, const void* y, double ys, void* out,
+              void* stream);
+
+/* out[i] = isnan(x[i]) as bytes; pxa_bool_reduce: out[0] = any (mode 0) / all (mode 1) of n bytes. */
+int pxa_isnan(int dtype, int64_t n, const void* x, void* out, void* stream);
+int pxa_bool_reduce(int64_t n, int mode, const void* x, void* out, void* stream);
+
+/* out = (dtype_out) x: float64 statistics to the array dtype and back. */
+int pxa_cast(int dtype_in, int dtype_out, int64_t n, const void* x, void* out, void* stream);
+
+/* out[r*ld + off + r] = value, r < rows (identity columns of LinOp.asarray, operator.py:1593-1628). */
+int pxa_set_diag(int dtype, int64_t rows, int64_t ld, int64_t off, double value, void* out, void* stream);
+
+/* dst (cols x rows) = src (rows x cols)^T (LinOp.asarray / TransposeRule.asarray, arithmetic.py:1496). */
+int pxa_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* dst, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused solver steps (the whole m_step of a recognised problem in one launch).

@@ -149,6 +149,18 @@ def storage_exclusive(t) -> bool:
     return _USE_COUNT(t.untyped_storage()._cdata) <= 2
 
 
+TUNE_PGD_KERNEL = 0  # PXA_TUNE_PGD_KERNEL: 0 auto (tile kernel), 5 persistent LDS-DMA kernel
+
+
+def tuning(key, value=-1):
+    """Process-wide kernel-selection knob of the C-ABI (pxa_tuning): sets it when value >= 0 and
+    returns the previous value.  For A/B measurements and variant-parity tests only."""
+    r = int(lib.pxa_tuning(int(key), int(value)))
+    if r < 0:
+        check(r, "pxa_tuning")
+    return r
+
+
 def empty(shape, like):
     return _torch().empty(shape, dtype=like.dtype, device=like.device)
 
@@ -320,6 +332,125 @@ def group_norm(x, outer, group, inner):
     x = require(x)
     out = empty((outer * inner,), x)
     check(lib.pxa_group_norm(dtcode(x), outer, group, inner, ptr(x), ptr(out), stream()), "pxa_group_norm")
+    return out
+
+
+# ------------------------------------------------------------------ array primitives (csrc/array.hip)
+UN_SQRT, UN_SIGN, UN_ABS, UN_NEG, UN_SQUARE, UN_RECIP = range(6)
+BIN_FMAX, BIN_FMIN, BIN_ADD, BIN_SUB, BIN_MUL, BIN_DIV, BIN_MAXIMUM, BIN_MINIMUM, BIN_POW = range(9)
+
+
+def copy2d(src, dst, rows, n, lds, ldd, src_off=0, dst_off=0, accumulate=False):
+    """dst[dst_off + r*ldd + i] (+)= src[src_off + r*lds + i] for r < rows, i < n (element offsets)."""
+    es = src.element_size()
+    check(lib.pxa_copy2d(dtcode(src), int(rows), int(n), ptr(src) + int(src_off) * es, int(lds),
+                         ptr(dst) + int(dst_off) * es, int(ldd), int(bool(accumulate)), stream()), "pxa_copy2d")
+    return dst
+
+
+def take_cols(x, off, n):
+    """x[..., off:off + n] as a contiguous device array (a view when x has no leading stack)."""
+    x = require(x)
+    d = x.shape[-1]
+    if x.ndim == 1 or x.numel() == d:
+        return x.reshape(-1)[off:off + n].reshape(*x.shape[:-1], n)
+    rows = x.numel() // d
+    out = empty((*x.shape[:-1], n), x)
+    return copy2d(x, out, rows, n, d, n, src_off=off)
+
+
+def concat_cols(parts, out=None):
+    """numpy.concatenate(parts, axis=-1) for device arrays with equal leading shapes."""
+    parts = [require(p) for p in parts]
+    lead = parts[0].shape[:-1]
+    total = sum(p.shape[-1] for p in parts)
+    out = empty((*lead, total), parts[0]) if out is None else out
+    rows = out.numel() // max(total, 1)
+    off = 0
+    for p in parts:
+        copy2d(p, out, rows, p.shape[-1], p.shape[-1], total, dst_off=off)
+        off += p.shape[-1]
+    return out
+
+
+def unary(op, x, out=None):
+    x = require(x)
+    out = empty_like(x) if out is None else out
+    check(lib.pxa_unary(dtcode(x), int(op), x.numel(), ptr(x), ptr(out), stream()), "pxa_unary")
+    return out
+
+
+def binary(op, x, y, out=None, like=None):
+    """out = op(x, y); x / y device arrays of one shape or Python scalars (broadcast)."""
+    xa = None if np.isscalar(x) else require(x, "x")
+    ya = None if np.isscalar(y) else require(y, "y")
+    ref = xa if xa is not None else (ya if ya is not None else like)
+    if xa is not None and ya is not None:
+        assert xa.shape == ya.shape and xa.dtype == ya.dtype, "binary: shapes / dtypes differ"
+    out = empty_like(ref) if out is None else out
+    check(lib.pxa_binary(dtcode(ref), int(op), ref.numel(), ptr(xa) if xa is not None else None,
+                         float(x) if xa is None else 0.0, ptr(ya) if ya is not None else None,
+                         float(y) if ya is None else 0.0, ptr(out), stream()), "pxa_binary")
+    return out
+
+
+def where(cond, x, y, like=None):
+    torch = _torch()
+    cond = require_bool(cond)
+    xa = None if np.isscalar(x) else require(x, "x")
+    ya = None if np.isscalar(y) else require(y, "y")
+    ref = xa if xa is not None else (ya if ya is not None else like)
+    out = empty(cond.shape, ref)
+    assert out.numel() == cond.numel()
+    check(lib.pxa_where(dtcode(ref), out.numel(), cond.data_ptr(), ptr(xa) if xa is not None else None,
+                        float(x) if xa is None else 0.0, ptr(ya) if ya is not None else None,
+                        float(y) if ya is None else 0.0, ptr(out), stream()), "pxa_where")
+    return out
+
+
+def require_bool(c):
+    torch = _torch()
+    if not (hasattr(c, "is_cuda") and c.is_cuda and c.dtype == torch.bool):
+        raise TypeError("pyxu_amd: condition must be a boolean device tensor")
+    return c if c.is_contiguous() else c.contiguous()
+
+
+def isnan(x):
+    torch = _torch()
+    x = require(x)
+    out = torch.empty(x.shape, dtype=torch.bool, device=x.device)
+    check(lib.pxa_isnan(dtcode(x), x.numel(), ptr(x), out.data_ptr(), stream()), "pxa_isnan")
+    return out
+
+
+def bool_reduce(c, mode):
+    """any (mode 0) / all (mode 1) of a boolean device tensor -> 0-d boolean device tensor."""
+    torch = _torch()
+    c = require_bool(c)
+    out = torch.empty((), dtype=torch.bool, device=c.device)
+    check(lib.pxa_bool_reduce(c.numel(), int(mode), c.data_ptr(), out.data_ptr(), stream()), "pxa_bool_reduce")
+    return out
+
+
+def cast(x, dtype_like):
+    """(dtype of dtype_like) copy of x (float32 <-> float64)."""
+    x = require(x)
+    out = _torch().empty(x.shape, dtype=dtype_like.dtype, device=x.device)
+    check(lib.pxa_cast(dtcode(x), dtcode(out), x.numel(), ptr(x), ptr(out), stream()), "pxa_cast")
+    return out
+
+
+def set_diag(out, rows, ld, off, value):
+    check(lib.pxa_set_diag(dtcode(out), int(rows), int(ld), int(off), float(value), ptr(out), stream()), "pxa_set_diag")
+    return out
+
+
+def transpose(x):
+    """(rows, cols) -> contiguous (cols, rows)."""
+    x = require(x)
+    rows, cols = x.shape
+    out = empty((cols, rows), x)
+    check(lib.pxa_transpose(dtcode(x), rows, cols, ptr(x), ptr(out), stream()), "pxa_transpose")
     return out
 
 

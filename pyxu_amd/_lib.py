@@ -23,6 +23,7 @@ EXPORTS = {
     "pxa_version": (ct.c_char_p, []),
     "pxa_error_string": (ct.c_char_p, [i32]),
     "pxa_abi_version": (i32, []),
+    "pxa_tuning": (i32, [i32, i32]),
     "pxa_axpby": (i32, [i32, i64, f64, vp, f64, vp, vp, vp]),
     "pxa_axpby_bcast": (i32, [i32, i64, f64, vp, f64, vp, i64, vp, vp]),
     "pxa_axpy_rows": (i32, [i32, i64, i64, vp, f64, vp, vp, vp, vp]),
@@ -57,6 +58,15 @@ EXPORTS = {
     "pxa_gradient2_adjoint": (i32, [i32, i64, i32, P_i64, i32, P_int, P_int, P_f64, P_int, P_f64, vp, vp, vp]),
     "pxa_dense_workspace_bytes": (sz, [i32, i32, i64, i64, i64]),
     "pxa_dense_matmat": (i32, [i32, i32, i64, i64, i64, vp, vp, vp, vp, vp]),
+    "pxa_copy2d": (i32, [i32, i64, i64, vp, i64, vp, i64, i32, vp]),
+    "pxa_unary": (i32, [i32, i32, i64, vp, vp, vp]),
+    "pxa_binary": (i32, [i32, i32, i64, vp, f64, vp, f64, vp, vp]),
+    "pxa_where": (i32, [i32, i64, vp, vp, f64, vp, f64, vp, vp]),
+    "pxa_cast": (i32, [i32, i32, i64, vp, vp, vp]),
+    "pxa_isnan": (i32, [i32, i64, vp, vp, vp]),
+    "pxa_bool_reduce": (i32, [i64, i32, vp, vp, vp]),
+    "pxa_set_diag": (i32, [i32, i64, i64, i64, f64, vp, vp]),
+    "pxa_transpose": (i32, [i32, i64, i64, vp, vp, vp]),
     "pxa_pgd_tv2d_partials_count": (i32, [i64, i64, i64]),
     "pxa_pgd_tv2d_step": (
         i32,

@@ -22,4 +22,18 @@ const char* pxa_error_string(int code) {
   }
 }
 
+// Process-wide kernel-selection knobs (A/B measurements and parity tests of kernel variants).
+static int g_tuning[PXA_TUNE_COUNT] = {0};
+
+int pxa_tuning(int key, int value) {
+  if (key < 0 || key >= PXA_TUNE_COUNT) return PXA_ERR_ARG;
+  const int prev = g_tuning[key];
+  if (value >= 0) g_tuning[key] = value;
+  return prev;
+}
+
 }  // extern "C"
+
+namespace pxa {
+int tuning(int key) { return (key >= 0 && key < PXA_TUNE_COUNT) ? g_tuning[key] : 0; }
+}  // namespace pxa

@@ -1,0 +1,285 @@
+// Array primitives of the operator algebra and of the NumPy-named `xp` shim: strided 2-D copies /
+// accumulations (block-operator concatenation and sums, blocks.py:660-679, 838-860; broadcasts),
+// element-wise unary / binary maps, where, dtype casts, diagonal writes and transposes.  They keep
+// every array operation of the product path inside this library (no torch arithmetic).
+//
+// All are HBM-bound streaming kernels: 16-B vectors where the rows allow it, grid-stride loops.
+#include "common.hpp"
+
+namespace pxa {
+namespace {
+
+// dst[r * ldd + i] = src[r * lds + i] (+ dst[r * ldd + i] when acc)     r < rows, i < n
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(kBlock) copy2d_kernel(int64_t rows, int64_t n, const T* src, int64_t lds, T* dst,
+                                                        int64_t ldd, int acc) {
+  constexpr int V = VEC ? kVecN<T> : 1;
+  using VT = typename Vec4<T>::type;
+  const int64_t nv = n / V;
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    const T* s = src + r * lds;
+    T* d = dst + r * ldd;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+      if constexpr (VEC) {
+        VT v = reinterpret_cast<const VT*>(s)[i];
+        if (acc) {
+          const VT o = reinterpret_cast<const VT*>(d)[i];
+          T* pv = reinterpret_cast<T*>(&v);
+          const T* po = reinterpret_cast<const T*>(&o);
+#pragma unroll
+          for (int k = 0; k < V; ++k) pv[k] = po[k] + pv[k];
+        }
+        reinterpret_cast<VT*>(d)[i] = v;
+      } else {
+        d[i] = acc ? d[i] + s[i] : s[i];
+      }
+    }
+  }
+}
+
+enum UnaryOp { kSqrt = 0, kSign = 1, kAbs = 2, kNeg = 3, kSquare = 4, kReciprocal = 5 };
+
+template <typename T>
+__device__ inline T unary(int op, T x) {
+  switch (op) {
+    case kSqrt:
+      return sqrt(x);
+    case kSign:  // numpy.sign: -1 / 0 / +1, NaN stays NaN
+      return x > T(0) ? T(1) : (x < T(0) ? T(-1) : x);
+    case kAbs:
+      return fabs(x);
+    case kNeg:
+      return -x;
+    case kSquare:
+      return x * x;
+    default:
+      return T(1) / x;
+  }
+}
+
+enum BinaryOp { kFmax = 0, kFmin = 1, kAdd = 2, kSub = 3, kMul = 4, kDiv = 5, kMaximum = 6, kMinimum = 7, kPow = 8 };
+
+template <typename T>
+__device__ inline T binary(int op, T a, T b) {
+  switch (op) {
+    case kFmax:  // numpy.fmax: NaN-ignoring
+      return fmax(a, b);
+    case kFmin:
+      return fmin(a, b);
+    case kAdd:
+      return a + b;
+    case kSub:
+      return a - b;
+    case kMul:
+      return a * b;
+    case kDiv:
+      return a / b;
+    case kMaximum:  // numpy.maximum: NaN-propagating
+      return (a != a || b != b) ? a + b : (a > b ? a : b);
+    case kMinimum:
+      return (a != a || b != b) ? a + b : (a < b ? a : b);
+    default:
+      return pow(a, b);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) unary_kernel(int64_t n, int op, const T* x, T* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = unary<T>(op, x[i]);
+}
+
+// x / y: arrays, or NULL for the broadcast scalars xs / ys
+template <typename T>
+__global__ void __launch_bounds__(kBlock) binary_kernel(int64_t n, int op, const T* x, T xs, const T* y, T ys,
+                                                        T* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = binary<T>(op, x ? x[i] : xs, y ? y[i] : ys);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) where_kernel(int64_t n, const unsigned char* cond, const T* x, T xs,
+                                                       const T* y, T ys, T* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = cond[i] ? (x ? x[i] : xs) : (y ? y[i] : ys);
+}
+
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(kBlock) cast_kernel(int64_t n, const TI* x, TO* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (TO)x[i];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) set_diag_kernel(int64_t rows, int64_t ld, int64_t off, T v, T* out) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x)
+    out[r * ld + off + r] = v;
+}
+
+// dst (cols, rows) = src (rows, cols)^T through a 32 x 33 LDS tile (conflict-free column reads)
+template <typename T>
+__global__ void __launch_bounds__(256) transpose_kernel(int64_t rows, int64_t cols, const T* src, T* dst) {
+  __shared__ T tile[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8 threads
+  for (int64_t bi = blockIdx.y; bi * 32 < rows; bi += gridDim.y) {
+    for (int64_t bj = blockIdx.x; bj * 32 < cols; bj += gridDim.x) {
+      const int64_t r0 = bi * 32, c0 = bj * 32;
+#pragma unroll
+      for (int k = 0; k < 32; k += 8) {
+        const int64_t r = r0 + ty + k, c = c0 + tx;
+        if (r < rows && c < cols) tile[ty + k][tx] = src[r * cols + c];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 32; k += 8) {
+        const int64_t c = c0 + ty + k, r = r0 + tx;
+        if (r < rows && c < cols) dst[c * rows + r] = tile[tx][ty + k];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) isnan_kernel(int64_t n, const T* x, unsigned char* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = x[i] != x[i] ? 1 : 0;
+}
+
+// out[0] = any(x) (mode 0) or all(x) (mode 1) over n bytes; out must be pre-set by the caller to the
+// neutral value (0 for any, 1 for all); every thread that sees the deciding value stores it (idempotent)
+__global__ void __launch_bounds__(kBlock) bool_reduce_kernel(int64_t n, int mode, const unsigned char* x,
+                                                             unsigned char* out) {
+  bool hit = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    hit |= mode == 0 ? (x[i] != 0) : (x[i] == 0);
+  if (hit) out[0] = mode == 0 ? 1 : 0;
+}
+
+inline unsigned gy(int64_t rows) { return (unsigned)(rows < 1 ? 1 : (rows > 65535 ? 65535 : rows)); }
+
+}  // namespace
+}  // namespace pxa
+
+using namespace pxa;
+
+extern "C" {
+
+int pxa_copy2d(int dtype, int64_t rows, int64_t n, const void* src, int64_t lds, void* dst, int64_t ldd, int accumulate,
+               void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && n >= 0 && lds >= 0 && ldd >= n);
+  if (rows == 0 || n == 0) return PXA_OK;
+  PXA_CHECK_ARG(src != nullptr && dst != nullptr);
+  PXA_DISPATCH(dtype, T, {
+    constexpr int V = kVecN<T>;
+    const bool vec = (n % V == 0) && (lds % V == 0) && (ldd % V == 0) && aligned16(src) && aligned16(dst);
+    const int64_t items = vec ? n / V : n;
+    int gx = (int)((items + kBlock - 1) / kBlock);
+    const unsigned gyv = gy(rows);
+    int64_t cap = (kMaxGrid + gyv - 1) / gyv;
+    if (gx > cap) gx = (int)cap;
+    if (gx < 1) gx = 1;
+    if (vec)
+      hipLaunchKernelGGL((copy2d_kernel<T, true>), dim3(gx, gyv), dim3(kBlock), 0, as_stream(stream), rows, n,
+                         (const T*)src, lds, (T*)dst, ldd, accumulate);
+    else
+      hipLaunchKernelGGL((copy2d_kernel<T, false>), dim3(gx, gyv), dim3(kBlock), 0, as_stream(stream), rows, n,
+                         (const T*)src, lds, (T*)dst, ldd, accumulate);
+    return last_launch_status();
+  });
+}
+
+int pxa_unary(int dtype, int op, int64_t n, const void* x, void* out, void* stream) {
+  PXA_CHECK_ARG(n >= 0 && op >= 0 && op <= kReciprocal);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && out != nullptr);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((unary_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, op, (const T*)x,
+                       (T*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_binary(int dtype, int op, int64_t n, const void* x, double xs, const void* y, double ys, void* out,
+               void* stream) {
+  PXA_CHECK_ARG(n >= 0 && op >= 0 && op <= kPow);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(out != nullptr);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((binary_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, op, (const T*)x,
+                       (T)xs, (const T*)y, (T)ys, (T*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_where(int dtype, int64_t n, const void* cond, const void* x, double xs, const void* y, double ys, void* out,
+              void* stream) {
+  PXA_CHECK_ARG(n >= 0);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(cond != nullptr && out != nullptr);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((where_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n,
+                       (const unsigned char*)cond, (const T*)x, (T)xs, (const T*)y, (T)ys, (T*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_cast(int dtype_in, int dtype_out, int64_t n, const void* x, void* out, void* stream) {
+  PXA_CHECK_ARG(n >= 0);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && out != nullptr);
+  PXA_DISPATCH(dtype_in, TI, {
+    PXA_DISPATCH(dtype_out, TO, {
+      hipLaunchKernelGGL((cast_kernel<TI, TO>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, (const TI*)x,
+                         (TO*)out);
+      return last_launch_status();
+    });
+  });
+}
+
+int pxa_set_diag(int dtype, int64_t rows, int64_t ld, int64_t off, double value, void* out, void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && off >= 0 && ld >= 0);
+  if (rows == 0) return PXA_OK;
+  PXA_CHECK_ARG(out != nullptr);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((set_diag_kernel<T>), dim3(grid_for(rows)), dim3(kBlock), 0, as_stream(stream), rows, ld, off,
+                       (T)value, (T*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* dst, void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && cols >= 0);
+  if (rows == 0 || cols == 0) return PXA_OK;
+  PXA_CHECK_ARG(src != nullptr && dst != nullptr && src != dst);
+  PXA_DISPATCH(dtype, T, {
+    const int64_t bx = (cols + 31) / 32, by = (rows + 31) / 32;
+    dim3 grid((unsigned)(bx > 1024 ? 1024 : bx), (unsigned)(by > 1024 ? 1024 : by));
+    hipLaunchKernelGGL((transpose_kernel<T>), grid, dim3(256), 0, as_stream(stream), rows, cols, (const T*)src, (T*)dst);
+    return last_launch_status();
+  });
+}
+
+int pxa_isnan(int dtype, int64_t n, const void* x, void* out, void* stream) {
+  PXA_CHECK_ARG(n >= 0);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && out != nullptr);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((isnan_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, (const T*)x,
+                       (unsigned char*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_bool_reduce(int64_t n, int mode, const void* x, void* out, void* stream) {
+  PXA_CHECK_ARG(n >= 0 && (mode == 0 || mode == 1) && out != nullptr);
+  hipError_t e = hipMemsetAsync(out, mode == 0 ? 0 : 1, 1, as_stream(stream));
+  if (e != hipSuccess) return (int)e;
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr);
+  hipLaunchKernelGGL(bool_reduce_kernel, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, mode,
+                     (const unsigned char*)x, (unsigned char*)out);
+  return last_launch_status();
+}
+
+}  // extern "C"

@@ -40,6 +40,9 @@ struct Vec4<double> {
   using type = double2;  // 16 B per lane for both precisions
 };
 
+// Current value of a pxa_tuning() knob (abi.hip).
+int tuning(int key);
+
 // Elements per 16-byte vector.
 template <typename T>
 constexpr int kVecN = 16 / sizeof(T);

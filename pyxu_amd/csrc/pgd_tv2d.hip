@@ -67,26 +67,16 @@ __device__ inline float tv_weight<float>(float n2, float lam, float mu, float in
   return lam * (r < inv_mu ? r : inv_mu);
 }
 
+// ---- phase 0 of the tile kernel: yk = (x - x_prev) * a + x on the A window, zero outside the image.
+// All K0 vector pairs of a thread are loaded before the first LDS store, so their latencies overlap.
 template <typename T, int R, bool EDGE>
-__device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
-                                const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
-                                T* __restrict__ xns, double* __restrict__ partials) {
+__device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0, const T* __restrict__ xs,
+                                   const T* __restrict__ xps) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
-  constexpr int CW = L::CW;
-  T* A = reinterpret_cast<T*>(smem);
-  T* PT = A + L::AR * L::AP;
-  T* KT = PT + L::AC * L::PTP;  // H taps for runtime-indexed reads (boundary corrections)
   const int n0 = p.n0, n1 = p.n1;
   const int tid = threadIdx.x;
-  if (EDGE && tid < 2 * R + 1) {
-    KT[tid] = p.k0[tid];
-    KT[kKT + tid] = p.k1[tid];
-  }
-
-  // ---- phase 0: yk = (x - x_prev) * a + x on A, zero outside the image.  All K0 vector pairs of a
-  // thread are loaded before the first LDS store, so their latencies overlap (one round trip, not K0).
   constexpr int K0 = cdiv(L::N0, kThreads);
   T xv[K0][V], pv[K0][V];
 #pragma unroll
@@ -127,11 +117,16 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       st_vec<T, V>(A + r * L::AP + V * g, out);
     }
   }
-  __syncthreads();
+}
 
-  // ---- pass A: PT[col][row] = (G0 yk)[row][col] for the TY tile rows and all A columns
+// ---- pass A: PT[col][row] = (G0 yk)[row][col] for the TY tile rows and all A columns
+template <typename T, int R, bool EDGE>
+__device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T* KT, int ty0) {
+  using L = Layout<T, R>;
+  constexpr int V = L::V;
+  const int tid = threadIdx.x;
   constexpr int KA = cdiv(L::NPA, kThreads);
-  const bool edge_rows = EDGE && (ty0 < R || ty0 + TY > n0 - R);
+  const bool edge_rows = EDGE && (ty0 < R || ty0 + TY > p.n0 - R);
 #pragma unroll
   for (int k = 0; k < KA; ++k) {
     const int it = tid + k * kThreads;
@@ -139,7 +134,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       const int a = it % L::NA, b = it / L::NA;  // row group fastest (conflict-free reads/writes)
       T acc[V][V];
       sweep<T, R, V, L::AP>(A + (V * a) * L::AP + V * b, p.g0, acc);
-      if (edge_rows) ghost_fix<T, R, V, L::AP>(ty0 + V * a, n0, ty0 - 2 * R, A + V * b, p.k0, KT, acc);
+      if (edge_rows) ghost_fix<T, R, V, L::AP>(ty0 + V * a, p.n0, ty0 - 2 * R, A + V * b, p.k0, KT, acc);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         T colv[V];
@@ -149,12 +144,23 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       }
     }
   }
-  __syncthreads();
+}
 
-  // ---- pass B: G1 along rows - b + Grad^T q; z = grad * (-tau) + yk; prox; store
+// ---- pass B: G1 along rows - b + Grad^T q; z = grad * (-tau) + yk; prox; store.
+// `bload(k, u, gr, gc, bv)` yields H^T y at row gr, columns gc .. gc + CW - 1 of item k (the tile
+// kernel loads it from global memory here; the persistent kernel hands over registers it prefetched).
+template <typename T, int R, bool EDGE, typename BLoad>
+__device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, const T* KT, int ty0, int tx0,
+                              BLoad&& bload, const T* __restrict__ xs, T* __restrict__ xns, bool want_part,
+                              double& part_d, double& part_x) {
+  using L = Layout<T, R>;
+  constexpr int V = L::V;
+  constexpr int CA = L::CA;
+  constexpr int CW = L::CW;
+  const int n0 = p.n0, n1 = p.n1;
+  const int tid = threadIdx.x;
   constexpr int KB = cdiv(L::NPB, kThreads);
   const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n1 - R);
-  double part_d = 0.0, part_x = 0.0;
 #pragma unroll
   for (int k = 0; k < KB; ++k) {
     const int it = tid + k * kThreads;
@@ -232,13 +238,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       for (int u = 0; u < V; ++u) {
         const int gr = ty0 + V * a + u, gc = tx0 + c0;
         T bv[CW], xo[CW];
-        if (!EDGE) {
-          if constexpr (CW == 2) ld_pair<T>(bs + (unsigned)(gr * n1 + gc), bv);
-          else bv[0] = bs[(unsigned)(gr * n1 + gc)];
-        } else {
-#pragma unroll
-          for (int w = 0; w < CW; ++w) bv[w] = (gr < n0 && gc + w < n1) ? bs[(int64_t)gr * n1 + gc + w] : T(0);
-        }
+        bload(k, u, gr, gc, bv);
 #pragma unroll
         for (int w = 0; w < CW; ++w) {
           T gsum = acc[w][u] - bv[w];  // G yk - H^T y
@@ -254,7 +254,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
           } else {
             xns[off] = xo[0];
           }
-          if (partials) {
+          if (want_part) {
 #pragma unroll
             for (int w = 0; w < CW; ++w) {
               const T xv = xs[off + w];
@@ -268,7 +268,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
           for (int w = 0; w < CW; ++w) {
             if (gc + w < n1) {
               xns[(int64_t)gr * n1 + gc + w] = xo[w];
-              if (partials) {
+              if (want_part) {
                 const T xv = xs[(int64_t)gr * n1 + gc + w];
                 const double dd = (double)xo[w] - (double)xv;
                 part_d += dd * dd;
@@ -280,29 +280,69 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       }
     }
   }
-  if (partials) {
+}
+
+// Workgroup fold of the per-thread RelError partials into partials[2 tile .. 2 tile + 1] (fixed order).
+// `red`: 2 * kThreads / 64 doubles of LDS that no other phase touches between the two barriers.
+template <typename Barrier>
+__device__ inline void fold_partials(double part_d, double part_x, double* red, double* partials, unsigned tile,
+                                     Barrier&& barrier) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      part_d += __shfl_down(part_d, off, 64);
-      part_x += __shfl_down(part_x, off, 64);
+  for (int off = 32; off > 0; off >>= 1) {
+    part_d += __shfl_down(part_d, off, 64);
+    part_x += __shfl_down(part_x, off, 64);
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  barrier();
+  if (lane == 0) {
+    red[w] = part_d;
+    red[kThreads / 64 + w] = part_x;
+  }
+  barrier();
+  if (tid == 0) {
+    double a0 = 0, a1 = 0;
+    for (int k = 0; k < kThreads / 64; ++k) {
+      a0 += red[k];
+      a1 += red[kThreads / 64 + k];
     }
-    double* red = reinterpret_cast<double*>(smem);
-    const int lane = tid & 63, w = tid >> 6;
-    __syncthreads();  // A / PT are free again
-    if (lane == 0) {
-      red[w] = part_d;
-      red[kThreads / 64 + w] = part_x;
+    partials[2 * tile] = a0;
+    partials[2 * tile + 1] = a1;
+  }
+}
+
+template <typename T, int R, bool EDGE>
+__device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
+                                const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
+                                T* __restrict__ xns, double* __restrict__ partials) {
+  using L = Layout<T, R>;
+  constexpr int CW = L::CW;
+  T* A = reinterpret_cast<T*>(smem);
+  T* PT = A + L::AR * L::AP;
+  T* KT = PT + L::AC * L::PTP;  // H taps for runtime-indexed reads (boundary corrections)
+  const int n0 = p.n0, n1 = p.n1;
+  const int tid = threadIdx.x;
+  if (EDGE && tid < 2 * R + 1) {
+    KT[tid] = p.k0[tid];
+    KT[kKT + tid] = p.k1[tid];
+  }
+  load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+  __syncthreads();
+  pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
+  __syncthreads();
+  auto bload = [&](int, int, int gr, int gc, T(&bv)[CW]) {
+    if (!EDGE) {
+      if constexpr (CW == 2) ld_pair<T>(bs + (unsigned)(gr * n1 + gc), bv);
+      else bv[0] = bs[(unsigned)(gr * n1 + gc)];
+    } else {
+#pragma unroll
+      for (int w = 0; w < CW; ++w) bv[w] = (gr < n0 && gc + w < n1) ? bs[(int64_t)gr * n1 + gc + w] : T(0);
     }
-    __syncthreads();
-    if (tid == 0) {
-      double a0 = 0, a1 = 0;
-      for (int k = 0; k < kThreads / 64; ++k) {
-        a0 += red[k];
-        a1 += red[kThreads / 64 + k];
-      }
-      partials[2 * tile] = a0;
-      partials[2 * tile + 1] = a1;
-    }
+  };
+  double part_d = 0.0, part_x = 0.0;
+  pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
+  if (partials) {
+    // A / PT are free again once every thread is past pass B
+    fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
   }
 }
 
@@ -346,6 +386,292 @@ int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void*
   }
   hipLaunchKernelGGL(kern, dim3(p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp, (const T*)b,
                      (T*)xn, partials);
+  return last_launch_status();
+}
+
+// =====================================================================================================
+// Persistent LDS-DMA pipelined form (fp32, n1 % 4 == 0, 16-B aligned arrays): the same per-tile
+// arithmetic (load_window's yk, pass_a, pass_b), with the global->on-chip traffic of tile t+1 in
+// flight while tile t computes.
+//
+// The tile kernel above serialises, per workgroup, window load -> pass A -> pass B (with H^T y loads
+// in its epilogue), and its 2 048 workgroups run as two synchronous rounds of 4 per CU: HBM idles
+// while every CU computes (SQ_WAIT_ANY ~50 % of wave cycles, r02a profiles).  Here 2 workgroups per
+// CU loop over their tiles (XCD-banded order):
+//   top:    own LDS-DMA of x / x_prev windows(t) landed (counted vmcnt) -> barrier
+//           issue H^T y(t) loads into registers (inline asm: counted by hand, see below)
+//           convert raw windows S -> yk in A (the tile kernel's phase-0 arithmetic)   -> barrier
+//           issue LDS-DMA of the x / x_prev windows of tile t+1 into S (global_load_lds_dwordx4)
+//           pass A (A -> PT)                                                         -> barrier
+//           vmcnt(NDW): H^T y(t) registers landed, tile t+1's DMA may stay in flight
+//           pass B (PT, A, H^T y regs -> x_new)
+// hipcc waits vmcnt(0) at the first use of an ordinary global load while an LDS-DMA is in flight
+// (cdna_hip_programming.md §5 "Pipelining across barriers"), which would drain tile t+1's DMA before
+// pass B: the H^T y loads are inline-asm global_load_dwordx2 with a hand-counted wait instead, and
+// barriers are raw s_barrier (a __syncthreads() would also drain the DMA).  Out-of-image window
+// slots DMA from a 16-byte zero page.  Each wave issues exactly NDW DMA instructions per tile (the
+// surplus instruction of the last wave and the tail window re-write slots with identical bytes), so
+// the hand-counted vmcnt values are exact.
+__device__ __attribute__((aligned(16))) float g_zero_page[4];
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+template <int R>
+struct V5 {
+  using L = Layout<float, R>;
+  static constexpr int SV = L::AC / 4;             // 16-B vectors per staged window row (unpadded)
+  static constexpr int SSLOTS = L::AR * SV;        // vectors per staged array
+  static constexpr int NSLOT = 2 * SSLOTS;         // x window then x_prev window
+  static constexpr int NDMA = cdiv(NSLOT, 64);     // wave-instructions per tile
+  static constexpr int NDW = cdiv(NDMA, kThreads / 64);  // per wave
+  static constexpr int A_OFF = NSLOT * 4;          // floats
+  static constexpr int PT_OFF = A_OFF + L::AR * L::AP;
+  static constexpr int KT_OFF = PT_OFF + L::AC * L::PTP;
+  static constexpr int RED_OFF = KT_OFF + 2 * kKT; // 2 * 4 doubles
+  static constexpr size_t BYTES = (size_t)(RED_OFF + 2 * 2 * (kThreads / 64)) * 4;
+  static_assert(NSLOT >= 64, "window smaller than one DMA instruction");
+  static_assert(NDW <= 15, "hand-counted vmcnt must fit the 6-bit counter with the b loads");
+  static_assert((A_OFF % 4) == 0 && (PT_OFF % 4) == 0 && (RED_OFF % 2) == 0, "LDS carve alignment");
+};
+
+__device__ inline void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ inline void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane global addresses into the
+// contiguous 1 KiB at `lds_dst` (wave-uniform, passed in M0).  Written as inline asm so that hipcc
+// does not see an LDS-DMA in flight: it would otherwise wait vmcnt(0) before every LDS access of
+// passes A / B (it cannot tell that they touch other LDS bytes) and drain the prefetch.  All waits
+// for these loads are the hand-counted ones of the persistent loop.
+__device__ inline void dma16(const float* gsrc, float* lds_dst) {
+  const unsigned lds_addr = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((lds_void*)lds_dst));
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
+// this wave's NDW LDS-DMA instructions for the raw x / x_prev windows of the tile at (ty0, tx0)
+template <int R, bool EDGE>
+__device__ inline void issue_windows(float* S, const float* xs, const float* xps, int ty0, int tx0, int n0, int n1) {
+  using P = V5<R>;
+  constexpr int CA = P::L::CA;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int i = 0; i < P::NDW; ++i) {
+    int ins = wave + (kThreads / 64) * i;
+    if (ins > P::NDMA - 1) ins = P::NDMA - 1;  // surplus: repeat the last instruction (same bytes)
+    int base = ins * 64;
+    if (base > P::NSLOT - 64) base = P::NSLOT - 64;  // tail window ends at the last slot
+    const int s = base + lane;
+    const int arr = s >= P::SSLOTS;
+    const int q = s - arr * P::SSLOTS;
+    const int r = q / P::SV, g = q - r * P::SV;
+    const int gr = ty0 - 2 * R + r, gc = tx0 - CA + 4 * g;
+    const float* img = arr ? xps : xs;
+    const float* src;
+    if (!EDGE) {
+      src = img + (unsigned)(gr * n1 + gc);
+    } else {
+      const bool in = gr >= 0 && gr < n0 && gc >= 0 && gc < n1;
+      src = in ? img + (int64_t)gr * n1 + gc : g_zero_page;
+    }
+    dma16(src, S + 4 * base);
+  }
+}
+
+__device__ inline void asm_load_b2(float2& v, const float* ptr) {
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+}
+
+template <int R, bool EDGE>
+__device__ inline void issue_b(float2 (&bq)[4], const float* bs, int ty0, int tx0, int n0, int n1) {
+  using L = Layout<float, R>;
+  int a, cb;
+  L::pass_b_item(threadIdx.x, a, cb);
+  const int gc = tx0 + 2 * cb;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int gr = ty0 + 4 * a + u;
+    const float* ptr;
+    if (!EDGE) ptr = bs + (unsigned)(gr * n1 + gc);
+    else ptr = (gr < n0 && gc < n1) ? bs + (int64_t)gr * n1 + gc : g_zero_page;  // n1 even: gc < n1 => gc+1 < n1
+    asm_load_b2(bq[u], ptr);
+  }
+}
+
+// raw windows -> yk in A (bit-identical to load_window's arithmetic; zero page => yk = 0 outside)
+template <int R>
+__device__ inline void convert_windows(const float* S, float* A, float a) {
+  using P = V5<R>;
+  using L = typename P::L;
+  const float* Sa = static_cast<const float*>(__builtin_assume_aligned(S, 16));
+  float* Aa = static_cast<float*>(__builtin_assume_aligned(A, 16));
+#pragma unroll
+  for (int k = 0; k < cdiv(P::SSLOTS, kThreads); ++k) {
+    const int it = threadIdx.x + k * kThreads;
+    if (it >= P::SSLOTS) break;
+    const int r = it / P::SV, g = it - r * P::SV;
+    float xv[4], pv[4], out[4];
+    ld_vec<float, 4>(Sa + 4 * it, xv);
+    ld_vec<float, 4>(Sa + 4 * (P::SSLOTS + it), pv);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float d = xv[v] - pv[v];
+      d = d * a;
+      out[v] = d + xv[v];
+    }
+    st_vec<float, 4>(Aa + r * L::AP + 4 * g, out);
+  }
+}
+
+struct TileOf {
+  unsigned tile, s;
+  int ty0, tx0;
+};
+
+template <int R>
+__global__ void __launch_bounds__(kThreads, 2) pgd_tv2d_persistent(PgdParams<float> p, const float* __restrict__ x,
+                                                                 const float* __restrict__ xp,
+                                                                 const float* __restrict__ b, float* __restrict__ xn,
+                                                                 double* __restrict__ partials) {
+  using P = V5<R>;
+  using L = typename P::L;
+  extern __shared__ __attribute__((aligned(16))) float smem5[];
+  float* S = smem5;
+  float* A = smem5 + P::A_OFF;
+  float* PT = smem5 + P::PT_OFF;
+  float* KT = smem5 + P::KT_OFF;
+  double* red = reinterpret_cast<double*>(smem5 + P::RED_OFF);
+  const int tid = threadIdx.x;
+  const int n0 = p.n0, n1 = p.n1;
+  const int64_t img = (int64_t)n0 * n1;
+  const unsigned tpi = (unsigned)p.tiles0 * (unsigned)p.tiles1;
+  // XCD-banded tile order: workgroup group g8 = blockIdx % 8 owns a contiguous band of tiles and its
+  // G/8 workgroups sweep that band together (halo re-reads of neighbouring tiles hit the XCD's L2)
+  const unsigned G8 = gridDim.x >> 3, g8 = blockIdx.x & 7u, j = blockIdx.x >> 3;
+  const unsigned q8 = p.ntiles >> 3, r8 = p.ntiles & 7u;
+  const unsigned band_lo = g8 * q8 + (g8 < r8 ? g8 : r8);
+  const unsigned band_hi = band_lo + q8 + (g8 < r8 ? 1u : 0u);
+  auto tile_at = [&](unsigned t) {
+    TileOf o;
+    o.tile = t;
+    o.s = t / tpi;
+    const unsigned tr = t - o.s * tpi;
+    const unsigned trow = tr / (unsigned)p.tiles1;
+    o.ty0 = (int)trow * TY;
+    o.tx0 = (int)(tr - trow * (unsigned)p.tiles1) * TX;
+    return o;
+  };
+  auto interior_at = [&](const TileOf& o) {
+    return o.ty0 - 2 * R >= 0 && o.ty0 + TY + 2 * R <= n0 && o.tx0 - L::CA >= 0 && o.tx0 + TX + L::CA <= n1;
+  };
+  auto issue_tile = [&](const TileOf& o) {
+    const float* xs = x + (int64_t)o.s * img;
+    const float* xps = xp + (int64_t)o.s * img;
+    if (interior_at(o)) issue_windows<R, false>(S, xs, xps, o.ty0, o.tx0, n0, n1);
+    else issue_windows<R, true>(S, xs, xps, o.ty0, o.tx0, n0, n1);
+  };
+  if (tid < 2 * R + 1) {
+    KT[tid] = p.k0[tid];
+    KT[kKT + tid] = p.k1[tid];
+  }
+  unsigned t = band_lo + j;
+  if (t < band_hi) issue_tile(tile_at(t));
+  bool prev_interior = false;  // stores of the previous tile: a known count only for interior tiles
+  const PgdParams<float>* pp = &p;
+  for (; t < band_hi; t += G8) {
+    // re-read the solver constants (taps, lam, tau, ...) from the kernel-argument segment in every
+    // iteration: hoisted out of the loop they would pin ~100 SGPRs and spill to VGPR lanes
+    asm volatile("" : "+s"(pp));
+    const PgdParams<float>& q = *pp;
+    const TileOf o = tile_at(t);
+    const bool interior = interior_at(o);
+    const unsigned tn = t + G8;
+    const bool has_next = tn < band_hi;
+    // 1. this wave's DMA of tile t landed (only the previous tile's 4 x_new stores may stay in flight)
+    if (prev_interior) wait_vm<4>();
+    else wait_vm<0>();
+    lds_barrier();  // every wave's DMA landed; the previous pass B is done with A / PT / red
+    const float* xs = x + (int64_t)o.s * img;
+    const float* bs = b + (int64_t)(o.s % (unsigned)p.y_images) * img;
+    float* xns = xn + (int64_t)o.s * img;
+    // 2. H^T y of this tile into registers (4 x dwordx2 per thread), counted by hand
+    float2 bq[4];
+    if (interior) issue_b<R, false>(bq, bs, o.ty0, o.tx0, n0, n1);
+    else issue_b<R, true>(bq, bs, o.ty0, o.tx0, n0, n1);
+    // 3. raw windows -> yk
+    convert_windows<R>(S, A, q.a);
+    lds_barrier();  // A complete; S free
+    // 4. next tile's windows in flight during passes A and B
+    if (has_next) issue_tile(tile_at(tn));
+    double part_d = 0.0, part_x = 0.0;
+    if (interior) {
+      pass_a<float, R, false>(q, A, PT, KT, o.ty0);
+      lds_barrier();
+      if (has_next) wait_vm<P::NDW>();
+      else wait_vm<0>();
+      asm volatile("" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+      auto bload = [&](int, int u, int, int, float(&bv)[2]) {
+        bv[0] = bq[u].x;
+        bv[1] = bq[u].y;
+      };
+      pass_b<float, R, false>(q, A, PT, KT, o.ty0, o.tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
+    } else {
+      pass_a<float, R, true>(q, A, PT, KT, o.ty0);
+      lds_barrier();
+      if (has_next) wait_vm<P::NDW>();
+      else wait_vm<0>();
+      asm volatile("" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+      auto bload = [&](int, int u, int, int, float(&bv)[2]) {
+        bv[0] = bq[u].x;
+        bv[1] = bq[u].y;
+      };
+      pass_b<float, R, true>(q, A, PT, KT, o.ty0, o.tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
+    }
+    if (partials) fold_partials(part_d, part_x, red, partials, o.tile, [] { lds_barrier(); });
+    prev_interior = interior && partials == nullptr;
+  }
+}
+
+template <int R>
+int launch_pgd_persistent(const PgdParams<float>& p, const void* x, const void* xp, const void* b, void* xn,
+                          double* partials, hipStream_t s) {
+  using P = V5<R>;
+  auto kern = pgd_tv2d_persistent<R>;
+  static int grid_cap = 0;  // resident workgroups on this device (2 per CU by LDS), multiple of 8
+  if (grid_cap == 0) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P::BYTES);
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return PXA_ERR_UNSUPPORTED;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return PXA_ERR_UNSUPPORTED;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kern, kThreads, P::BYTES) != hipSuccess)
+      return PXA_ERR_UNSUPPORTED;
+    if (per < 1) per = 1;
+    if (per > 2) per = 2;
+    grid_cap = cus * per;
+  }
+  int grid = grid_cap;
+  if ((int64_t)grid > (int64_t)p.ntiles) grid = (int)p.ntiles;
+  grid = grid < 8 ? 8 : (grid & ~7);  // the XCD banding needs a multiple of 8 (idle groups just exit)
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), P::BYTES, s, p, (const float*)x, (const float*)xp,
+                     (const float*)b, (float*)xn, partials);
   return last_launch_status();
 }
 
@@ -407,6 +733,22 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new);
   p.tv = lam != 0.0;
   p.prox = prox;
+  if constexpr (sizeof(T) == 4) {
+    // persistent LDS-DMA kernel (opt-in, PXA_TUNE_PGD_KERNEL = 5): 16-B vectors along rows and 32-bit
+  // in-image offsets.  Measured slower than the tile kernel at 2048^2 (50 vs 27 us): see its header.
+    if (p.vec_ok && n0 * n1 <= 0x7fffffff && tuning(PXA_TUNE_PGD_KERNEL) == 5) {
+      switch (R) {
+        case 1: return launch_pgd_persistent<1>(p, x, x_prev, hty, x_new, partials, s);
+        case 2: return launch_pgd_persistent<2>(p, x, x_prev, hty, x_new, partials, s);
+        case 3: return launch_pgd_persistent<3>(p, x, x_prev, hty, x_new, partials, s);
+        case 4: return launch_pgd_persistent<4>(p, x, x_prev, hty, x_new, partials, s);
+        case 5: return launch_pgd_persistent<5>(p, x, x_prev, hty, x_new, partials, s);
+        case 6: return launch_pgd_persistent<6>(p, x, x_prev, hty, x_new, partials, s);
+        case 7: return launch_pgd_persistent<7>(p, x, x_prev, hty, x_new, partials, s);
+        default: return launch_pgd_persistent<8>(p, x, x_prev, hty, x_new, partials, s);
+      }
+    }
+  }
   switch (R) {
     case 1: return launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s);
     case 2: return launch_pgd<T, 2>(p, x, x_prev, hty, x_new, partials, s);

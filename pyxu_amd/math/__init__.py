@@ -12,14 +12,14 @@ def norm(x, ord=None, axis=None, keepdims=False):
         raise NotImplementedError("pyxu_amd.math.norm: last-axis norms only.")
     x2 = x.reshape(-1, x.shape[-1]) if axis is not None else x.reshape(1, -1)
     if ord in (None, 2):
-        r = _dev.row_reduce(_dev.RED_SUMSQ, x2) ** 0.5
+        r = _dev.unary(_dev.UN_SQRT, _dev.row_reduce(_dev.RED_SUMSQ, x2))
     elif ord == 1:
         r = _dev.row_reduce(_dev.RED_ABS, x2)
     elif ord == np.inf:
         r = _dev.row_reduce(_dev.RED_MAXABS, x2)
     else:
         raise NotImplementedError(f"ord={ord}")
-    r = r.to(x.dtype)
+    r = _dev.cast(r, x)
     if axis is None:
         return r.reshape(()) if not keepdims else r.reshape((1,) * x.ndim)
     return r.reshape(*x.shape[:-1], 1) if keepdims else r.reshape(x.shape[:-1])

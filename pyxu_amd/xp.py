@@ -15,8 +15,9 @@ import numpy as np
 from pyxu_amd import _dev
 
 __all__ = [
-    "zeros", "ones", "full", "empty", "zeros_like", "empty_like", "asarray", "array", "arange",
-    "fabs", "abs", "sign", "fmax", "fmin", "clip", "sqrt", "linalg",
+    "zeros", "ones", "full", "empty", "zeros_like", "empty_like", "asarray", "array", "arange", "eye",
+    "fabs", "abs", "sign", "fmax", "fmin", "maximum", "minimum", "clip", "sqrt", "where", "isnan", "any", "all",
+    "concatenate", "stack", "pad", "broadcast_to", "linalg",
 ]
 
 
@@ -78,64 +79,151 @@ def arange(*args, dtype=None):
     return asarray(np.arange(*args, dtype=dtype))
 
 
+def eye(N, M=None, k=0, dtype=None):
+    M = N if M is None else M
+    out = zeros((N, M), dtype=dtype)
+    rows = min(N, M - k) if k >= 0 else min(N + k, M)
+    if rows > 0:
+        _dev.set_diag(out, rows, M + 0, k if k >= 0 else -k * M, 1.0)
+    return out
+
+
 # ------------------------------------------------------------------ arithmetic (HIP kernels)
 def fabs(x):
-    """|x| = x - 2 min(x, 0), from the clip / axpby kernels."""
-    return _dev.axpby(1.0, x, -2.0, _neg_part(x))
+    return _dev.unary(_dev.UN_ABS, x)
 
 
 abs = fabs  # noqa: A001
 
 
-def _neg_part(x):
-    # min(x, 0) = -clip(-x, 0)
-    return _dev.axpby(-1.0, _dev.clip(_dev.axpby(-1.0, x), 0.0))
+def sign(x):
+    """numpy.sign: -1 / 0 / +1 (NaN stays NaN)."""
+    return _dev.unary(_dev.UN_SIGN, x)
 
 
-def fmax(x, y):
-    if np.isscalar(x) and not np.isscalar(y):
-        x, y = y, x
-    if np.isscalar(y):
-        return _dev.clip(x, float(y))
-    raise NotImplementedError("pyxu_amd.xp.fmax: only an array-scalar form has a kernel")
+def sqrt(x, out=None):
+    return _dev.unary(_dev.UN_SQRT, x, out=out)
 
 
-def fmin(x, y):
-    if np.isscalar(x) and not np.isscalar(y):
-        x, y = y, x
-    if np.isscalar(y):  # min(x, c) = -max(-x, -c)
-        return _dev.axpby(-1.0, _dev.clip(_dev.axpby(-1.0, x), -float(y)))
-    raise NotImplementedError("pyxu_amd.xp.fmin: only an array-scalar form has a kernel")
+def _bin(op, x, y, out=None):
+    if np.isscalar(x) and np.isscalar(y):
+        raise TypeError("pyxu_amd.xp: at least one operand must be a device array")
+    return _dev.binary(op, x, y, out=out)
+
+
+def fmax(x, y, out=None):
+    """numpy.fmax (NaN-ignoring), array-array or array-scalar."""
+    return _bin(_dev.BIN_FMAX, x, y, out)
+
+
+def fmin(x, y, out=None):
+    return _bin(_dev.BIN_FMIN, x, y, out)
+
+
+def maximum(x, y, out=None):
+    """numpy.maximum (NaN-propagating)."""
+    return _bin(_dev.BIN_MAXIMUM, x, y, out)
+
+
+def minimum(x, y, out=None):
+    return _bin(_dev.BIN_MINIMUM, x, y, out)
 
 
 def clip(x, a_min, a_max=None):
     return _dev.clip(x, float(a_min) if a_min is not None else -np.inf, None if a_max is None else float(a_max))
 
 
-def sign(x):
-    raise NotImplementedError("pyxu_amd.xp.sign: no standalone kernel (L1Norm.prox fuses sign into pxa_prox_l1)")
+def where(cond, x, y):
+    """numpy.where(cond, x, y) with x / y device arrays of cond's shape or scalars."""
+    like = x if not np.isscalar(x) else (y if not np.isscalar(y) else None)
+    if like is None:
+        raise TypeError("pyxu_amd.xp.where: at least one of x, y must be a device array")
+    return _dev.where(cond, x, y, like=like)
 
 
-def sqrt(x, out=None):
-    raise NotImplementedError("pyxu_amd.xp.sqrt: no standalone kernel (fused into the L21 kernels)")
+def isnan(x):
+    return _dev.isnan(x)
+
+
+def any(x, axis=None):  # noqa: A001
+    if axis is not None:
+        raise NotImplementedError("pyxu_amd.xp.any: axis=None only")
+    return _dev.bool_reduce(x, 0)
+
+
+def all(x, axis=None):  # noqa: A001
+    if axis is not None:
+        raise NotImplementedError("pyxu_amd.xp.all: axis=None only")
+    return _dev.bool_reduce(x, 1)
+
+
+# ------------------------------------------------------------------ joins / shape (HIP copies)
+def concatenate(arrays, axis=0):
+    """numpy.concatenate for device arrays: each part is viewed as (outer, k_i * inner) around `axis`
+    and copied into its column band of the (outer, sum k_i * inner) result (pxa_copy2d)."""
+    arrays = [_dev.require(a) for a in arrays]
+    nd = arrays[0].ndim
+    ax = axis % nd
+    shp = list(arrays[0].shape)
+    outer = int(np.prod(shp[:ax])) if ax > 0 else 1
+    inner = int(np.prod(shp[ax + 1:])) if ax + 1 < nd else 1
+    total = sum(a.shape[ax] for a in arrays)
+    shp[ax] = total
+    out = _dev.empty(tuple(shp), arrays[0])
+    off = 0
+    for a in arrays:
+        assert a.ndim == nd and a.dtype == arrays[0].dtype
+        w = a.shape[ax] * inner
+        _dev.copy2d(a, out, outer, w, w, total * inner, dst_off=off)
+        off += w
+    return out
+
+
+def stack(arrays, axis=0):
+    arrays = [_dev.require(a) for a in arrays]
+    nd = arrays[0].ndim + 1
+    ax = axis % nd
+    return concatenate([a.reshape(*a.shape[:ax], 1, *a.shape[ax:]) for a in arrays], axis=ax)
+
+
+def pad(x, pad_width, mode="constant"):
+    """numpy.pad over every axis of x (modes of operator/linop/pad.py: constant (0), wrap, reflect,
+    symmetric, edge) through pxa_pad."""
+    x = _dev.require(x)
+    if np.isscalar(pad_width):
+        pad_width = [(int(pad_width), int(pad_width))] * x.ndim
+    pad_width = [(int(p), int(p)) if np.isscalar(p) else (int(p[0]), int(p[1])) for p in pad_width]
+    if len(pad_width) == 1 and x.ndim > 1:
+        pad_width = pad_width * x.ndim
+    lo = [p[0] for p in pad_width]
+    hi = [p[1] for p in pad_width]
+    y = _dev.pad(x, 1, tuple(x.shape), lo, hi, [mode] * x.ndim)
+    return y.reshape(*[n + l + h for n, l, h in zip(x.shape, lo, hi)])
+
+
+def broadcast_to(x, shape):
+    """Read-only broadcast VIEW (numpy.broadcast_to semantics: no data is written)."""
+    return x.expand(*shape)
 
 
 # ------------------------------------------------------------------ linalg
 def _norm(x, ord=None, axis=None, keepdims=False):
-    """numpy.linalg.norm for vectors along the last axis (ord in {None, 1, 2, inf})."""
+    """numpy.linalg.norm for vectors along the last axis (any ord >= 0 and inf)."""
     if axis not in (None, -1, x.ndim - 1):
         raise NotImplementedError("pyxu_amd.xp.linalg.norm: only axis=-1 (row norms) has a kernel")
     if axis is None and x.ndim != 1:
         x = x.reshape(-1)
     if ord in (None, 2):
-        v = _dev.row_reduce(_dev.RED_SUMSQ, x).sqrt_()
+        v = _dev.unary(_dev.UN_SQRT, _dev.row_reduce(_dev.RED_SUMSQ, x))
     elif ord == 1:
         v = _dev.row_reduce(_dev.RED_ABS, x)
     elif ord in (np.inf, float("inf")):
         v = _dev.row_reduce(_dev.RED_MAXABS, x)
-    else:
-        raise NotImplementedError(f"pyxu_amd.xp.linalg.norm: ord={ord}")
-    v = v.to(x.dtype)
+    elif ord == 0:
+        v = _dev.row_reduce_pow(0.0, x)
+    else:  # any other p > 0: (sum |x|^p)^(1/p)
+        v = _dev.binary(_dev.BIN_POW, _dev.row_reduce_pow(float(ord), x), 1.0 / float(ord))
+    v = _dev.cast(v, x)
     if keepdims:
         v = v.reshape(*x.shape[:-1], 1)
     elif x.ndim == 1:

@@ -1,0 +1,101 @@
+"""
+The persistent LDS-DMA PGD kernel (pgd_tv2d_persistent, opt-in PXA_TUNE_PGD_KERNEL = 5 for fp32 images
+with n1 % 4 == 0) against the per-tile kernel (pgd_tv2d_kernel, the default): both run the same per-tile
+arithmetic (load_window's yk, pass_a, pass_b in csrc/pgd_tv2d.hip), so x_new and the RelError
+partials must agree BIT FOR BIT on every shape class: interior and edge tiles, fewer tiles than
+resident workgroups, ragged tile grids, stacks with shared and per-image data, every blur radius
+1..8, every prox kind.  The tile kernel itself is pinned to the oracle by test_gpu_parity.py and
+test_gpu_bench_shapes.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs an MI355X", allow_module_level=True)
+
+import pyxu_amd.operator as pxo  # noqa: E402
+import pyxu_amd.opt.solver as pxs  # noqa: E402
+import pyxu_amd.opt.stop as pxst  # noqa: E402
+import pyxu_amd.runtime as pxrt  # noqa: E402
+from pyxu_amd import _dev  # noqa: E402
+from pyxu_amd._lib import lib  # noqa: E402
+from pyxu_amd.util import to_device, to_NUMPY  # noqa: E402
+
+
+def _plan(sh, stack, y_images, sigma, g_kind, lam=0.02, mu=0.01, seed=0):
+    rng = np.random.default_rng(seed)
+    N = int(np.prod(sh))
+    y = rng.standard_normal(y_images * N).astype(np.float32)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        if y_images == 1:
+            H = pxo.Gaussian(arg_shape=sh, sigma=sigma)
+            G = pxo.Gradient(arg_shape=sh)
+            dim = N
+            l21 = pxo.L21Norm(arg_shape=(2, *sh))
+        else:
+            H = pxo.Gaussian(arg_shape=(y_images, *sh), sigma=(0, sigma, sigma))
+            G = pxo.Gradient(arg_shape=(y_images, *sh), directions=(1, 2))
+            dim = y_images * N
+            l21 = pxo.L21Norm(arg_shape=(2, y_images, *sh))
+        f = 0.5 * pxo.SquaredL2Norm(dim=dim).asloss(to_device(y)) * H + lam * l21.moreau_envelope(mu) * G
+        f.diff_lipschitz = 1 + 8 * lam / mu
+        g = {"none": None, "pos": pxo.PositiveOrthant(dim=dim), "l1": 0.01 * pxo.L1Norm(dim=dim)}[g_kind]
+        s = pxs.PGD(f=f, g=g, show_progress=False)
+        rows = stack // y_images
+        x0 = rng.uniform(0, 1, (rows, dim) if rows > 1 else dim).astype(np.float32)
+        s.fit(x0=to_device(x0), stop_crit=pxst.MaxIter(2))
+        assert s._plan is not None
+        return s
+
+
+def _step(s, kernel):
+    p, m = s._plan, s._mstate
+    x, xp = m["x"], m["x_prev"]
+    out = _dev.empty_like(x)
+    nparts = int(lib.pxa_pgd_tv2d_partials_count(p["stack"], p["n0"], p["n1"]))
+    parts = torch.full((2 * nparts,), -1.0, dtype=torch.float64, device=x.device)
+    prev = _dev.tuning(_dev.TUNE_PGD_KERNEL, kernel)
+    try:
+        _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
+                           p["h1"], p["lam"], p["mu"], 0.37, m["tau"], p["prox"], m["tau"] * p["prox_scale"])
+        out2 = _dev.empty_like(x)
+        _dev.pgd_tv2d_step(x, xp, p["hty"], out2, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
+                           p["h1"], p["lam"], p["mu"], 0.37, m["tau"], p["prox"], m["tau"] * p["prox_scale"], partials=parts)
+        torch.cuda.synchronize()
+    finally:
+        _dev.tuning(_dev.TUNE_PGD_KERNEL, prev)
+    return to_NUMPY(out), to_NUMPY(out2), to_NUMPY(parts)
+
+
+CASES = [
+    # (shape, stack, y_images, sigma, g)
+    ((2048, 2048), 1, 1, 2.0, "pos"),   # the bench workload: interior + edge tiles, 4 tiles / workgroup
+    ((96, 128), 1, 1, 2.0, "l1"),       # fewer tiles than workgroups (idle XCD groups)
+    ((1000, 1004), 1, 1, 2.5, "pos"),   # ragged tile grid, R = 8
+    ((300, 260), 1, 1, 0.3, "none"),    # R = 1
+    ((257, 516), 1, 1, 1.0, "l1"),      # R = 3, odd row count
+    ((128, 192), 3, 1, 2.0, "pos"),     # stacked initial points, one y
+    ((64, 320), 4, 4, 1.5, "pos"),      # batch-as-axis: per-image data
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}-sig{c[3]}-{c[4]}")
+def test_persistent_kernel_bit_exact_vs_tile_kernel(case):
+    sh, stack, y_images, sigma, g_kind = case
+    s = _plan(sh, stack, y_images, sigma, g_kind)
+    a, a_p, pa = _step(s, 5)
+    b, b_p, pb = _step(s, 0)
+    assert np.array_equal(a, b)
+    assert np.array_equal(a_p, b_p) and np.array_equal(a, a_p)
+    assert np.array_equal(pa, pb) and np.all(pa >= 0)
+
+
+def test_kernel_knob_round_trips():
+    """The kernel-selection knob round-trips (default 0 = tile kernel)."""
+    assert _dev.tuning(_dev.TUNE_PGD_KERNEL) == 0
+    prev = _dev.tuning(_dev.TUNE_PGD_KERNEL, 5)
+    assert prev == 0 and _dev.tuning(_dev.TUNE_PGD_KERNEL) == 5
+    _dev.tuning(_dev.TUNE_PGD_KERNEL, 0)
