@@ -254,20 +254,24 @@ int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, cons
  * runs outside this library.
  * ------------------------------------------------------------------------------------------- */
 
-/* dst[r*ldd + i] = src[r*lds + i]  (+ dst[r*ldd + i] when accumulate != 0), r < rows, i < n.
+/* dst[r*ldd + i] = src[r*lds + i] (accumulate 0), dst + src (1), or 0 + src (2: the first term of
+ * a Python sum(), which maps -0.0 to +0.0 exactly as the reference's row sums), r < rows, i < n.
  * Block operators (operator/blocks.py:660-679, 838-860: slicing arr[..., off:off+dim], the row sums
  * of hstack.apply / vstack.adjoint, concatenate), lds = 0 broadcasts one row (CG x0 broadcast,
- * opt/solver/cg.py:96-110), diagonal extraction (lds = n + 1). */
-int pxa_copy2d(int dtype, int64_t rows, int64_t n, const void* src, int64_t lds, void* dst, int64_t ldd, int accumulate,
-               void* stream);
+ * opt/solver/cg.py:96-110), diagonal extraction (lds = n + 1).  src_col_stride is 1, or 0 to repeat
+ * src[r*lds] along the row (Sum.adjoint, operator/linop/reduce.py). */
+int pxa_copy2d(int dtype, int64_t rows, int64_t n, const void* src, int64_t lds, int64_t src_col_stride, void* dst,
+               int64_t ldd, int accumulate, void* stream);
 
-/* out = f(x): op 0 sqrt, 1 sign (numpy.sign), 2 fabs, 3 negative, 4 square, 5 reciprocal. */
+/* out = f(x): op 0 sqrt, 1 sign (numpy.sign), 2 fabs, 3 negative, 4 square, 5 reciprocal,
+ * 6 (x > 0 ? +inf : 0) (indicator value from a violation count, func/indicator.py:198-202). */
 #define PXA_UN_SQRT 0
 #define PXA_UN_SIGN 1
 #define PXA_UN_ABS 2
 #define PXA_UN_NEG 3
 #define PXA_UN_SQUARE 4
 #define PXA_UN_RECIP 5
+#define PXA_UN_POSINF 6
 int pxa_unary(int dtype, int op, int64_t n, const void* x, void* out, void* stream);
 
 /* out = f(x, y) with x / y arrays of n elements or NULL for the broadcast scalars xs / ys:

@@ -336,15 +336,17 @@ def group_norm(x, outer, group, inner):
 
 
 # ------------------------------------------------------------------ array primitives (csrc/array.hip)
-UN_SQRT, UN_SIGN, UN_ABS, UN_NEG, UN_SQUARE, UN_RECIP = range(6)
+UN_SQRT, UN_SIGN, UN_ABS, UN_NEG, UN_SQUARE, UN_RECIP, UN_POSINF = range(7)
 BIN_FMAX, BIN_FMIN, BIN_ADD, BIN_SUB, BIN_MUL, BIN_DIV, BIN_MAXIMUM, BIN_MINIMUM, BIN_POW = range(9)
 
 
-def copy2d(src, dst, rows, n, lds, ldd, src_off=0, dst_off=0, accumulate=False):
-    """dst[dst_off + r*ldd + i] (+)= src[src_off + r*lds + i] for r < rows, i < n (element offsets)."""
+def copy2d(src, dst, rows, n, lds, ldd, src_off=0, dst_off=0, accumulate=0, col_stride=1):
+    """dst[dst_off + r*ldd + i] = src[src_off + r*lds + i*col_stride] for r < rows, i < n (element
+    offsets; col_stride 0 repeats one value per row); accumulate 1: dst += src; 2: dst = 0 + src (the
+    first term of a Python sum)."""
     es = src.element_size()
-    check(lib.pxa_copy2d(dtcode(src), int(rows), int(n), ptr(src) + int(src_off) * es, int(lds),
-                         ptr(dst) + int(dst_off) * es, int(ldd), int(bool(accumulate)), stream()), "pxa_copy2d")
+    check(lib.pxa_copy2d(dtcode(src), int(rows), int(n), ptr(src) + int(src_off) * es, int(lds), int(col_stride),
+                         ptr(dst) + int(dst_off) * es, int(ldd), int(accumulate), stream()), "pxa_copy2d")
     return dst
 
 

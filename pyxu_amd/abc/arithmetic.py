@@ -161,8 +161,9 @@ class ScaleRule(Rule):
         return _dev.axpby(self._cst, out, out=out)
 
     def asarray(self, **kwargs):
-        A = self._op.asarray(**kwargs)
-        return A * self._cst
+        xp = kwargs.pop("xp", None)
+        A = _dev.axpby(self._cst, _dev.require(self._op.asarray(**kwargs)))
+        return A.cpu().numpy() if xp is np else A
 
     def svdvals(self, **kwargs):
         return self._op.svdvals(**kwargs) * abs(self._cst)
@@ -252,7 +253,9 @@ class ArgScaleRule(Rule):
         return _dev.axpby(self._cst, out, out=out)
 
     def asarray(self, **kwargs):
-        return self._op.asarray(**kwargs) * self._cst
+        xp = kwargs.pop("xp", None)
+        A = _dev.axpby(self._cst, _dev.require(self._op.asarray(**kwargs)))
+        return A.cpu().numpy() if xp is np else A
 
     def gram(self):
         return self._op.gram() * (self._cst**2)
@@ -501,7 +504,15 @@ class AddRule(Rule):
         return _dev.axpby(1.0, out, 1.0, self._rhs.adjoint(arr_r), out=out)
 
     def asarray(self, **kwargs):
-        return self._lhs.asarray(**kwargs) + self._rhs.asarray(**kwargs)
+        xp = kwargs.pop("xp", None)
+        L = _dev.require(self._lhs.asarray(**kwargs))
+        Rm = _dev.require(self._rhs.asarray(**kwargs))
+        if L.shape != Rm.shape:  # (1, N) + (M, N) range broadcasting (arithmetic.py:843-849)
+            big, small = (L, Rm) if L.numel() >= Rm.numel() else (Rm, L)
+            A = _dev.axpby_bcast(1.0, big, 1.0, small)
+        else:
+            A = _dev.axpby(1.0, L, 1.0, Rm)
+        return A.cpu().numpy() if xp is np else A
 
     def gram(self):
         op = self._lhs.gram() + self._rhs.gram() + (self._lhs.T * self._rhs + self._rhs.T * self._lhs).asop(pxo.SelfAdjointOp)
@@ -642,18 +653,24 @@ class ChainRule(Rule):
         x = self._lhs.grad(self._rhs.apply(arr))
         if arr.ndim == 1 or self._rhs.has(pxo.Property.LINEAR):
             return self._rhs.jacobian(arr).adjoint(x)
-        import torch
-
         a2 = arr.reshape(-1, arr.shape[-1])
         x2 = x.reshape(a2.shape[0], -1)
-        return torch.stack([self._rhs.jacobian(a).adjoint(b) for a, b in zip(a2, x2)], dim=0).reshape(arr.shape)
+        out = _dev.empty(a2.shape, a2)
+        for r, (a, b) in enumerate(zip(a2, x2)):  # per-row Jacobians (non-linear rhs), rows written in place
+            g = _dev.require(self._rhs.jacobian(a).adjoint(b))
+            _dev.copy2d(g, out, 1, g.numel(), g.numel(), g.numel(), dst_off=r * a2.shape[1])
+        return out.reshape(arr.shape)
 
     @pxrt.enforce_precision(i="arr")
     def adjoint(self, arr):
         return self._rhs.adjoint(self._lhs.adjoint(arr))
 
     def asarray(self, **kwargs):
-        return self._lhs.asarray(**kwargs) @ self._rhs.asarray(**kwargs)
+        xp = kwargs.pop("xp", None)
+        L = _dev.require(self._lhs.asarray(**kwargs))
+        Rm = _dev.require(self._rhs.asarray(**kwargs))
+        A = _dev.dense_matmat(Rm, L, 1)  # rows of L times R (pxa_dense_matmat, trans = 1)
+        return A.cpu().numpy() if xp is np else A
 
     def gram(self):
         return (self._rhs.T * self._lhs.gram() * self._rhs).asop(pxo.SelfAdjointOp).squeeze()
@@ -748,7 +765,9 @@ class TransposeRule(Rule):
         return self._op.apply(arr)
 
     def asarray(self, **kwargs):
-        return self._op.asarray(**kwargs).T
+        xp = kwargs.pop("xp", None)
+        A = _dev.transpose(_dev.require(self._op.asarray(**kwargs)))
+        return A.cpu().numpy() if xp is np else A
 
     def gram(self):
         return self._op.cogram()

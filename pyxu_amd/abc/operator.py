@@ -85,12 +85,12 @@ def _rows(arr):
 def _rowsum(arr):
     """sum over the last axis, keepdims, in arr's dtype (device)."""
     s = _dev.row_reduce(_dev.RED_SUM, _rows(arr))
-    return s.to(arr.dtype).reshape(*arr.shape[:-1], 1)
+    return _dev.cast(s, arr).reshape(*arr.shape[:-1], 1)
 
 
 def _dot(a, b):
     s = _dev.row_reduce(_dev.RED_DOT, _rows(a), _rows(b))
-    return s.to(a.dtype).reshape(*a.shape[:-1], 1)
+    return _dev.cast(s, a).reshape(*a.shape[:-1], 1)
 
 
 class Operator:
@@ -385,7 +385,7 @@ class ProxFunc(Func):
             x = self.prox(arr, tau=_._mu)
             out = copy_if_unsafe(self.apply(x))
             d = _dev.axpby(1.0, arr, -1.0, x)
-            n2 = _dev.row_reduce(_dev.RED_SUMSQ, _rows(d)).to(arr.dtype).reshape(*arr.shape[:-1], 1)
+            n2 = _dev.cast(_dev.row_reduce(_dev.RED_SUMSQ, _rows(d)), arr).reshape(*arr.shape[:-1], 1)
             return _dev.axpby(1.0, out, 0.5 / _._mu, n2)
 
         @pxrt.enforce_precision(i="arr")
@@ -533,10 +533,10 @@ class LinOp(DiffMap):
         n_iter = int(kwargs.get("n_iter", 200))
         tol = float(kwargs.get("tol", 1e-6))
         seed = int(kwargs.get("seed", 0))
-        dtype = pxrt.getPrecision().torch
-        g = torch.Generator(device="cpu").manual_seed(seed)
-        x = torch.randn((self.dim,), generator=g, dtype=dtype).to("cuda")
-        x = _dev.div(x, float(torch.linalg.vector_norm(x.cpu())))
+        from pyxu_amd.util import to_device
+
+        x = np.random.default_rng(seed).standard_normal(self.dim).astype(pxrt.getPrecision().value)
+        x = to_device(x / np.linalg.norm(x))  # host start vector (synthetic), uploaded once
         L_prev = 0.0
         with pxrt.EnforcePrecision(False):
             for _ in range(n_iter):
@@ -562,15 +562,16 @@ class LinOp(DiffMap):
 
         dtype = pxrt.getPrecision().value if dtype is None else np.dtype(dtype)
         tdt = pxrt.Width(np.dtype(dtype)).torch
-        cols = []
+        At = torch.empty((self.dim, self.codim), dtype=tdt, device="cuda")  # A^T, built row block by row block
         blk = 4096
         with pxrt.EnforcePrecision(False):
             for j0 in range(0, self.dim, blk):
                 j1 = min(self.dim, j0 + blk)
-                E = torch.zeros((j1 - j0, self.dim), dtype=tdt, device="cuda")
-                E[torch.arange(j1 - j0), torch.arange(j0, j1)] = 1
-                cols.append(self.apply(E))
-        A = torch.cat(cols, dim=0).T.contiguous()
+                E = _dev.fill(torch.empty((j1 - j0, self.dim), dtype=tdt, device="cuda"), 0.0)
+                _dev.set_diag(E, j1 - j0, self.dim, j0, 1.0)  # identity columns j0 .. j1 - 1
+                Y = _dev.require(self.apply(E)).reshape(j1 - j0, self.codim)
+                _dev.copy2d(Y, At, j1 - j0, self.codim, self.codim, self.codim, dst_off=j0 * self.codim)
+        A = _dev.transpose(At)
         if xp is np:
             return A.cpu().numpy()
         return A
@@ -643,8 +644,11 @@ class SquareOp(LinOp):
 
     @pxrt.enforce_precision()
     def trace(self, **kwargs):
-        A = self.asarray()
-        return float(A.diagonal().sum().cpu())
+        A = _dev.require(self.asarray())
+        n = A.shape[0]
+        d = _dev.empty((n,), A)
+        _dev.copy2d(A, d, n, 1, n + 1, 1)  # the diagonal (stride n + 1)
+        return float(_dev.row_reduce(_dev.RED_SUM, d.reshape(1, n)).cpu()[0])
 
 
 class NormalOp(SquareOp):

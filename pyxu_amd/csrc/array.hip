@@ -9,10 +9,10 @@
 namespace pxa {
 namespace {
 
-// dst[r * ldd + i] = src[r * lds + i] (+ dst[r * ldd + i] when acc)     r < rows, i < n
+// dst[r * ldd + i] = src[r * lds + i] (acc 0), dst + src (acc 1), 0 + src (acc 2)     r < rows, i < n
 template <typename T, bool VEC>
-__global__ void __launch_bounds__(kBlock) copy2d_kernel(int64_t rows, int64_t n, const T* src, int64_t lds, T* dst,
-                                                        int64_t ldd, int acc) {
+__global__ void __launch_bounds__(kBlock) copy2d_kernel(int64_t rows, int64_t n, const T* src, int64_t lds, int64_t sci,
+                                                        T* dst, int64_t ldd, int acc) {
   constexpr int V = VEC ? kVecN<T> : 1;
   using VT = typename Vec4<T>::type;
   const int64_t nv = n / V;
@@ -22,7 +22,11 @@ __global__ void __launch_bounds__(kBlock) copy2d_kernel(int64_t rows, int64_t n,
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
       if constexpr (VEC) {
         VT v = reinterpret_cast<const VT*>(s)[i];
-        if (acc) {
+        if (acc == 2) {  // 0 + s: the first term of a Python sum() (turns -0.0 into +0.0, as the reference)
+          T* pv = reinterpret_cast<T*>(&v);
+#pragma unroll
+          for (int k = 0; k < V; ++k) pv[k] = T(0) + pv[k];
+        } else if (acc) {
           const VT o = reinterpret_cast<const VT*>(d)[i];
           T* pv = reinterpret_cast<T*>(&v);
           const T* po = reinterpret_cast<const T*>(&o);
@@ -31,29 +35,32 @@ __global__ void __launch_bounds__(kBlock) copy2d_kernel(int64_t rows, int64_t n,
         }
         reinterpret_cast<VT*>(d)[i] = v;
       } else {
-        d[i] = acc ? d[i] + s[i] : s[i];
+        const T v = s[i * sci];
+        d[i] = acc == 2 ? T(0) + v : (acc ? d[i] + v : v);
       }
     }
   }
 }
 
-enum UnaryOp { kSqrt = 0, kSign = 1, kAbs = 2, kNeg = 3, kSquare = 4, kReciprocal = 5 };
+enum UnaryOp { kSqrt = 0, kSign = 1, kAbs = 2, kNeg = 3, kSquare = 4, kReciprocal = 5, kPosInf = 6 };
 
 template <typename T>
 __device__ inline T unary(int op, T x) {
   switch (op) {
     case kSqrt:
       return sqrt(x);
-    case kSign:  // numpy.sign: -1 / 0 / +1, NaN stays NaN
-      return x > T(0) ? T(1) : (x < T(0) ? T(-1) : x);
+    case kSign:  // numpy.sign: -1 / +0 / +1 (also for -0.0), NaN stays NaN
+      return x > T(0) ? T(1) : (x < T(0) ? T(-1) : (x == T(0) ? T(0) : x));
     case kAbs:
       return fabs(x);
     case kNeg:
       return -x;
     case kSquare:
       return x * x;
-    default:
+    case kReciprocal:
       return T(1) / x;
+    default:  // indicator value of a violated constraint count: +inf if x > 0 else 0
+      return x > T(0) ? T(INFINITY) : T(0);
   }
 }
 
@@ -165,14 +172,16 @@ using namespace pxa;
 
 extern "C" {
 
-int pxa_copy2d(int dtype, int64_t rows, int64_t n, const void* src, int64_t lds, void* dst, int64_t ldd, int accumulate,
-               void* stream) {
-  PXA_CHECK_ARG(rows >= 0 && n >= 0 && lds >= 0 && ldd >= n);
+int pxa_copy2d(int dtype, int64_t rows, int64_t n, const void* src, int64_t lds, int64_t src_col_stride, void* dst,
+               int64_t ldd, int accumulate, void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && n >= 0 && lds >= 0 && ldd >= n && (src_col_stride == 0 || src_col_stride == 1));
+  PXA_CHECK_ARG(accumulate >= 0 && accumulate <= 2);
   if (rows == 0 || n == 0) return PXA_OK;
   PXA_CHECK_ARG(src != nullptr && dst != nullptr);
   PXA_DISPATCH(dtype, T, {
     constexpr int V = kVecN<T>;
-    const bool vec = (n % V == 0) && (lds % V == 0) && (ldd % V == 0) && aligned16(src) && aligned16(dst);
+    const bool vec = src_col_stride == 1 && (n % V == 0) && (lds % V == 0) && (ldd % V == 0) && aligned16(src) &&
+                     aligned16(dst);
     const int64_t items = vec ? n / V : n;
     int gx = (int)((items + kBlock - 1) / kBlock);
     const unsigned gyv = gy(rows);
@@ -181,16 +190,16 @@ int pxa_copy2d(int dtype, int64_t rows, int64_t n, const void* src, int64_t lds,
     if (gx < 1) gx = 1;
     if (vec)
       hipLaunchKernelGGL((copy2d_kernel<T, true>), dim3(gx, gyv), dim3(kBlock), 0, as_stream(stream), rows, n,
-                         (const T*)src, lds, (T*)dst, ldd, accumulate);
+                         (const T*)src, lds, (int64_t)1, (T*)dst, ldd, accumulate);
     else
       hipLaunchKernelGGL((copy2d_kernel<T, false>), dim3(gx, gyv), dim3(kBlock), 0, as_stream(stream), rows, n,
-                         (const T*)src, lds, (T*)dst, ldd, accumulate);
+                         (const T*)src, lds, src_col_stride, (T*)dst, ldd, accumulate);
     return last_launch_status();
   });
 }
 
 int pxa_unary(int dtype, int op, int64_t n, const void* x, void* out, void* stream) {
-  PXA_CHECK_ARG(n >= 0 && op >= 0 && op <= kReciprocal);
+  PXA_CHECK_ARG(n >= 0 && op >= 0 && op <= kPosInf);
   if (n == 0) return PXA_OK;
   PXA_CHECK_ARG(x != nullptr && out != nullptr);
   PXA_DISPATCH(dtype, T, {

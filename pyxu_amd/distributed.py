@@ -123,7 +123,11 @@ def gather_slabs(x_local, n_global, group=None):
         buf = buf.cpu()
     parts = [torch.empty_like(buf) for _ in range(w)]
     _dist().all_gather(parts, buf.contiguous(), group=group)
-    return torch.cat([p[:s] for p, s in zip(parts, sizes)], dim=0).to(dev)
+    if parts[0].is_cuda:  # RCCL: assemble the slabs on the device (pxa_copy2d)
+        from pyxu_amd import xp
+
+        return xp.concatenate([p[:s] for p, s in zip(parts, sizes)], axis=0)
+    return torch.cat([p[:s] for p, s in zip(parts, sizes)], dim=0).to(dev)  # gloo: host staging
 
 
 class _ShardedMixin:
@@ -248,7 +252,11 @@ def halo_pad(x, lo, hi, group=None):
         if hi:
             recvs.append((right, rank + 1))
     _p2p(sends, recvs, group)
-    return torch.cat([left, x, right], dim=1)
+    if x.is_cuda:
+        from pyxu_amd import xp
+
+        return xp.concatenate([left, x.contiguous(), right], axis=1)
+    return torch.cat([left, x, right], dim=1)  # gloo CPU tests
 
 
 def halo_reduce(xp, lo, hi, group=None):

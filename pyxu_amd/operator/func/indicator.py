@@ -18,9 +18,7 @@ class PositiveOrthant(pxa.ProxFunc):
     @pxrt.enforce_precision(i="arr")
     def apply(self, arr):
         neg = _dev.row_reduce(_dev.RED_NEGCNT, arr.reshape(-1, arr.shape[-1]))
-        out = neg.clone()
-        out[neg > 0] = float("inf")
-        return out.to(arr.dtype).reshape(*arr.shape[:-1], 1)
+        return _dev.cast(_dev.unary(_dev.UN_POSINF, neg), arr).reshape(*arr.shape[:-1], 1)
 
     @pxrt.enforce_precision(i=("arr", "tau"))
     def prox(self, arr, tau):

@@ -12,7 +12,7 @@ def _row(arr, op, y=None):
     """(..., N) -> (..., 1) in arr.dtype: device row reduction (double accumulation)."""
     x2 = arr.reshape(-1, arr.shape[-1])
     r = _dev.row_reduce(op, x2, None if y is None else y.reshape(x2.shape))
-    return r.to(arr.dtype).reshape(*arr.shape[:-1], 1)
+    return _dev.cast(r, arr).reshape(*arr.shape[:-1], 1)
 
 
 class _ShiftLossMixin:
@@ -52,8 +52,8 @@ class L2Norm(_ShiftLossMixin, pxa.ProxFunc):
 
     @pxrt.enforce_precision(i="arr")
     def apply(self, arr):
-        r = _dev.row_reduce(_dev.RED_SUMSQ, arr.reshape(-1, arr.shape[-1])) ** 0.5
-        return r.to(arr.dtype).reshape(*arr.shape[:-1], 1)
+        r = _dev.unary(_dev.UN_SQRT, _dev.row_reduce(_dev.RED_SUMSQ, arr.reshape(-1, arr.shape[-1])))
+        return _dev.cast(r, arr).reshape(*arr.shape[:-1], 1)
 
     @pxrt.enforce_precision(i=("arr", "tau"))
     def prox(self, arr, tau):
@@ -153,7 +153,7 @@ class L21Norm(_ShiftLossMixin, pxa.ProxFunc):
             g = int(np.prod([self._arg_shape[a] for a in self._l2_axis]))
             n = _dev.group_norm(x, x.numel() // g, g, 1)
         r = _dev.row_reduce(_dev.RED_SUM, n.reshape(S, -1))
-        return r.to(arr.dtype).reshape(*sh, 1)
+        return _dev.cast(r, arr).reshape(*sh, 1)
 
     @pxrt.enforce_precision(i=("arr", "tau"))
     def prox(self, arr, tau):

@@ -143,11 +143,21 @@ def Sum(arg_shape, axis=None):
 
     @pxrt.enforce_precision(i="arr")
     def op_adjoint(_, arr):
-        return arr.expand(*arr.shape[:-1], _.dim).contiguous()
+        z = _dev.require(arr)
+        rows = z.numel()
+        out = _dev.empty((*z.shape[:-1], _.dim), z)
+        return _dev.copy2d(z, out, rows, _.dim, 1, _.dim, col_stride=0)  # each row's scalar repeated
 
     op = from_source(cls=pxa.LinFunc, shape=(1, dim), embed=dict(_name="Sum"), apply=op_apply, adjoint=op_adjoint)
     op.lipschitz = np.sqrt(dim)
     return op
+
+
+def _like(tdt):
+    """A 1-element device tensor of torch dtype `tdt` (dtype carrier for _dev.cast)."""
+    import torch
+
+    return torch.empty((1,), dtype=tdt, device="cuda")
 
 
 def _ExplicitLinOp(cls, mat, enable_warnings=True):
@@ -167,7 +177,7 @@ def _ExplicitLinOp(cls, mat, enable_warnings=True):
         if m is None:
             if _._mat.dtype != dtype and _._enable_warnings:
                 warnings.warn("Computation may not be performed at the requested precision.")
-            m = _._mat if _._mat.dtype == dtype else _._mat.to(dtype)
+            m = _._mat if _._mat.dtype == dtype else _dev.cast(_._mat, _like(dtype))
             cache[dtype] = m
         return m
 
@@ -187,7 +197,8 @@ def _ExplicitLinOp(cls, mat, enable_warnings=True):
 
     def op_asarray(_, xp=None, dtype=None):
         dtype = pxrt.getPrecision().value if dtype is None else np.dtype(dtype)
-        A = _._mat.to(pxrt.Width(np.dtype(dtype)).torch)
+        tdt = pxrt.Width(np.dtype(dtype)).torch
+        A = _._mat if _._mat.dtype == tdt else _dev.cast(_._mat, _like(tdt))
         return A.cpu().numpy() if xp is np else A
 
     klass = cls

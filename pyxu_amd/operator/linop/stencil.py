@@ -68,9 +68,10 @@ class _StencilSpec:
         if key not in self._dev_taps:
             offs = np.array([t[0] for t in self.taps], dtype=np.int32).reshape(-1, self.kernel.ndim)
             coefs = np.array([t[1] for t in self.taps], dtype=np.float64)
-            self._dev_taps[key] = (
+            npdt = np.float32 if like.dtype == torch.float32 else np.float64
+            self._dev_taps[key] = (  # host -> device uploads (the coefficients cast on the host)
                 torch.from_numpy(offs).to(like.device),
-                torch.from_numpy(coefs).to(device=like.device, dtype=like.dtype),
+                torch.from_numpy(coefs.astype(npdt)).to(like.device),
             )
         return self._dev_taps[key]
 
@@ -162,7 +163,9 @@ class Stencil(pxa.SquareOp):
             return arr
         if self._enable_warnings:
             warnings.warn("Computation may not be performed at the requested precision.", PrecisionWarning)
-        return arr.to(pxrt.Width(self._dtype).torch)
+        import torch
+
+        return _dev.cast(arr, torch.empty((1,), dtype=pxrt.Width(self._dtype).torch, device=arr.device))
 
     # ------------------------------------------------------------------ FFT path (large N-D kernels)
     FFT_MIN_TAPS = 256  # non-separable constant-mode kernels with at least this many taps go through the FFT
@@ -204,7 +207,8 @@ class Stencil(pxa.SquareOp):
                 tgt = tuple(((c[:, None] - idx) % np.array(L)[:, None]))
                 np.add.at(kc, tgt, k.reshape(-1))
                 kc /= float(np.prod(L))  # the unnormalised inverse FFT's 1/prod(L), folded into the spectrum
-                kd = torch.from_numpy(kc.reshape(-1)).to(device=x.device, dtype=x.dtype)
+                npdt = np.float32 if x.dtype == torch.float32 else np.float64
+                kd = torch.from_numpy(kc.reshape(-1).astype(npdt)).to(x.device)  # host-cast upload
                 spec = _dev.fft(_dev.real_to_complex(kd), L, tuple(range(len(L))), 1, inverse=False)
                 plan = dict(L=L, spec=spec)
         if cache is None:

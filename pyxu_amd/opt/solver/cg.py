@@ -57,10 +57,19 @@ class CG(pxa.Solver):
             mst["b"] = b
             mst["x"] = _dev.copy(x0)
         else:
-            import torch
+            # broadcast the single right-hand side or initial point over the other's stack (pxa_copy2d
+            # with a zero source stride)
+            x0 = _dev.require(x0, "x0")
+            big = b if b.numel() >= x0.numel() else x0
+            n = big.shape[-1]
+            rows = big.numel() // n
 
-            bb, xx = torch.broadcast_tensors(b, x0)
-            mst["b"], mst["x"] = bb.contiguous(), xx.contiguous()
+            def bcast(t):
+                if t.numel() == big.numel():
+                    return _dev.copy(t) if t is x0 else t
+                return _dev.copy2d(t, _dev.empty(big.shape, t), rows, n, 0, n)
+
+            mst["b"], mst["x"] = bcast(b), bcast(x0)
         mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(mst["x"]))
         mst["conjugate_dir"] = _dev.copy(mst["residual"])
         self._rr = None  # ||r||^2 of the current residual, carried from the previous step's beta
@@ -106,7 +115,7 @@ class CG(pxa.Solver):
         x, b = self._mstate["x"], self._mstate["b"]
         f = _dev.axpby(0.5, self._A.apply(x), -1.0, b)
         r = _dev.row_reduce(_dev.RED_DOT, f.reshape(-1, f.shape[-1]), x.reshape(-1, x.shape[-1]))
-        return r.to(x.dtype).reshape(*x.shape[:-1], 1)
+        return _dev.cast(r, x).reshape(*x.shape[:-1], 1)
 
     def solution(self):
         data, _ = self.stats()

@@ -106,6 +106,18 @@ def _is_tensor(x) -> bool:
     return type(x).__module__.startswith("torch") and hasattr(x, "data_ptr")
 
 
+def _torch_float_types():
+    import torch
+
+    return (torch.float32, torch.float64)
+
+
+def _carrier(tdt, device):
+    import torch
+
+    return torch.empty((1,), dtype=tdt, device=device)
+
+
 def coerce(x):
     """Cast a scalar / NDArray to the runtime precision (_runtime.py:213-245).
 
@@ -120,7 +132,13 @@ def coerce(x):
         if x.is_complex():
             raise TypeError(f"Cannot coerce {x.dtype} tensor to precision {width.value}.")
         tdt = width.torch
-        return x if x.dtype == tdt else x.to(tdt)
+        if x.dtype == tdt:
+            return x
+        if x.is_cuda and x.dtype in (_torch_float_types()):
+            from pyxu_amd import _dev
+
+            return _dev.cast(x, _carrier(tdt, x.device))  # HIP cast kernel
+        return x.to(tdt)  # host tensors (construction-time data, e.g. a shift vector before upload)
     try:
         dt = x.dtype
     except AttributeError:

@@ -33,7 +33,11 @@ def to_device(x, dtype=None, device=None):
     import torch
 
     if is_device_array(x):
-        return x if dtype is None else x.to(dtype)
+        if dtype is None or x.dtype == dtype:
+            return x
+        from pyxu_amd import _dev
+
+        return _dev.cast(x, torch.empty((1,), dtype=dtype, device=x.device))  # device -> device: HIP cast
     a = np.ascontiguousarray(x)
     t = torch.from_numpy(a)
     if dtype is not None:

@@ -355,6 +355,50 @@ def gen_admm():
         save(f"admm_{w}", A=A, y=y, x0=x0, lam=lam, tau=1.0, **res)
 
 
+def gen_blocks():
+    """vstack / hstack / block_diag / coo_block (operator/blocks.py): apply / adjoint on stacked
+    inputs, prox / grad of functional hstacks, Lipschitz constants of the rule protocol."""
+    rng = np.random.default_rng(20)
+    for w, width in WIDTHS.items():
+        dt = width.value
+        A = rng.standard_normal((5, 7)).astype(dt)
+        B = rng.standard_normal((2, 7)).astype(dt)
+        C = rng.standard_normal((5, 4)).astype(dt)
+        D = rng.standard_normal((3, 6)).astype(dt)
+        out = dict(A=A, B=B, C=C, D=D)
+        with pxrt.Precision(width):
+            oA, oB, oC, oD = (pxa.LinOp.from_array(M) for M in (A, B, C, D))
+            ops = {
+                "vstack": pxo.vstack([oA, oB]),
+                "hstack": pxo.hstack([oA, oC]),
+                "bdiag": pxo.block_diag([oA, oD]),
+                "coo": pxo.coo_block(([oA, oB, oC, oD], ([0, 1, 0, 2], [0, 0, 2, 1])), grid_shape=(3, 3)),
+                "gradid": pxo.vstack([pxo.Gradient(arg_shape=(6, 5)), pxo.IdentityOp(dim=30)]),
+            }
+            for k, op in ops.items():
+                x = rng.standard_normal((2, 3, op.dim)).astype(dt)
+                z = rng.standard_normal((2, 3, op.codim)).astype(dt)
+                out[f"{k}_shape"] = np.array(op.shape)
+                out[f"{k}_x"], out[f"{k}_y"] = x, op.apply(x)
+                out[f"{k}_z"], out[f"{k}_adj"] = z, op.adjoint(z)
+                out[f"{k}_x1"] = x[0, 0]
+                out[f"{k}_y1"] = op.apply(x[0, 0])
+                out[f"{k}_lip"] = float(op.lipschitz)
+                out[f"{k}_cls"] = type(op).__name__
+            F = pxo.hstack([pxo.L1Norm(dim=5), pxo.SquaredL2Norm(dim=7)])
+            Q = pxo.hstack([pxo.SquaredL2Norm(dim=5), 2.0 * pxo.SquaredL2Norm(dim=7)])
+            v = rng.standard_normal((2, 12)).astype(dt)
+            out["func_v"] = v
+            out["func_l1l2_apply"] = F.apply(v)
+            out["func_l1l2_prox"] = F.prox(v, tau=0.7)
+            out["func_l1l2_cls"] = type(F).__name__
+            out["func_q_apply"] = Q.apply(v)
+            out["func_q_grad"] = Q.grad(v)
+            out["func_q_cls"] = type(Q).__name__
+            out["func_q_dl"] = float(Q.diff_lipschitz)
+        save(f"blocks_{w}", **out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # e.g. `make_goldens.py diffops`: regenerate only the named families
         for name in sys.argv[1:]:
@@ -369,3 +413,4 @@ if __name__ == "__main__":
     gen_pgd()
     gen_pds()
     gen_admm()
+    gen_blocks()

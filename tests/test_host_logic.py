@@ -273,3 +273,44 @@ def test_threaded_cpu_baseline_is_the_oracle():
     for th in (1, 4, 9):
         out, _ = pgd_tv_threaded(x0, blur, y, lam, mu, orc.positive_orthant_prox, tau, 4, th)
         assert np.array_equal(out, ref)
+
+
+def test_block_operator_property_inference():
+    """blocks.py:_COOBlock._infer_op / op(): the classes and Lipschitz bounds the reference infers
+    (tests/golden/blocks_*.npz record them from the reference; checked here without a GPU)."""
+    from conftest import load_golden
+
+    g = load_golden("blocks_f32")
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        V = pxo.vstack([pxo.Gradient(arg_shape=(6, 5)), pxo.IdentityOp(dim=30)])
+        assert type(V).__name__ == str(g["gradid_cls"]) and V.shape == tuple(g["gradid_shape"])
+        assert np.isclose(float(V.lipschitz), float(g["gradid_lip"]), rtol=1e-6)
+        F = pxo.hstack([pxo.L1Norm(dim=5), pxo.SquaredL2Norm(dim=7)])
+        assert type(F).__name__ == str(g["func_l1l2_cls"])
+        Q = pxo.hstack([pxo.SquaredL2Norm(dim=5), 2.0 * pxo.SquaredL2Norm(dim=7)])
+        assert type(Q).__name__ == str(g["func_q_cls"])
+        assert np.isclose(float(Q.diff_lipschitz), float(g["func_q_dl"]), rtol=1e-6)
+        B = pxo.block_diag([pxo.IdentityOp(dim=3), pxo.Gradient(arg_shape=(4,))])
+        assert B.shape == (7, 7) and isinstance(B, pxa.SquareOp)
+        assert np.isclose(float(B.lipschitz), 2.0)  # block-diagonal: max of the blocks' constants
+        assert pxo.vstack([pxo.IdentityOp(dim=4)]).shape == (4, 4)  # a single block is returned as is
+        with pytest.raises(AssertionError):
+            pxo.vstack([pxo.IdentityOp(dim=4), pxo.IdentityOp(dim=5)])
+
+
+def test_no_torch_arithmetic_in_the_product_path():
+    """Every array operation of pyxu_amd goes through libpyxu_amd.so: torch is the device-array
+    container only (north_star).  Allowed: allocation / views / host<->device copies, and the host
+    staging of the gloo (CPU) collectives, marked on their lines."""
+    import pathlib
+    import re
+
+    bad = re.compile(r"torch\.(cat|stack|linalg|matmul|mm|bmm|sqrt|exp|log|abs|sum|mean|where|clamp|maximum|minimum)\(|"
+                     r"\.sqrt_\(|\.diagonal\(|broadcast_tensors|\.to\(\s*(torch\.)?(float|double)|\.sum\(\)\.cpu")
+    hits = []
+    for p in pathlib.Path(ROOT, "pyxu_amd").rglob("*.py"):
+        for i, line in enumerate(p.read_text().splitlines(), 1):
+            code = line.split("#")[0]
+            if bad.search(code) and "gloo" not in line and "host" not in line:
+                hits.append(f"{p.relative_to(ROOT)}:{i}: {line.strip()}")
+    assert not hits, "\n".join(hits)
