@@ -399,6 +399,86 @@ def gen_blocks():
         save(f"blocks_{w}", **out)
 
 
+def gen_filters():
+    """DifferenceOfGaussians / Laplace / Sobel / Prewitt / Scharr / StructureTensor / MovingAverage
+    (operator/linop/filter.py) on 2-D and 3-D images: apply on stacked inputs and, for the linear
+    ones, adjoint."""
+    rng = np.random.default_rng(40)
+    for w, width in WIDTHS.items():
+        dt = width.value
+        out = {}
+        with pxrt.Precision(width):
+            for tag, sh in (("2d", (9, 11)), ("3d", (5, 6, 7))):
+                ops = {
+                    "dog": pxo.DifferenceOfGaussians(arg_shape=sh, low_sigma=1.0),
+                    "dog_s": pxo.DoG(arg_shape=sh, low_sigma=0.7, high_sigma=1.3, mode="reflect", sampling=2.0),
+                    "laplace": pxo.Laplace(arg_shape=sh),
+                    "laplace_w": pxo.Laplace(arg_shape=sh, mode="wrap", sampling=2.0),
+                    "sobel0": pxo.Sobel(arg_shape=sh, axis=0),
+                    "sobel": pxo.Sobel(arg_shape=sh),
+                    "prewitt1": pxo.Prewitt(arg_shape=sh, axis=1, mode="edge"),
+                    "prewitt": pxo.Prewitt(arg_shape=sh, mode="symmetric"),
+                    "scharr": pxo.Scharr(arg_shape=sh, sampling=0.5),
+                    "scharr01": pxo.Scharr(arg_shape=sh, axis=(0, 1)),
+                    "st": pxo.StructureTensor(arg_shape=sh),
+                    "st_nos": pxo.StructureTensor(arg_shape=sh, smooth_sigma=0, mode="reflect"),
+                    "mavg": pxo.MovingAverage(arg_shape=sh, size=3, center=None, mode="constant"),
+                }
+                N = int(np.prod(sh))
+                for k, op in ops.items():
+                    key = f"{tag}_{k}"
+                    x = rng.standard_normal((2, N)).astype(dt)
+                    out[f"{key}_x"], out[f"{key}_y"] = x, op.apply(x)
+                    out[f"{key}_cls"] = type(op).__name__
+                    out[f"{key}_shape"] = np.array(op.shape)
+                    if isinstance(op, pxa.LinOp):
+                        z = rng.standard_normal((2, op.codim)).astype(dt)
+                        out[f"{key}_z"], out[f"{key}_adj"] = z, op.adjoint(z)
+            out["shape_2d"], out["shape_3d"] = np.array((9, 11)), np.array((5, 6, 7))
+        save(f"filters_{w}", **out)
+
+
+def gen_aliases():
+    """ChambollePock / LorisVerhoeven / DavisYin / DouglasRachford / ForwardBackward /
+    ProximalPoint (opt/solver/pds.py aliases) trajectories on a small TV deblurring problem."""
+    for w, width in WIDTHS.items():
+        dt = width.value
+        rng = np.random.default_rng(50)
+        dims = (12, 14)
+        N = int(np.prod(dims))
+        H, y = _deblur_problem(width, dims, 1.5, rng)
+        lam = 0.05
+        x0 = rng.uniform(0, 1, N).astype(dt)
+        res = {}
+        with pxrt.Precision(width):
+            f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * H
+            f.diff_lipschitz = 1.0
+            K = pxo.Gradient(arg_shape=dims)
+            h = lam * pxo.L21Norm(arg_shape=(2, *dims))
+            g = pxo.PositiveOrthant(dim=N)
+            l1 = lam * pxo.L1Norm(dim=N)
+            cases = {
+                "cp": lambda: pxsl.CP(g=g, h=h, K=K, show_progress=False),
+                "cp_pd3o": lambda: pxsl.CP(g=g, h=h, K=K, base=pxsl.PD3O, show_progress=False),
+                "lv": lambda: pxsl.LV(f=f, h=h, K=K, show_progress=False),
+                "dy": lambda: pxsl.DY(f=f, g=g, h=l1, show_progress=False),
+                "dr": lambda: pxsl.DR(g=g, h=l1, show_progress=False),
+                "fb": lambda: pxsl.FB(f=f, g=l1, show_progress=False),
+                "pp": lambda: pxsl.PP(g=l1, show_progress=False),
+            }
+            for name, mk in cases.items():
+                for n_it in (1, 10, 50):
+                    slvr = mk()
+                    slvr.fit(x0=x0, stop_crit=pxst.MaxIter(n_it))
+                    data, _ = slvr.stats()
+                    res[f"{name}_x_{n_it}"] = data["x"]
+                    res[f"{name}_cls"] = type(slvr).__name__
+                res[f"{name}_tau"] = float(slvr._mstate["tau"])
+                res[f"{name}_sigma"] = float(slvr._mstate["sigma"])
+                res[f"{name}_rho"] = float(slvr._mstate["rho"])
+        save(f"aliases_{w}", arg_shape=np.array(dims), y=y, x0=x0, lam=lam, sigma=1.5, **res)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # e.g. `make_goldens.py diffops`: regenerate only the named families
         for name in sys.argv[1:]:
@@ -414,3 +494,5 @@ if __name__ == "__main__":
     gen_pds()
     gen_admm()
     gen_blocks()
+    gen_filters()
+    gen_aliases()

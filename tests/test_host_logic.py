@@ -314,3 +314,36 @@ def test_no_torch_arithmetic_in_the_product_path():
             if bad.search(code) and "gloo" not in line and "host" not in line:
                 hits.append(f"{p.relative_to(ROOT)}:{i}: {line.strip()}")
     assert not hits, "\n".join(hits)
+
+
+def test_filter_and_alias_construction_matches_reference_classes():
+    """Host-only: the filters' and alias solvers' classes / shapes equal the reference's (goldens
+    filters_*.npz, aliases_*.npz); the numerics are in tests/test_gpu_filters.py."""
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.opt.solver as pxs
+    import pyxu_amd.runtime as pxrt
+    from conftest import load_golden
+
+    g = load_golden("filters_f64")
+    for tag in ("2d", "3d"):
+        sh = tuple(int(v) for v in g[f"shape_{tag}"])
+        with pxrt.Precision(pxrt.Width.DOUBLE):
+            ops = {
+                "dog": pxo.DoG(arg_shape=sh, low_sigma=1.0),
+                "laplace": pxo.Laplace(arg_shape=sh),
+                "sobel0": pxo.Sobel(arg_shape=sh, axis=0),
+                "sobel": pxo.Sobel(arg_shape=sh),
+                "prewitt1": pxo.Prewitt(arg_shape=sh, axis=1, mode="edge"),
+                "scharr01": pxo.Scharr(arg_shape=sh, axis=(0, 1)),
+                "st": pxo.StructureTensor(arg_shape=sh),
+                "st_nos": pxo.StructureTensor(arg_shape=sh, smooth_sigma=0, mode="reflect"),
+            }
+        for k, op in ops.items():
+            assert type(op).__name__ == str(g[f"{tag}_{k}_cls"]), (tag, k)
+            assert op.shape == tuple(g[f"{tag}_{k}_shape"]), (tag, k)
+    a = load_golden("aliases_f64")
+    N = int(np.prod(a["arg_shape"]))
+    l1 = pxo.L1Norm(dim=N)
+    assert type(pxs.PP(g=l1, show_progress=False)).__name__ == str(a["pp_cls"])
+    assert type(pxs.DR(g=l1, h=l1, show_progress=False)).__name__ == str(a["dr_cls"])
+    assert type(pxs.FB(f=pxo.SquaredL2Norm(dim=N), g=l1, show_progress=False)).__name__ == str(a["fb_cls"])
