@@ -221,6 +221,16 @@ int pxa_pad_adjoint(int dtype, int64_t stack, int ndim, const int64_t* shape, co
 int pxa_trim(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* lo, const int64_t* hi,
              int embed, const void* x, void* y, void* stream);
 
+/* SubSample.apply (select.py:119-141) for any index specifier: y (rows, m) = x[:, idx] with x
+ * (rows, n) and idx_dev (m,) int64 flat positions in [0, n) (the host ravels numpy's indexing). */
+int pxa_gather_cols(int dtype, int64_t rows, int64_t n, const void* x, int64_t m, const int64_t* idx_dev, void* y,
+                    void* stream);
+
+/* SubSample.adjoint (select.py:143-167): out (rows, n) = 0, then out[:, idx] = y (rows, m).  idx
+ * entries must be unique (the host keeps numpy's last-write-wins entry of a repeated position). */
+int pxa_scatter_cols(int dtype, int64_t rows, int64_t m, const void* y, int64_t n, const int64_t* idx_dev, void* out,
+                     void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Gradient (operator/linop/diff.py Gradient :1113-1265 = vstack of 2-tap finite-difference
  * Stencils, blocks.py:660-679, :838-860) in ONE pass over x (apply) or z (adjoint),

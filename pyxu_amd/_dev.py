@@ -627,6 +627,27 @@ def trim(x, stack, big_shape, lo, hi, embed):
     return y
 
 
+def gather_cols(x, idx, out=None):
+    """out[r, j] = x[r, idx[j]] for x (rows, n) and device int64 idx (m,)."""
+    x = require(x)
+    n = x.shape[-1]
+    rows = int(np.prod(x.shape[:-1]))
+    m = idx.numel()
+    out = empty((*x.shape[:-1], m), x) if out is None else out
+    check(lib.pxa_gather_cols(dtcode(x), rows, n, ptr(x), m, ptr(idx), ptr(out), stream()), "pxa_gather_cols")
+    return out
+
+
+def scatter_cols(y, idx, n, out=None):
+    """out (rows, n) = 0 then out[r, idx[j]] = y[r, j] (idx unique)."""
+    y = require(y)
+    m = y.shape[-1]
+    rows = int(np.prod(y.shape[:-1]))
+    out = empty((*y.shape[:-1], n), y) if out is None else out
+    check(lib.pxa_scatter_cols(dtcode(y), rows, m, ptr(y), n, ptr(idx), ptr(out), stream()), "pxa_scatter_cols")
+    return out
+
+
 # ------------------------------------------------------------------ gradient
 def gradient2(x, stack, shape, dirs, o0, c0, o1, c1, adjoint=False):
     D = len(dirs)

@@ -54,6 +54,8 @@ EXPORTS = {
     "pxa_pad": (i32, [i32, i64, i32, P_i64, P_i64, P_i64, P_int, vp, vp, vp]),
     "pxa_pad_adjoint": (i32, [i32, i64, i32, P_i64, P_i64, P_i64, P_int, vp, vp, vp, vp]),
     "pxa_trim": (i32, [i32, i64, i32, P_i64, P_i64, P_i64, i32, vp, vp, vp]),
+    "pxa_gather_cols": (i32, [i32, i64, i64, vp, i64, vp, vp, vp]),
+    "pxa_scatter_cols": (i32, [i32, i64, i64, vp, i64, vp, vp, vp]),
     "pxa_gradient2": (i32, [i32, i64, i32, P_i64, i32, P_int, P_int, P_f64, P_int, P_f64, vp, vp, vp]),
     "pxa_gradient2_adjoint": (i32, [i32, i64, i32, P_i64, i32, P_int, P_int, P_f64, P_int, P_f64, vp, vp, vp]),
     "pxa_dense_workspace_bytes": (sz, [i32, i32, i64, i64, i64]),

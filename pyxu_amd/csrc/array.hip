@@ -163,6 +163,24 @@ __global__ void __launch_bounds__(kBlock) bool_reduce_kernel(int64_t n, int mode
   if (hit) out[0] = mode == 0 ? 1 : 0;
 }
 
+// y[r, j] = x[r, idx[j]]  (SubSample.apply)            r < rows, j < m
+template <typename T>
+__global__ void __launch_bounds__(kBlock) gather_cols_kernel(int64_t rows, int64_t n, const T* x, int64_t m,
+                                                             const int64_t* idx, T* y) {
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y)
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x)
+      y[r * m + j] = x[r * n + idx[j]];
+}
+
+// out[r, idx[j]] = y[r, j] over an out the caller zero-filled (SubSample.adjoint); idx unique
+template <typename T>
+__global__ void __launch_bounds__(kBlock) scatter_cols_kernel(int64_t rows, int64_t m, const T* y, int64_t n,
+                                                              const int64_t* idx, T* out) {
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y)
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x)
+      out[r * n + idx[j]] = y[r * m + j];
+}
+
 inline unsigned gy(int64_t rows) { return (unsigned)(rows < 1 ? 1 : (rows > 65535 ? 65535 : rows)); }
 
 }  // namespace
@@ -289,6 +307,40 @@ int pxa_bool_reduce(int64_t n, int mode, const void* x, void* out, void* stream)
   hipLaunchKernelGGL(bool_reduce_kernel, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), n, mode,
                      (const unsigned char*)x, (unsigned char*)out);
   return last_launch_status();
+}
+
+int pxa_gather_cols(int dtype, int64_t rows, int64_t n, const void* x, int64_t m, const int64_t* idx_dev, void* y,
+                    void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && n >= 0 && m >= 0);
+  if (rows == 0 || m == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && y != nullptr && idx_dev != nullptr && n > 0);
+  PXA_DISPATCH(dtype, T, {
+    const unsigned gyv = gy(rows);
+    int64_t gx = (m + kBlock - 1) / kBlock, cap = (kMaxGrid + gyv - 1) / gyv;
+    gx = gx > cap ? cap : gx;
+    hipLaunchKernelGGL((gather_cols_kernel<T>), dim3((unsigned)gx, gyv), dim3(kBlock), 0, as_stream(stream), rows, n,
+                       (const T*)x, m, idx_dev, (T*)y);
+    return last_launch_status();
+  });
+}
+
+int pxa_scatter_cols(int dtype, int64_t rows, int64_t m, const void* y, int64_t n, const int64_t* idx_dev, void* out,
+                     void* stream) {
+  PXA_CHECK_ARG(rows >= 0 && n >= 0 && m >= 0);
+  if (rows == 0 || n == 0) return PXA_OK;
+  PXA_CHECK_ARG(out != nullptr);
+  PXA_DISPATCH(dtype, T, {
+    hipError_t e = hipMemsetAsync(out, 0, (size_t)(rows * n) * sizeof(T), as_stream(stream));
+    if (e != hipSuccess) return (int)e;
+    if (m == 0) return PXA_OK;
+    PXA_CHECK_ARG(y != nullptr && idx_dev != nullptr);
+    const unsigned gyv = gy(rows);
+    int64_t gx = (m + kBlock - 1) / kBlock, cap = (kMaxGrid + gyv - 1) / gyv;
+    gx = gx > cap ? cap : gx;
+    hipLaunchKernelGGL((scatter_cols_kernel<T>), dim3((unsigned)gx, gyv), dim3(kBlock), 0, as_stream(stream), rows, m,
+                       (const T*)y, n, idx_dev, (T*)out);
+    return last_launch_status();
+  });
 }
 
 }  // extern "C"

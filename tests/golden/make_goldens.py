@@ -479,6 +479,50 @@ def gen_aliases():
         save(f"aliases_{w}", arg_shape=np.array(dims), y=y, x0=x0, lam=lam, sigma=1.5, **res)
 
 
+def gen_padselect():
+    """Pad (every mode, mixed per-axis modes, asymmetric widths) and SubSample / Trim (ints, slices
+    with steps, index lists incl. repeats and negatives, boolean masks, broadcast index pairs)."""
+    rng = np.random.default_rng(60)
+    for w, width in WIDTHS.items():
+        dt = width.value
+        out = {}
+        with pxrt.Precision(width):
+            pads = {
+                "c1": ((7,), 3, "constant"),
+                "w2": ((5, 6), ((2, 1), (0, 3)), "wrap"),
+                "r2": ((5, 6), (2, 3), "reflect"),
+                "s3": ((4, 5, 6), 2, "symmetric"),
+                "e2": ((5, 6), ((3, 0), (1, 4)), "edge"),
+                "mix": ((5, 6, 4), ((1, 2), (3, 3), (0, 2)), ("edge", "wrap", "reflect")),
+            }
+            for k, (sh, pw, mode) in pads.items():
+                op = pxo.Pad(arg_shape=sh, pad_width=pw, mode=mode)
+                x = rng.standard_normal((2, op.dim)).astype(dt)
+                z = rng.standard_normal((2, op.codim)).astype(dt)
+                out[f"pad_{k}_x"], out[f"pad_{k}_y"] = x, op.apply(x)
+                out[f"pad_{k}_z"], out[f"pad_{k}_adj"] = z, op.adjoint(z)
+                out[f"pad_{k}_lip"] = float(op.lipschitz)
+                out[f"pad_{k}_shape"] = np.array(op.shape)
+            sels = {
+                "slice": ((10,), (slice(1, None, 3),)),
+                "cols": ((3, 40), (slice(None), [1, 3, -1])),
+                "mask": ((3, 5, 4), (0, np.r_[True, False, False, True, False])),
+                "rep": ((8, 6), ([2, 5, 2, 7],)),
+                "pairs": ((6, 7), ([0, 2, 5], [1, 1, 6])),
+                "neg": ((9, 8), (slice(None, None, -2), slice(2, 7))),
+                "trim": ((9, 8, 5), None),
+            }
+            for k, (sh, idx) in sels.items():
+                op = pxo.Trim(arg_shape=sh, trim_width=((1, 2), (0, 3), (2, 1))) if idx is None else \
+                    pxo.SubSample(sh, *idx)
+                x = rng.standard_normal((2, op.dim)).astype(dt)
+                z = rng.standard_normal((2, op.codim)).astype(dt)
+                out[f"sel_{k}_x"], out[f"sel_{k}_y"] = x, op.apply(x)
+                out[f"sel_{k}_z"], out[f"sel_{k}_adj"] = z, op.adjoint(z)
+                out[f"sel_{k}_shape"] = np.array(op.shape)
+        save(f"padselect_{w}", **out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # e.g. `make_goldens.py diffops`: regenerate only the named families
         for name in sys.argv[1:]:
@@ -496,3 +540,4 @@ if __name__ == "__main__":
     gen_blocks()
     gen_filters()
     gen_aliases()
+    gen_padselect()

@@ -347,3 +347,32 @@ def test_filter_and_alias_construction_matches_reference_classes():
     assert type(pxs.PP(g=l1, show_progress=False)).__name__ == str(a["pp_cls"])
     assert type(pxs.DR(g=l1, h=l1, show_progress=False)).__name__ == str(a["dr_cls"])
     assert type(pxs.FB(f=pxo.SquaredL2Norm(dim=N), g=l1, show_progress=False)).__name__ == str(a["fb_cls"])
+
+
+def test_pad_subsample_shapes_and_lipschitz_match_reference():
+    """Host-only: Pad / SubSample / Trim shapes and Pad's Lipschitz rule vs padselect goldens, and
+    the SubSample index resolution (numpy semantics) vs a NumPy evaluation of the same selector."""
+    import pyxu_amd.operator as pxo
+    from conftest import load_golden
+
+    g = load_golden("padselect_f64")
+    pads = {"w2": ((5, 6), ((2, 1), (0, 3)), "wrap"), "r2": ((5, 6), (2, 3), "reflect"),
+            "e2": ((5, 6), ((3, 0), (1, 4)), "edge"),
+            "mix": ((5, 6, 4), ((1, 2), (3, 3), (0, 2)), ("edge", "wrap", "reflect"))}
+    for k, (sh, pw, mode) in pads.items():
+        op = pxo.Pad(arg_shape=sh, pad_width=pw, mode=mode)
+        assert op.shape == tuple(g[f"pad_{k}_shape"]) and np.isclose(op.lipschitz, float(g[f"pad_{k}_lip"]))
+    sels = {"rep": ((8, 6), ([2, 5, 2, 7],)), "pairs": ((6, 7), ([0, 2, 5], [1, 1, 6])),
+            "neg": ((9, 8), (slice(None, None, -2), slice(2, 7))),
+            "mask": ((3, 5, 4), (0, np.r_[True, False, False, True, False]))}
+    for k, (sh, idx) in sels.items():
+        op = pxo.SubSample(sh, *idx)
+        assert op.shape == tuple(g[f"sel_{k}_shape"]), k
+        x = g[f"sel_{k}_x"][0]
+        assert np.array_equal(x[op._pos_host], g[f"sel_{k}_y"][0]), k  # resolved positions reproduce apply
+        z = g[f"sel_{k}_z"][0]
+        up = np.zeros(op.dim)
+        up[op._pos_host[op._keep_host]] = z[op._keep_host]
+        assert np.array_equal(up, g[f"sel_{k}_adj"][0]), k  # last-write-wins adjoint
+    with pytest.raises(AssertionError):
+        pxo.Pad(arg_shape=(4,), pad_width=4, mode="reflect")
