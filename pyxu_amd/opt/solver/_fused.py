@@ -8,6 +8,8 @@ parameters from the operator tree (introspection fields ``_op/_cst/_lhs/_rhs`` s
 exactly the reference's embedding convention) and returns None when the tree does not match, in
 which case the solver runs the generic (still all-HIP) rule-by-rule path.
 """
+import warnings
+
 import numpy as np
 
 import pyxu_amd.abc as pxa
@@ -20,6 +22,20 @@ from pyxu_amd.util import is_device_array
 __all__ = ["match_pgd_deblur", "match_pds_deblur"]
 
 MAX_R = 8
+
+
+class FusedPathWarning(UserWarning):
+    """The problem has the fused kernel's structure but a parameter outside its envelope: the solver
+    runs the generic rule-by-rule HIP path (2-3x slower) instead."""
+
+
+def _radius_ok(o):
+    r = max(abs(v) for v in o)
+    if r > MAX_R:
+        warnings.warn(f"blur radius {r} > {MAX_R}: the fused one-launch step is not used; running the generic "
+                      f"per-operator HIP path.", FusedPathWarning, stacklevel=4)
+        return False
+    return True
 
 
 def _unscale(op):
@@ -89,7 +105,7 @@ def _stencil_axes(H, sh):
             o, c = [0], [1.0]
         else:
             o, c = st.axis_taps()
-        if max(abs(v) for v in o) > MAX_R:
+        if not _radius_ok(o):
             return None
         taps.append((list(o), list(c)))
     return taps
@@ -162,7 +178,7 @@ def _all_axis_taps(H, sh):
             taps.append(([0], [1.0]))
             continue
         o, c = st.axis_taps()
-        if max(abs(v) for v in o) > MAX_R:
+        if not _radius_ok(o):
             return None
         taps.append((list(o), list(c)))
     return taps

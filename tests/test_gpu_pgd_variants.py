@@ -25,7 +25,7 @@ from pyxu_amd._lib import lib  # noqa: E402
 from pyxu_amd.util import to_device, to_NUMPY  # noqa: E402
 
 
-def _plan(sh, stack, y_images, sigma, g_kind, lam=0.02, mu=0.01, seed=0):
+def _plan(sh, stack, y_images, sigma, g_kind, lam=0.02, mu=0.01, seed=0, fused=True):
     rng = np.random.default_rng(seed)
     N = int(np.prod(sh))
     y = rng.standard_normal(y_images * N).astype(np.float32)
@@ -47,7 +47,7 @@ def _plan(sh, stack, y_images, sigma, g_kind, lam=0.02, mu=0.01, seed=0):
         rows = stack // y_images
         x0 = rng.uniform(0, 1, (rows, dim) if rows > 1 else dim).astype(np.float32)
         s.fit(x0=to_device(x0), stop_crit=pxst.MaxIter(2))
-        assert s._plan is not None
+        assert (s._plan is not None) == fused
         return s
 
 
@@ -99,3 +99,11 @@ def test_kernel_knob_round_trips():
     prev = _dev.tuning(_dev.TUNE_PGD_KERNEL, 5)
     assert prev == 0 and _dev.tuning(_dev.TUNE_PGD_KERNEL) == 5
     _dev.tuning(_dev.TUNE_PGD_KERNEL, 0)
+
+
+def test_wide_blur_warns_and_runs_generic_path():
+    """A sigma = 3 blur (radius 9 > MAX_R) keeps the generic path, loudly (FusedPathWarning)."""
+    from pyxu_amd.opt.solver._fused import FusedPathWarning
+
+    with pytest.warns(FusedPathWarning):
+        _plan((64, 96), 1, 1, 3.0, "pos", fused=False)
