@@ -72,9 +72,12 @@ def MovingAverage(arg_shape, size, center=None, mode="constant", gpu=True, dtype
     arg_shape = tuple(arg_shape)
     dtype = pxrt.getPrecision().value if dtype is None else dtype
     size = _canon(size, arg_shape)
-    center = [s // 2 for s in size] if center is None else list(center)
-    kernel = [np.ones(int(s), dtype=dtype) / s for s in size]
-    op = Stencil(arg_shape=arg_shape, kernel=kernel, center=center, mode=mode)
+    if center is None:
+        assert all(s % 2 == 1 for s in size), \
+            "Can only infer center for odd `size`s. For even `size`s, please provide the desired `center`s."
+        center = [s // 2 for s in size]
+    kernel = [np.ones(int(s), dtype=dtype) for s in size]  # separable box, scaled once as the reference
+    op = (1 / np.prod(size)) * Stencil(arg_shape=arg_shape, kernel=kernel, center=list(center), mode=mode)
     op._name = "MovingAverage"
     return op
 
