@@ -69,9 +69,13 @@ __device__ inline float tv_weight<float>(float n2, float lam, float mu, float in
 
 // ---- phase 0 of the tile kernel: yk = (x - x_prev) * a + x on the A window, zero outside the image.
 // All K0 vector pairs of a thread are loaded before the first LDS store, so their latencies overlap.
-template <typename T, int R, bool EDGE>
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+template <typename T, int R, bool EDGE, typename Hook = NoHook>
 __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0, const T* __restrict__ xs,
-                                   const T* __restrict__ xps) {
+                                   const T* __restrict__ xps, Hook&& after_issue = Hook()) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
@@ -102,6 +106,7 @@ __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0
       }
     }
   }
+  after_issue();  // more loads whose latency overlaps the window's (issued after it: in-order vmcnt)
 #pragma unroll
   for (int k = 0; k < K0; ++k) {
     const int it = tid + k * kThreads;
@@ -310,12 +315,38 @@ __device__ inline void fold_partials(double part_d, double part_x, double* red, 
   }
 }
 
-template <typename T, int R, bool EDGE>
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt) but not for
+// its global loads, so register prefetches issued before it stay in flight (a __syncthreads() fence
+// would drain them with vmcnt(0)).  The "memory" clobbers keep LDS accesses on their side.
+__device__ inline void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// H^T y at row gr, columns gc .. gc + CW - 1 (zero outside the image on edge tiles)
+template <typename T, int CW, bool EDGE>
+__device__ inline void load_b(const T* __restrict__ bs, int gr, int gc, int n0, int n1, T (&bv)[CW]) {
+  if (!EDGE) {
+    if constexpr (CW == 2) ld_pair<T>(bs + (unsigned)(gr * n1 + gc), bv);
+    else bv[0] = bs[(unsigned)(gr * n1 + gc)];
+  } else {
+#pragma unroll
+    for (int w = 0; w < CW; ++w) bv[w] = (gr < n0 && gc + w < n1) ? bs[(int64_t)gr * n1 + gc + w] : T(0);
+  }
+}
+
+// PREB 1: the H^T y values of the thread's pass-B pixels are loaded into registers right behind the
+// window loads (one global round trip per tile instead of two); PREB 2: they are issued as pass B
+// starts, so that their latency overlaps pass B's TV stencil and G1 sweep.  Both use lds_sync().
+template <typename T, int R, bool EDGE, int PREB>
 __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
                                 const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
                                 T* __restrict__ xns, double* __restrict__ partials) {
   using L = Layout<T, R>;
   constexpr int CW = L::CW;
+  constexpr int V = L::V;
+  constexpr int KB = cdiv(L::NPB, kThreads);
   T* A = reinterpret_cast<T*>(smem);
   T* PT = A + L::AR * L::AP;
   T* KT = PT + L::AC * L::PTP;  // H taps for runtime-indexed reads (boundary corrections)
@@ -325,29 +356,49 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     KT[tid] = p.k0[tid];
     KT[kKT + tid] = p.k1[tid];
   }
-  load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
-  __syncthreads();
-  pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
-  __syncthreads();
-  auto bload = [&](int, int, int gr, int gc, T(&bv)[CW]) {
-    if (!EDGE) {
-      if constexpr (CW == 2) ld_pair<T>(bs + (unsigned)(gr * n1 + gc), bv);
-      else bv[0] = bs[(unsigned)(gr * n1 + gc)];
-    } else {
-#pragma unroll
-      for (int w = 0; w < CW; ++w) bv[w] = (gr < n0 && gc + w < n1) ? bs[(int64_t)gr * n1 + gc + w] : T(0);
-    }
-  };
   double part_d = 0.0, part_x = 0.0;
-  pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
-  if (partials) {
-    // A / PT are free again once every thread is past pass B
-    fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
+  if constexpr (PREB != 0) {
+    T bq[KB][V][CW];
+    auto issue_b = [&] {
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const int it = tid + k * kThreads;
+        int a = 0, cb = 0;
+        if (it < L::NPB) L::pass_b_item(it, a, cb);
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+          if (it < L::NPB) load_b<T, CW, EDGE>(bs, ty0 + V * a + u, tx0 + CW * cb, n0, n1, bq[k][u]);
+        }
+      }
+    };
+    if constexpr (PREB == 1) load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps, issue_b);
+    else load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+    lds_sync();
+    pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
+    lds_sync();
+    if constexpr (PREB == 2) issue_b();
+    auto bload = [&](int k, int u, int, int, T(&bv)[CW]) {
+#pragma unroll
+      for (int w = 0; w < CW; ++w) bv[w] = bq[k][u][w];
+    };
+    pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
+    if (partials) fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { lds_sync(); });
+  } else {
+    load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+    __syncthreads();
+    pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
+    __syncthreads();
+    auto bload = [&](int, int, int gr, int gc, T(&bv)[CW]) { load_b<T, CW, EDGE>(bs, gr, gc, n0, n1, bv); };
+    pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
+    if (partials) {
+      // A / PT are free again once every thread is past pass B
+      fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
+    }
   }
 }
 
-template <typename T, int R>
-__global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
+template <typename T, int R, int PREB, int OCC>
+__global__ void __launch_bounds__(kThreads, OCC) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
                                                             const T* __restrict__ xp, const T* __restrict__ b,
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
@@ -368,17 +419,17 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
   const bool interior = p.vec_ok && img <= 0x7fffffff && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0 &&
                         tx0 - L::CA >= 0 && tx0 + TX + L::CA <= p.n1;
   if (interior)
-    pgd_tile<T, R, false>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
+    pgd_tile<T, R, false, PREB>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
   else
-    pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
+    pgd_tile<T, R, true, PREB>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
 }
 
-template <typename T, int R>
-int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
-               hipStream_t s) {
+template <typename T, int R, int PREB, int OCC = 4>
+int launch_pgd_v(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
+                 hipStream_t s) {
   using L = Layout<T, R>;
   const size_t smem = L::BYTES;
-  auto kern = pgd_tv2d_kernel<T, R>;
+  auto kern = pgd_tv2d_kernel<T, R, PREB, OCC>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -387,6 +438,17 @@ int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void*
   hipLaunchKernelGGL(kern, dim3(p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp, (const T*)b,
                      (T*)xn, partials);
   return last_launch_status();
+}
+
+template <typename T, int R>
+int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
+               hipStream_t s) {
+  const int k = tuning(PXA_TUNE_PGD_KERNEL);
+  if (k == 6) return launch_pgd_v<T, R, 1>(p, x, xp, b, xn, partials, s);
+  if (k == 7) return launch_pgd_v<T, R, 2>(p, x, xp, b, xn, partials, s);
+  if (k == 8) return launch_pgd_v<T, R, 1, 3>(p, x, xp, b, xn, partials, s);
+  if (k == 9) return launch_pgd_v<T, R, 0, 3>(p, x, xp, b, xn, partials, s);
+  return launch_pgd_v<T, R, 0>(p, x, xp, b, xn, partials, s);
 }
 
 // =====================================================================================================

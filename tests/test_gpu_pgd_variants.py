@@ -82,11 +82,14 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("kernel", [5, 6, 7, 8, 9])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}-sig{c[3]}-{c[4]}")
-def test_persistent_kernel_bit_exact_vs_tile_kernel(case):
+def test_kernel_variants_bit_exact_vs_tile_kernel(case, kernel):
+    """5 persistent LDS-DMA kernel; 6 / 7 tile kernel with H^T y prefetched behind the window loads /
+    at the start of pass B; 8 / 9 the prefetching / plain tile kernel at 3 workgroups per CU."""
     sh, stack, y_images, sigma, g_kind = case
     s = _plan(sh, stack, y_images, sigma, g_kind)
-    a, a_p, pa = _step(s, 5)
+    a, a_p, pa = _step(s, kernel)
     b, b_p, pb = _step(s, 0)
     assert np.array_equal(a, b)
     assert np.array_equal(a_p, b_p) and np.array_equal(a, a_p)
