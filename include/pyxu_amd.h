@@ -61,6 +61,8 @@ extern "C" {
 #define PXA_RED_MAXABS 4 /* max |x|            : LInfinityNorm / norm(ord=inf) */
 #define PXA_RED_SUM 5    /* sum x              : Sum / QuadraticFunc.apply (operator.py:1255-1262) */
 #define PXA_RED_NEGCNT 6 /* count(x < 0)       : PositiveOrthant.apply (func/indicator.py:198-202) */
+#define PXA_RED_MIN 7    /* min x (NaN-propagating, numpy.min) : Memorize.info (opt/stop.py:181-196) */
+#define PXA_RED_MAX 8    /* max x (NaN-propagating, numpy.max) : Memorize.info */
 
 /* ---------------------------------------------------------------------------------------------
  * Library information

@@ -13,7 +13,7 @@ from pyxu_amd._lib import check, f64_array, i32_array, i64_array, int_array, lib
 
 __all__ = []  # internal module
 
-RED_SUMSQ, RED_DIFFSQ, RED_DOT, RED_ABS, RED_MAXABS, RED_SUM, RED_NEGCNT = range(7)
+RED_SUMSQ, RED_DIFFSQ, RED_DOT, RED_ABS, RED_MAXABS, RED_SUM, RED_NEGCNT, RED_MIN, RED_MAX = range(9)
 MODES = {"constant": 0, "wrap": 1, "reflect": 2, "symmetric": 3, "edge": 4}
 
 

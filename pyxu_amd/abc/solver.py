@@ -9,6 +9,7 @@ import datetime as dt
 import enum
 import logging
 import operator
+import os
 import pathlib as plib
 import shutil
 import sys
@@ -21,6 +22,19 @@ import pyxu_amd.runtime as pxrt
 from pyxu_amd.util import to_NUMPY
 
 __all__ = ["Mode", "Solver", "StoppingCriterion"]
+
+
+def _on_device(v):
+    return getattr(getattr(v, "device", None), "type", "cpu") != "cpu"
+
+
+def _atomic_savez(path, arrays):
+    """np.savez into a sibling temporary file, then rename over `path`."""
+    path = plib.Path(path)
+    tmp = path.with_name(path.name + ".tmp")
+    with open(tmp, "wb") as f:
+        np.savez(f, **arrays)
+    os.replace(tmp, path)
 
 
 @enum.unique
@@ -182,15 +196,72 @@ class Solver:
         self._astate["active"].clear()
         self._astate["worker"].join()
         self._astate.update(mode=None, active=None, worker=None)
+        self._wb_drain()
         self._cleanup_logger()
 
     def writeback(self):
-        """Checkpoint ``log_var`` + history to ``workdir/data.npz`` (solver.py:562-570)."""
+        """Checkpoint ``log_var`` + history to ``workdir/data.npz`` (solver.py:562-570).  Synchronous:
+        earlier asynchronous checkpoints are drained first, so the file holds this state on return."""
         if self._astate.get("internal"):
             return
+        self._wb_drain()
         data, history = self.stats()
         kwargs = {k: to_NUMPY(v) for (k, v) in dict(history=history, **data).items() if (v is not None)}
-        np.savez(self.datafile, **kwargs)
+        _atomic_savez(self.datafile, kwargs)
+
+    def _writeback_async(self):
+        """Mid-run checkpoint (``writeback_rate``) without stalling the device queue: the ``log_var``
+        arrays are snapshotted on the device (pxa_copy2d into fresh buffers, ordered on the solver's
+        stream before the next m_step) and a writer thread waits for that snapshot's event, copies it
+        to the host and writes ``data.npz`` (checkpoints land in iteration order; the file is replaced
+        atomically, so a reader never sees a partial checkpoint)."""
+        if self._astate.get("internal"):
+            return
+        from pyxu_amd import _dev
+
+        data, history = self.stats()
+        snap, ev = {}, None
+        for k, v in data.items():
+            if v is None:
+                continue
+            if _on_device(v):
+                c = _dev.empty_like(v)
+                n = v.numel()
+                if n:
+                    _dev.copy2d(v.contiguous(), c, 1, n, n, n)
+                snap[k] = c
+            else:
+                snap[k] = np.array(v, copy=True)
+        if any(_on_device(v) for v in snap.values()):
+            import torch
+
+            ev = torch.cuda.Event()
+            ev.record()
+        prev = self._astate.get("wb_thread")
+        ast = self._astate
+
+        def job():
+            if prev is not None:
+                prev.join()
+            try:
+                if ev is not None:
+                    ev.synchronize()
+                kwargs = {k: to_NUMPY(v) for (k, v) in dict(history=history, **snap).items() if (v is not None)}
+                _atomic_savez(self.datafile, kwargs)
+            except Exception as e:  # surfaced by the next synchronous writeback
+                ast["wb_error"] = e
+
+        t = threading.Thread(target=job, name="pyxu_amd-writeback", daemon=True)
+        t.start()
+        ast["wb_thread"] = t
+
+    def _wb_drain(self):
+        t = self._astate.pop("wb_thread", None)
+        if t is not None:
+            t.join()
+        e = self._astate.pop("wb_error", None)
+        if e is not None:
+            raise e
 
     def default_stop_crit(self):
         raise NotImplementedError("No default stopping criterion defined.")
@@ -289,7 +360,7 @@ class Solver:
                 with ast["lock"]:
                     self._record(idx, ast["stop_crit"].info() if _ms else None, dt.datetime.now(),
                                  pxrt.getPrecision().value, _ml and log_on)
-                self.writeback()
+                self._writeback_async()
                 ast["idx"] += 1
                 self.m_step()
                 return True
@@ -316,6 +387,10 @@ class Solver:
                 ast["exception"] = e
                 return False
             print("\n".join([msg, f"More information: {self.logfile}."]), file=sys.stderr)
+            try:  # the "last valid checkpoint" below is on disk once the writer is drained
+                self._wb_drain()
+            except Exception:
+                pass
             if ast["wb_rate"] is not None:
                 _, r = divmod(ast["idx"], ast["wb_rate"])
                 msg = "\n".join([msg, f"Last valid checkpoint done at iteration={ast['idx'] - r}."])

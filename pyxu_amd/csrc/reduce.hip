@@ -31,12 +31,23 @@ __device__ inline double elem(T x, T y) {
   if (OP == PXA_RED_MAXABS) return fabs((double)x);
   if (OP == PXA_RED_SUM) return (double)x;
   if (OP == PXA_RED_NEGCNT) return x < T(0) ? 1.0 : 0.0;
+  if (OP == PXA_RED_MIN || OP == PXA_RED_MAX) return (double)x;
+  return 0.0;
+}
+
+// identity of the fold (also the value of lanes / threads without elements)
+template <int OP>
+__device__ inline double ident() {
+  if (OP == PXA_RED_MIN) return INFINITY;
+  if (OP == PXA_RED_MAX) return -INFINITY;
   return 0.0;
 }
 
 template <int OP>
 __device__ inline double combine(double a, double b) {
   if (OP == PXA_RED_MAXABS) return a > b ? a : b;
+  if (OP == PXA_RED_MIN) return (a < b || a != a) ? a : b;  // NaN in either operand wins
+  if (OP == PXA_RED_MAX) return (a > b || a != a) ? a : b;
   return a + b;
 }
 
@@ -56,7 +67,7 @@ __global__ void __launch_bounds__(kBlock) row_partial_kernel(int64_t n, int nb, 
   int64_t chunk = (n + nb - 1) / nb;
   int64_t lo = (int64_t)blockIdx.x * chunk;
   int64_t hi = lo + chunk < n ? lo + chunk : n;
-  double acc = 0.0;
+  double acc = ident<OP>();
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc = combine<OP>(acc, elem<T, OP>(xr[i], yr ? yr[i] : T(0)));
   acc = wave_reduce<OP>(acc);
   __shared__ double sw[kBlock / kWave];
@@ -77,7 +88,7 @@ __global__ void __launch_bounds__(kBlock) row_final_kernel(int64_t rows, int nb,
   const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wavefront per row
   if (r >= rows) return;
   const double* pr = part + r * nb;
-  double acc = lane < nb ? pr[lane] : 0.0;
+  double acc = lane < nb ? pr[lane] : ident<OP>();
   for (int k = lane + 64; k < nb; k += 64) acc = combine<OP>(acc, pr[k]);
   acc = wave_reduce<OP>(acc);
   if (lane == 0) out[r] = acc;
@@ -238,6 +249,8 @@ int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, co
     PXA_RED_CASE(PXA_RED_MAXABS)
     PXA_RED_CASE(PXA_RED_SUM)
     PXA_RED_CASE(PXA_RED_NEGCNT)
+    PXA_RED_CASE(PXA_RED_MIN)
+    PXA_RED_CASE(PXA_RED_MAX)
     default:
       return PXA_ERR_ARG;
   }

@@ -114,26 +114,59 @@ class MaxDuration(pxa.StoppingCriterion):
 
 
 class Memorize(pxa.StoppingCriterion):
+    """Record min / max of a state variable (stop.py:181-210) without stalling the solver loop.
+
+    For a device variable, stop() reduces it on the device (pxa_row_reduce MIN / MAX) and starts an
+    asynchronous copy of the two doubles into pinned host memory; info() waits only for that copy
+    (an event recorded before the solver enqueues its next m_step), so the host never blocks the
+    device queue to log an objective value."""
+
     def __init__(self, var):
         self._var = var
         self._val = np.r_[0]
+        self._pending = None  # (event, pinned (2,) float64, size)
 
     def stop(self, state) -> bool:
         x = state[self._var]
         if isinstance(x, numbers.Real):
             x = np.r_[x]
+        if hasattr(x, "device") and getattr(x.device, "type", "cpu") != "cpu":
+            import torch
+
+            assert x.ndim == 1
+            flat = x.reshape(1, -1)
+            mm = torch.empty((2,), dtype=torch.float64, device=x.device)
+            _dev.row_reduce(_dev.RED_MIN, flat, out=mm[0:1])
+            _dev.row_reduce(_dev.RED_MAX, flat, out=mm[1:2])
+            host = torch.empty((2,), dtype=torch.float64, pin_memory=True)
+            host.copy_(mm, non_blocking=True)  # D2H into pinned memory (ordered on the stream)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending = (ev, host, x.numel(), mm)
+            return False
         x = x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
         assert x.ndim == 1
+        self._pending = None
         self._val = x
         return False
 
+    def _resolve(self):
+        if self._pending is not None:
+            ev, host, size, _ = self._pending
+            ev.synchronize()
+            mn, mx = float(host[0]), float(host[1])
+            self._val = np.r_[mx] if size == 1 else np.r_[mn, mx]
+            self._pending = None
+
     def info(self):
+        self._resolve()
         if self._val.size == 1:
             return {f"Memorize[{self._var}]": float(self._val.max())}
         return {f"Memorize[{self._var}]_min": float(self._val.min()), f"Memorize[{self._var}]_max": float(self._val.max())}
 
     def clear(self):
         self._val = np.r_[0]
+        self._pending = None
 
 
 class AbsError(pxa.StoppingCriterion):

@@ -376,3 +376,78 @@ def test_pad_subsample_shapes_and_lipschitz_match_reference():
         assert np.array_equal(up, g[f"sel_{k}_adj"][0]), k  # last-write-wins adjoint
     with pytest.raises(AssertionError):
         pxo.Pad(arg_shape=(4,), pad_width=4, mode="reflect")
+
+
+class _ToySolver:
+    """Host-only solver over numpy state: x_{k+1} = x_k / 2 (exercises the engine, not the math)."""
+
+    @staticmethod
+    def make(**kw):
+        import pyxu_amd.abc as pxa
+
+        class Toy(pxa.Solver):
+            def m_init(self, x0, fail_at=None):
+                self._mstate["x"] = np.asarray(x0, dtype=np.float64)
+                self._mstate["k"] = 0
+                self._fail_at = fail_at
+
+            def m_step(self):
+                self._mstate["k"] += 1
+                if self._fail_at is not None and self._mstate["k"] == self._fail_at:
+                    raise RuntimeError("boom")
+                self._mstate["x"] = self._mstate["x"] / 2
+
+            def default_stop_crit(self):
+                import pyxu_amd.opt.stop as pxst
+
+                return pxst.MaxIter(5)
+
+            def objective_func(self):
+                return np.r_[float(np.sum(self._mstate["x"]))]
+
+            def solution(self):
+                return self._mstate["x"]
+
+        return Toy(log_var="x", show_progress=False, **kw)
+
+
+def test_writeback_checkpoints_and_history_semantics(tmp_path):
+    """stop_rate / writeback_rate / verbosity bookkeeping of abc/solver.py (reference solver.py:588-663):
+    asynchronous mid-run checkpoints land in order and the final data.npz holds the final state;
+    history has one record per stop check; track_objective adds Memorize columns."""
+    import pyxu_amd.opt.stop as pxst
+
+    s = _ToySolver.make(folder=tmp_path / "a", stop_rate=2, writeback_rate=4)
+    s.fit(x0=np.ones(3) * 64, stop_crit=pxst.MaxIter(9), track_objective=True)
+    d = np.load(s.datafile)
+    # MaxIter counts stop checks (reference stop.py MaxIter): the 10th check, at idx 18, stops
+    assert np.array_equal(d["x"], np.ones(3) * 64 / 2**18)
+    h = d["history"]
+    assert list(h["iteration"]) == list(range(0, 19, 2))
+    assert "Memorize[objective_func]" in h.dtype.names
+    assert np.allclose(h["Memorize[objective_func]"], [3 * 64 / 2**i for i in range(0, 19, 2)])
+    assert not (s.workdir / "data.npz.tmp").exists()
+
+    # MANUAL mode: a checkpoint at idx 4 holds the pre-step state x_4
+    s2 = _ToySolver.make(folder=tmp_path / "b", stop_rate=1, writeback_rate=4)
+    s2.fit(x0=np.ones(2) * 16, stop_crit=pxst.MaxIter(100), mode=__import__("pyxu_amd.abc", fromlist=["Mode"]).Mode.MANUAL)
+    for _ in s2.steps(5):
+        pass
+    s2._wb_drain()
+    assert np.array_equal(np.load(s2.datafile)["x"], np.ones(2) * 16 / 2**4)
+
+
+def test_writeback_bad_rates_and_failure_keeps_last_checkpoint(tmp_path, capsys):
+    import pyxu_amd.opt.stop as pxst
+
+    with pytest.raises(ValueError):
+        _ToySolver.make(folder=tmp_path / "c", stop_rate=3, writeback_rate=4)
+    with pytest.raises(ValueError):
+        _ToySolver.make(folder=tmp_path / "d", stop_rate=2, verbosity=3)
+    s = _ToySolver.make(folder=tmp_path / "e", stop_rate=1, writeback_rate=2)
+    s.fit(x0=np.ones(2) * 8, stop_crit=pxst.MaxIter(50), fail_at=5)
+    err = capsys.readouterr().err
+    assert "Something went wrong" in err
+    log = s.logfile.read_text()
+    assert "Last valid checkpoint done at iteration=4" in log
+    assert np.array_equal(np.load(s.datafile)["x"], np.ones(2) * 8 / 2**4)
