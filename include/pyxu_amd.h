@@ -48,9 +48,8 @@ extern "C" {
 #define PXA_MODE_EDGE 4
 
 /* Kernel-selection knobs (pxa_tuning). */
-#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 auto (= 4, the tile kernel), 5 persistent LDS-DMA kernel (fp32),
-                                 6 / 7 tile kernel with H^T y prefetched behind the window / at pass B,
-                                 8 / 9 prefetching / plain tile kernel at 3 workgroups per CU */
+#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 auto (the tile kernel, staged row-major epilogue),
+                                 4 tile kernel with the item-order epilogue, 5 persistent LDS-DMA kernel (fp32) */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */

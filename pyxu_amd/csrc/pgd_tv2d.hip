@@ -151,13 +151,69 @@ __device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T*
   }
 }
 
-// ---- pass B: G1 along rows - b + Grad^T q; z = grad * (-tau) + yk; prox; store.
-// `bload(k, u, gr, gc, bv)` yields H^T y at row gr, columns gc .. gc + CW - 1 of item k (the tile
-// kernel loads it from global memory here; the persistent kernel hands over registers it prefetched).
-template <typename T, int R, bool EDGE, typename BLoad>
+// ---- epilogue of CW pixels of one row: z = ((G yk + Grad^T q) - b) * (-tau) + yk; prox; store;
+// RelError partials sum (x_new - x)^2, sum x^2 in double.
+template <typename T, int CW, bool EDGE>
+__device__ inline void finish_run(const PgdParams<T>& p, int gr, int gc, const T (&g)[CW], const T (&bv)[CW],
+                                  const T (&yc)[CW], const T* __restrict__ xs, T* __restrict__ xns, bool want_part,
+                                  double& part_d, double& part_x) {
+  const int n0 = p.n0, n1 = p.n1;
+  T xo[CW];
+#pragma unroll
+  for (int w = 0; w < CW; ++w) {
+    T gsum = g[w] - bv[w];  // (G yk + Grad^T q) - H^T y
+    T z = gsum * (-p.tau);
+    z = z + yc[w];
+    xo[w] = apply_prox<T>(p.prox, z, p.pw);
+  }
+  if (!EDGE) {
+    const unsigned off = (unsigned)(gr * n1 + gc);
+    if constexpr (CW == 4) {
+      *reinterpret_cast<float4*>(xns + off) = make_float4(xo[0], xo[1], xo[2], xo[3]);
+    } else if constexpr (CW == 2 && sizeof(T) == 4) {
+      *reinterpret_cast<float2*>(xns + off) = make_float2(xo[0], xo[1]);
+    } else if constexpr (CW == 2) {
+      st_vec<T, 2>(xns + off, xo);
+    } else {
+      xns[off] = xo[0];
+    }
+    if (want_part) {
+      T xv[CW];
+      if constexpr (CW * sizeof(T) == 16) ld_vec<T, CW>(xs + off, xv);
+      else {
+#pragma unroll
+        for (int w = 0; w < CW; ++w) xv[w] = xs[off + w];
+      }
+#pragma unroll
+      for (int w = 0; w < CW; ++w) {
+        const double dd = (double)xo[w] - (double)xv[w];
+        part_d += dd * dd;
+        part_x += (double)xv[w] * (double)xv[w];
+      }
+    }
+  } else if (gr < n0) {
+#pragma unroll
+    for (int w = 0; w < CW; ++w) {
+      if (gc + w < n1) {
+        xns[(int64_t)gr * n1 + gc + w] = xo[w];
+        if (want_part) {
+          const T xv = xs[(int64_t)gr * n1 + gc + w];
+          const double dd = (double)xo[w] - (double)xv;
+          part_d += dd * dd;
+          part_x += (double)xv * (double)xv;
+        }
+      }
+    }
+  }
+}
+
+// ---- pass B: G1 along rows + Grad^T q, handed per output row-run to
+// `emit(k, u, gr, gc, g, yc)`: g = (G yk + Grad^T q) at row gr, columns gc .. gc + CW - 1 of item k,
+// yc = yk there.  The emitter finishes the pixels in place (finish_run) or stages g for the
+// coalesced epilogue (epilogue_staged).
+template <typename T, int R, bool EDGE, typename Emit>
 __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, const T* KT, int ty0, int tx0,
-                              BLoad&& bload, const T* __restrict__ xs, T* __restrict__ xns, bool want_part,
-                              double& part_d, double& part_x) {
+                              Emit&& emit) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
@@ -241,49 +297,61 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
       if (edge_cols) ghost_fix<T, R, CW, L::PTP>(tx0 + c0, n1, tx0 - CA, PT + V * a, p.k1, KT + kKT, acc);
 #pragma unroll
       for (int u = 0; u < V; ++u) {
-        const int gr = ty0 + V * a + u, gc = tx0 + c0;
-        T bv[CW], xo[CW];
-        bload(k, u, gr, gc, bv);
+        T g[CW], y[CW];
 #pragma unroll
         for (int w = 0; w < CW; ++w) {
-          T gsum = acc[w][u] - bv[w];  // G yk - H^T y
-          if (p.tv) gsum = gsum + tv[u][w];
-          T z = gsum * (-p.tau);
-          z = z + yc[u][w];
-          xo[w] = apply_prox<T>(p.prox, z, p.pw);
+          g[w] = p.tv ? acc[w][u] + tv[u][w] : acc[w][u];
+          y[w] = yc[u][w];
         }
-        if (!EDGE) {
-          const unsigned off = (unsigned)(gr * n1 + gc);
-          if constexpr (CW == 2) {
-            *reinterpret_cast<float2*>(xns + off) = make_float2(xo[0], xo[1]);
-          } else {
-            xns[off] = xo[0];
-          }
-          if (want_part) {
-#pragma unroll
-            for (int w = 0; w < CW; ++w) {
-              const T xv = xs[off + w];
-              const double dd = (double)xo[w] - (double)xv;
-              part_d += dd * dd;
-              part_x += (double)xv * (double)xv;
-            }
-          }
-        } else if (gr < n0) {
-#pragma unroll
-          for (int w = 0; w < CW; ++w) {
-            if (gc + w < n1) {
-              xns[(int64_t)gr * n1 + gc + w] = xo[w];
-              if (want_part) {
-                const T xv = xs[(int64_t)gr * n1 + gc + w];
-                const double dd = (double)xo[w] - (double)xv;
-                part_d += dd * dd;
-                part_x += (double)xv * (double)xv;
-              }
-            }
-          }
-        }
+        emit(k, u, ty0 + V * a + u, tx0 + c0, g, y);
       }
     }
+  }
+}
+
+// ---- staged epilogue: every thread parks g = G yk + Grad^T q of its pass-B pixels in O (the PT
+// region, free once all G1 sweeps are done), then the workgroup finishes the tile in row-major order:
+// each 16-B vector of a row is one lane (16 lanes per fp32 row), so H^T y / x loads and x_new stores
+// are full 128-B lines instead of the pass-B item order's 64-B row pieces (measured on MI355X: a
+// 2048^2 fp32 store in the item order 7.2 us, row-major 5.2 us).  yk comes from A.
+template <typename T, int R>
+struct Stage {
+  using L = Layout<T, R>;
+  static constexpr int V = L::V;
+  static constexpr int OP = sizeof(T) == 4 ? TX + 4 : TX + 2;  // conflict-free item-order writes (fp32)
+  static constexpr int LPR = TX / V;                           // lanes per tile row
+  static constexpr int RPS = kThreads / LPR;                   // rows per sweep
+  static_assert(TY * OP <= L::AC * L::PTP, "O must fit in the PT region");
+};
+
+template <typename T, int R, bool EDGE>
+__device__ inline void epilogue_staged(const PgdParams<T>& p, const T* A, const T* O, int ty0, int tx0,
+                                       const T* __restrict__ bs, const T* __restrict__ xs, T* __restrict__ xns,
+                                       bool want_part, double& part_d, double& part_x) {
+  using L = Layout<T, R>;
+  using S = Stage<T, R>;
+  constexpr int V = L::V;
+  const int n0 = p.n0, n1 = p.n1;
+  const int cq = threadIdx.x % S::LPR, r0 = threadIdx.x / S::LPR;
+  constexpr int NS = TY / S::RPS;
+  T bv[NS][V];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {  // all H^T y loads first: one round trip
+    const int gr = ty0 + r0 + s * S::RPS, gc = tx0 + V * cq;
+    if (!EDGE) {
+      ld_vec<T, V>(bs + (unsigned)(gr * n1 + gc), bv[s]);
+    } else {
+#pragma unroll
+      for (int v = 0; v < V; ++v) bv[s][v] = (gr < n0 && gc + v < n1) ? bs[(int64_t)gr * n1 + gc + v] : T(0);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int r = r0 + s * S::RPS;
+    T g[V], y[V];
+    ld_vec<T, V>(O + r * S::OP + V * cq, g);
+    ld_vec<T, V>(A + (r + 2 * R) * L::AP + L::CA + V * cq, y);
+    finish_run<T, V, EDGE>(p, ty0 + r, tx0 + V * cq, g, bv[s], y, xs, xns, want_part, part_d, part_x);
   }
 }
 
@@ -315,15 +383,6 @@ __device__ inline void fold_partials(double part_d, double part_x, double* red, 
   }
 }
 
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt) but not for
-// its global loads, so register prefetches issued before it stay in flight (a __syncthreads() fence
-// would drain them with vmcnt(0)).  The "memory" clobbers keep LDS accesses on their side.
-__device__ inline void lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 // H^T y at row gr, columns gc .. gc + CW - 1 (zero outside the image on edge tiles)
 template <typename T, int CW, bool EDGE>
 __device__ inline void load_b(const T* __restrict__ bs, int gr, int gc, int n0, int n1, T (&bv)[CW]) {
@@ -336,10 +395,9 @@ __device__ inline void load_b(const T* __restrict__ bs, int gr, int gc, int n0, 
   }
 }
 
-// PREB 1: the H^T y values of the thread's pass-B pixels are loaded into registers right behind the
-// window loads (one global round trip per tile instead of two); PREB 2: they are issued as pass B
-// starts, so that their latency overlaps pass B's TV stencil and G1 sweep.  Both use lds_sync().
-template <typename T, int R, bool EDGE, int PREB>
+// STAGED (the default): pass B parks its results in LDS and the tile is finished in row-major order
+// (epilogue_staged); otherwise each pass-B item finishes its own pixels (finish_run in item order).
+template <typename T, int R, bool EDGE, bool STAGED>
 __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
                                 const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
                                 T* __restrict__ xns, double* __restrict__ partials) {
@@ -357,39 +415,52 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     KT[kKT + tid] = p.k1[tid];
   }
   double part_d = 0.0, part_x = 0.0;
-  if constexpr (PREB != 0) {
-    T bq[KB][V][CW];
-    auto issue_b = [&] {
+  if constexpr (STAGED) {
+    using S = Stage<T, R>;
+    load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+    __syncthreads();
+    pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
+    __syncthreads();
+    T st[KB][V][CW];
+    pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
 #pragma unroll
-      for (int k = 0; k < KB; ++k) {
-        const int it = tid + k * kThreads;
-        int a = 0, cb = 0;
-        if (it < L::NPB) L::pass_b_item(it, a, cb);
+      for (int w = 0; w < CW; ++w) st[k][u][w] = g[w];
+    });
+    __syncthreads();  // every G1 sweep is done with PT: O may overwrite it
+    T* O = PT;
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int it = tid + k * kThreads;
+      if (it < L::NPB) {
+        int a, cb;
+        L::pass_b_item(it, a, cb);
 #pragma unroll
         for (int u = 0; u < V; ++u) {
-          if (it < L::NPB) load_b<T, CW, EDGE>(bs, ty0 + V * a + u, tx0 + CW * cb, n0, n1, bq[k][u]);
+          T* o = O + (V * a + u) * S::OP + CW * cb;
+          if constexpr (CW == 2) {
+            const T pr[2] = {st[k][u][0], st[k][u][1]};
+            if constexpr (sizeof(T) == 4) *reinterpret_cast<float2*>(o) = make_float2(pr[0], pr[1]);
+            else st_vec<T, 2>(o, pr);
+          } else {
+            o[0] = st[k][u][0];
+          }
         }
       }
-    };
-    if constexpr (PREB == 1) load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps, issue_b);
-    else load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
-    lds_sync();
-    pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
-    lds_sync();
-    if constexpr (PREB == 2) issue_b();
-    auto bload = [&](int k, int u, int, int, T(&bv)[CW]) {
-#pragma unroll
-      for (int w = 0; w < CW; ++w) bv[w] = bq[k][u][w];
-    };
-    pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
-    if (partials) fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { lds_sync(); });
+    }
+    __syncthreads();
+    epilogue_staged<T, R, EDGE>(p, A, O, ty0, tx0, bs, xs, xns, partials != nullptr, part_d, part_x);
+    if (partials) fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
   } else {
     load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
     __syncthreads();
     pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
     __syncthreads();
-    auto bload = [&](int, int, int gr, int gc, T(&bv)[CW]) { load_b<T, CW, EDGE>(bs, gr, gc, n0, n1, bv); };
-    pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
+    const bool want = partials != nullptr;
+    pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, [&](int, int, int gr, int gc, const T(&g)[CW], const T(&y)[CW]) {
+      T bv[CW];
+      load_b<T, CW, EDGE>(bs, gr, gc, n0, n1, bv);
+      finish_run<T, CW, EDGE>(p, gr, gc, g, bv, y, xs, xns, want, part_d, part_x);
+    });
     if (partials) {
       // A / PT are free again once every thread is past pass B
       fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
@@ -397,8 +468,8 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   }
 }
 
-template <typename T, int R, int PREB, int OCC>
-__global__ void __launch_bounds__(kThreads, OCC) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
+template <typename T, int R, bool STAGED>
+__global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
                                                             const T* __restrict__ xp, const T* __restrict__ b,
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
@@ -419,17 +490,17 @@ __global__ void __launch_bounds__(kThreads, OCC) pgd_tv2d_kernel(PgdParams<T> p,
   const bool interior = p.vec_ok && img <= 0x7fffffff && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0 &&
                         tx0 - L::CA >= 0 && tx0 + TX + L::CA <= p.n1;
   if (interior)
-    pgd_tile<T, R, false, PREB>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
+    pgd_tile<T, R, false, STAGED>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
   else
-    pgd_tile<T, R, true, PREB>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
+    pgd_tile<T, R, true, STAGED>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
 }
 
-template <typename T, int R, int PREB, int OCC = 4>
+template <typename T, int R, bool STAGED>
 int launch_pgd_v(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
                  hipStream_t s) {
   using L = Layout<T, R>;
   const size_t smem = L::BYTES;
-  auto kern = pgd_tv2d_kernel<T, R, PREB, OCC>;
+  auto kern = pgd_tv2d_kernel<T, R, STAGED>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -443,12 +514,9 @@ int launch_pgd_v(const PgdParams<T>& p, const void* x, const void* xp, const voi
 template <typename T, int R>
 int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
                hipStream_t s) {
-  const int k = tuning(PXA_TUNE_PGD_KERNEL);
-  if (k == 6) return launch_pgd_v<T, R, 1>(p, x, xp, b, xn, partials, s);
-  if (k == 7) return launch_pgd_v<T, R, 2>(p, x, xp, b, xn, partials, s);
-  if (k == 8) return launch_pgd_v<T, R, 1, 3>(p, x, xp, b, xn, partials, s);
-  if (k == 9) return launch_pgd_v<T, R, 0, 3>(p, x, xp, b, xn, partials, s);
-  return launch_pgd_v<T, R, 0>(p, x, xp, b, xn, partials, s);
+  // 4: item-order epilogue (the round-1 kernel), kept selectable for A/B measurements
+  if (tuning(PXA_TUNE_PGD_KERNEL) == 4) return launch_pgd_v<T, R, false>(p, x, xp, b, xn, partials, s);
+  return launch_pgd_v<T, R, true>(p, x, xp, b, xn, partials, s);
 }
 
 // =====================================================================================================
@@ -690,22 +758,24 @@ __global__ void __launch_bounds__(kThreads, 2) pgd_tv2d_persistent(PgdParams<flo
       if (has_next) wait_vm<P::NDW>();
       else wait_vm<0>();
       asm volatile("" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
-      auto bload = [&](int, int u, int, int, float(&bv)[2]) {
-        bv[0] = bq[u].x;
-        bv[1] = bq[u].y;
-      };
-      pass_b<float, R, false>(q, A, PT, KT, o.ty0, o.tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
+      const bool want = partials != nullptr;
+      pass_b<float, R, false>(q, A, PT, KT, o.ty0, o.tx0,
+                           [&](int, int u, int gr, int gc, const float(&g)[2], const float(&y)[2]) {
+                             const float bv[2] = {bq[u].x, bq[u].y};
+                             finish_run<float, 2, false>(q, gr, gc, g, bv, y, xs, xns, want, part_d, part_x);
+                           });
     } else {
       pass_a<float, R, true>(q, A, PT, KT, o.ty0);
       lds_barrier();
       if (has_next) wait_vm<P::NDW>();
       else wait_vm<0>();
       asm volatile("" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
-      auto bload = [&](int, int u, int, int, float(&bv)[2]) {
-        bv[0] = bq[u].x;
-        bv[1] = bq[u].y;
-      };
-      pass_b<float, R, true>(q, A, PT, KT, o.ty0, o.tx0, bload, xs, xns, partials != nullptr, part_d, part_x);
+      const bool want = partials != nullptr;
+      pass_b<float, R, true>(q, A, PT, KT, o.ty0, o.tx0,
+                           [&](int, int u, int gr, int gc, const float(&g)[2], const float(&y)[2]) {
+                             const float bv[2] = {bq[u].x, bq[u].y};
+                             finish_run<float, 2, true>(q, gr, gc, g, bv, y, xs, xns, want, part_d, part_x);
+                           });
     }
     if (partials) fold_partials(part_d, part_x, red, partials, o.tile, [] { lds_barrier(); });
     prev_interior = interior && partials == nullptr;

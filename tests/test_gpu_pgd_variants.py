@@ -1,11 +1,11 @@
 """
-The persistent LDS-DMA PGD kernel (pgd_tv2d_persistent, opt-in PXA_TUNE_PGD_KERNEL = 5 for fp32 images
-with n1 % 4 == 0) against the per-tile kernel (pgd_tv2d_kernel, the default): both run the same per-tile
-arithmetic (load_window's yk, pass_a, pass_b in csrc/pgd_tv2d.hip), so x_new and the RelError
-partials must agree BIT FOR BIT on every shape class: interior and edge tiles, fewer tiles than
-resident workgroups, ragged tile grids, stacks with shared and per-image data, every blur radius
-1..8, every prox kind.  The tile kernel itself is pinned to the oracle by test_gpu_parity.py and
-test_gpu_bench_shapes.py.
+PGD kernel variants against the default tile kernel (pgd_tv2d_kernel with the staged row-major
+epilogue): PXA_TUNE_PGD_KERNEL = 4 (item-order epilogue) and 5 (persistent LDS-DMA kernel, fp32,
+n1 % 4 == 0).  All run the same per-pixel arithmetic (load_window's yk, pass_a, pass_b, finish_run
+in csrc/pgd_tv2d.hip), so x_new must agree BIT FOR BIT on every shape class: interior and edge tiles,
+fewer tiles than resident workgroups, ragged tile grids, stacks with shared and per-image data,
+every blur radius 1..8, every prox kind.  The default kernel itself is pinned to the oracle by
+test_gpu_parity.py and test_gpu_bench_shapes.py.
 """
 import numpy as np
 import pytest
@@ -82,18 +82,19 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("kernel", [5, 6, 7, 8, 9])
+@pytest.mark.parametrize("kernel", [4, 5])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}-sig{c[3]}-{c[4]}")
 def test_kernel_variants_bit_exact_vs_tile_kernel(case, kernel):
-    """5 persistent LDS-DMA kernel; 6 / 7 tile kernel with H^T y prefetched behind the window loads /
-    at the start of pass B; 8 / 9 the prefetching / plain tile kernel at 3 workgroups per CU."""
+    """4 the item-order epilogue, 5 the persistent LDS-DMA kernel, against the default (staged
+    row-major epilogue): x_new bit for bit; the RelError partials are the same double sums in another
+    association order (<= 1e-12 relative)."""
     sh, stack, y_images, sigma, g_kind = case
     s = _plan(sh, stack, y_images, sigma, g_kind)
     a, a_p, pa = _step(s, kernel)
     b, b_p, pb = _step(s, 0)
     assert np.array_equal(a, b)
     assert np.array_equal(a_p, b_p) and np.array_equal(a, a_p)
-    assert np.array_equal(pa, pb) and np.all(pa >= 0)
+    assert np.allclose(pa, pb, rtol=1e-12, atol=0) and np.all(pa >= 0)
 
 
 def test_kernel_knob_round_trips():
