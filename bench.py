@@ -216,28 +216,45 @@ def cpu_baseline(n0, n1, seed, budget_s, threads, lam=0.01, mu=0.01, sigma=2.0):
 
 # ----------------------------------------------------------------------------- timing helpers
 class Ctx:
-    def __init__(self, world, rank, dist):
-        self.world, self.rank, self.dist = world, rank, dist
+    """Rank bookkeeping of one bench process; the scalar collectives run on the GPU under RCCL and on
+    the host under gloo (CPU rehearsals and tests)."""
+
+    def __init__(self, world, rank, dist, coll_device="cuda"):
+        self.world, self.rank, self.dist, self.coll_device = world, rank, dist, coll_device
 
     def barrier(self):
         if self.world > 1:
             self.dist.barrier()
 
-    def max_over_ranks(self, v):
+    def _reduce(self, v, op):
         import torch
 
-        t = torch.tensor([float(v)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.coll_device)
         if self.world > 1:
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            self.dist.all_reduce(t, op=op)
         return float(t.item())
+
+    def max_over_ranks(self, v):
+        return self._reduce(v, self.dist.ReduceOp.MAX if self.world > 1 else None)
 
     def sum_over_ranks(self, v):
-        import torch
+        return self._reduce(v, self.dist.ReduceOp.SUM if self.world > 1 else None)
 
-        t = torch.tensor([float(v)], dtype=torch.float64, device="cuda")
-        if self.world > 1:
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+
+def prime_loop(ctx, gen, seconds, chunk=200, sync=None):
+    """Untimed priming: run `chunk` steps at a time until `seconds` have passed.  Every continue/stop
+    decision is agreed over the ranks (max of the per-rank "time left" flags), so all ranks run the
+    same number of steps: each stop check of a distributed solver is a collective, and ranks that ran
+    different step counts would block in it.  Returns the number of steps run."""
+    n = 0
+    t_end = time.perf_counter() + seconds
+    while ctx.max_over_ranks(1.0 if time.perf_counter() < t_end else 0.0) > 0:
+        for _ in range(chunk):
+            next(gen)
+        n += chunk
+        if sync is not None:
+            sync()
+    return n
 
 
 def timed_steps(ctx, gen, warmup, steps, timer=None):
@@ -288,11 +305,7 @@ def run_pgd(ctx, f, g, stop_rate, warmup, steps, fused, prime_s=0.0, kernel_time
         # and caches at steady state before the measured solver's W + K steps (which it does not change)
         s, _ = new_solver()
         gen = s.steps()
-        t_end = time.perf_counter() + prime_s
-        while time.perf_counter() < t_end:
-            for _ in range(200):
-                next(gen)
-            torch.cuda.synchronize()
+        prime_loop(ctx, gen, prime_s, sync=torch.cuda.synchronize)
         del s, gen
     slvr, rel = new_solver()
     # prime the stop-check path once (loads its kernels' code objects) so that a warmup shorter than
@@ -452,7 +465,7 @@ def main():
     from pyxu_amd import _dev
 
     _dev.tuning(_dev.TUNE_PGD_KERNEL, args.pgd_kernel)
-    ctx = Ctx(world, rank, dist)
+    ctx = Ctx(world, rank, dist, coll_device="cpu" if backend == "gloo" else "cuda")
 
     n0 = n1 = args.n
     N = n0 * n1

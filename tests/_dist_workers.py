@@ -280,3 +280,24 @@ def gpu_row_sharded_admm(rank, world, M, N, n_iter):
             s1.fit(x0=to_device(np.zeros(N, np.float32)), tau=tau, stop_crit=pxst.MaxIter(n_iter))
             out["x_ref"] = to_NUMPY(s1.solution())
     return out
+
+
+def bench_prime_agreement(rank, world, budgets):
+    """bench.prime_loop with a different time budget per rank: the ranks must still run the same
+    number of steps (each stop check of the primed solver is a collective)."""
+    import itertools
+    import time
+
+    import torch.distributed as dist
+
+    import bench
+
+    ctx = bench.Ctx(world, rank, dist, coll_device="cpu")
+
+    def steps():
+        for i in itertools.count():
+            time.sleep(0.0005 * (rank + 1))  # ranks step at different speeds too
+            yield i
+
+    n = bench.prime_loop(ctx, steps(), budgets[rank], chunk=10)
+    return {"n": n}

@@ -133,3 +133,10 @@ def test_gloo_slab_halo_exchange_matches_global(world, kind, halo):
     for r in range(world):
         np.testing.assert_allclose(res[r]["apply"], ref_a, rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(res[r]["adjoint"], ref_t, rtol=1e-12, atol=1e-12)
+
+
+def test_bench_prime_loop_ranks_agree_on_step_count():
+    """bench.py's untimed priming: ranks with different clocks / budgets run the same number of steps,
+    so no rank blocks in a stop-check collective that the others never reach (the N>1 bench hang)."""
+    res = spawn("bench_prime_agreement", budgets=[0.05, 0.3])
+    assert res[0]["n"] == res[1]["n"] and res[0]["n"] >= 10
