@@ -50,6 +50,8 @@ extern "C" {
 /* Kernel-selection knobs (pxa_tuning). */
 #define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 auto (the tile kernel, staged row-major epilogue),
                                  4 tile kernel with the item-order epilogue, 5 persistent LDS-DMA kernel (fp32) */
+#define PXA_TUNE_NORMAL_DIAG 1 /* pxa_dense_normal timing probes (WRONG results, measurement only): 0 off,
+                                  1 no x loads, 2 no cross-wave reduction, 3 no LDS accumulator */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */
@@ -260,6 +262,18 @@ int pxa_gradient2_adjoint(int dtype, int64_t stack, int ndim, const int64_t* sha
 size_t pxa_dense_workspace_bytes(int dtype, int trans, int64_t M, int64_t N, int64_t B);
 int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, const void* A, const void* X, void* Y,
                      void* work, void* stream);
+
+/* Normal operator of a dense LinOp in ONE pass over A: Y = s * A^T (A X) + d * X, one right-hand side
+ * (B = 1), fp32, N % 4 == 0, N <= 65536.  Replaces the apply of the CG operator Q + I / tau that
+ * QuadraticFunc.prox builds for ADMM's x-update (abc/operator.py:1273-1291 QuadraticFunc.prox,
+ * opt/solver/pds.py:1645-1653, Q = K^T c K from abc/arithmetic.py ChainRule._quad_spec), i.e. the
+ * K.apply -> K.adjoint -> AddRule chain of opt/solver/cg.py:130 (`Ap = self._A.apply(p)`).
+ * Workgroup partials of A^T (A X) (fixed partition) are summed in a fixed order: deterministic.
+ * pxa_dense_normal_workspace_bytes() returns 0 for unsupported cases, where pxa_dense_normal returns
+ * PXA_ERR_UNSUPPORTED (the caller then composes pxa_dense_matmat calls). */
+size_t pxa_dense_normal_workspace_bytes(int dtype, int64_t M, int64_t N, int64_t B);
+int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, const void* X, double s, double d,
+                     void* Y, void* work, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Array primitives: the data movement of the operator algebra and the NumPy-named functions of the

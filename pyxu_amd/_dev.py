@@ -149,6 +149,7 @@ def storage_exclusive(t) -> bool:
     return _USE_COUNT(t.untyped_storage()._cdata) <= 2
 
 
+TUNE_NORMAL_DIAG = 1  # PXA_TUNE_NORMAL_DIAG: pxa_dense_normal timing probes (wrong results)
 TUNE_PGD_KERNEL = 0  # PXA_TUNE_PGD_KERNEL: 0 auto (tile kernel), 5 persistent LDS-DMA kernel
 
 
@@ -675,6 +676,30 @@ def dense_matmat(A, X, trans):
         lib.pxa_dense_matmat(dtcode(X), int(trans), M, N, B, ptr(A), ptr(X), ptr(Y), ptr(work) if work is not None else None, stream()),
         "pxa_dense_matmat",
     )
+    return Y
+
+
+def dense_normal_supported(A, x):
+    """True when pxa_dense_normal takes (A, x): one fp32 right-hand side, N % 4 == 0, N <= 65536."""
+    M, N = A.shape
+    B = x.numel() // max(N, 1)
+    return (A.dtype == x.dtype and x.shape[-1] == N and B == 1 and A.is_contiguous() and x.is_contiguous()
+            and int(lib.pxa_dense_normal_workspace_bytes(dtcode(x), M, N, 1)) > 0)
+
+
+def dense_normal(A, x, s, d, work=None):
+    """Y = s * A^T (A x) + d * x in one pass over A (pxa_dense_normal); `work`: a reusable uint8 device
+    buffer of at least pxa_dense_normal_workspace_bytes bytes (allocated when None)."""
+    torch = _torch()
+    M, N = A.shape
+    wsz = int(lib.pxa_dense_normal_workspace_bytes(dtcode(x), M, N, 1))
+    if wsz == 0:
+        raise ValueError("pxa_dense_normal: unsupported operand (see dense_normal_supported)")
+    if work is None or work.numel() < wsz:
+        work = torch.empty((wsz,), dtype=torch.uint8, device=x.device)
+    Y = empty(x.shape, x)
+    check(lib.pxa_dense_normal(dtcode(x), M, N, 1, ptr(A), ptr(x), float(s), float(d), ptr(Y), ptr(work), stream()),
+          "pxa_dense_normal")
     return Y
 
 

@@ -60,6 +60,8 @@ EXPORTS = {
     "pxa_gradient2_adjoint": (i32, [i32, i64, i32, P_i64, i32, P_int, P_int, P_f64, P_int, P_f64, vp, vp, vp]),
     "pxa_dense_workspace_bytes": (sz, [i32, i32, i64, i64, i64]),
     "pxa_dense_matmat": (i32, [i32, i32, i64, i64, i64, vp, vp, vp, vp, vp]),
+    "pxa_dense_normal_workspace_bytes": (sz, [i32, i64, i64, i64]),
+    "pxa_dense_normal": (i32, [i32, i64, i64, i64, vp, vp, f64, f64, vp, vp, vp]),
     "pxa_copy2d": (i32, [i32, i64, i64, vp, i64, i64, vp, i64, i32, vp]),
     "pxa_unary": (i32, [i32, i32, i64, vp, vp, vp]),
     "pxa_binary": (i32, [i32, i32, i64, vp, f64, vp, f64, vp, vp]),

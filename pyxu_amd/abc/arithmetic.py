@@ -55,6 +55,23 @@ def _quad_Q(op):
     return op._quad_spec()[0]
 
 
+def _memo_quad_spec(func):
+    """(Q, c, t) of a rule-built quadratic, computed once per precision: the operator is immutable, and
+    the reference's re-evaluation on every QuadraticFunc.prox call (abc/arithmetic.py ChainRule /
+    ArgShiftRule._quad_spec) rebuilds the operators and reads t = f(shift) back from the device -- a
+    host sync per ADMM x-update."""
+
+    def memo(self):
+        key = pxrt.getPrecision()
+        cache = self.__dict__.setdefault("_quad_spec_memo", {})
+        if key not in cache:
+            cache[key] = func(self)
+        return cache[key]
+
+    memo.__wrapped__ = func
+    return memo
+
+
 class Rule:
     def op(self):
         raise NotImplementedError
@@ -64,6 +81,8 @@ class Rule:
             for name in p.arithmetic_methods():
                 func = getattr(self.__class__, name, None)
                 if func is not None:
+                    if name == "_quad_spec":
+                        func = _memo_quad_spec(func)
                     setattr(op, name, types.MethodType(func, op))
 
     @staticmethod
@@ -650,6 +669,13 @@ class ChainRule(Rule):
 
     @pxrt.enforce_precision(i="arr")
     def grad(self, arr):
+        P = pxo.Property
+        if {P.LINEAR, P.FUNCTIONAL} <= self._lhs.properties() and self._rhs.has(P.LINEAR):
+            # a linear functional's gradient does not depend on where it is taken: skip rhs.apply(arr)
+            # (the reference evaluates it and discards it; for ADMM's c o K that is a full pass over K
+            # per QuadraticFunc.prox call; reference arithmetic.py:1288-1291)
+            y = _dev.zeros((*arr.shape[:-1], self._rhs.codim), arr)
+            return self._rhs.adjoint(self._lhs.grad(y))
         x = self._lhs.grad(self._rhs.apply(arr))
         if arr.ndim == 1 or self._rhs.has(pxo.Property.LINEAR):
             return self._rhs.jacobian(arr).adjoint(x)

@@ -297,6 +297,220 @@ inline size_t mfma_workspace_bytes(int64_t P, int64_t Q, int64_t K) {
   return m.splits > 1 ? (size_t)m.splits * (size_t)P * (size_t)Q * sizeof(float) : 0;
 }
 
+
+// ------------------------------------------------------------------ normal operator, one pass over A
+// Y = s * A^T (A x) + d * x for ONE right-hand side (fp32, N % 4 == 0, N <= kNormMaxN): the
+// QuadraticFunc.prox CG operator of ADMM (K^T K + I / tau, opt/solver/pds.py:1645-1653 via
+// abc/arithmetic.py ChainRule._quad_spec + AddRule) without the second pass over A.
+//
+// A 1024-thread workgroup (one per CU: its LDS use excludes a second) owns rows g, g + G, g + 2G, ...
+// of A.  A row (N <= 65536 fp32) is held in registers, 16 B per lane-vector, NV vectors per thread
+// (64 VGPRs at N = 65536): phase 1 forms t = <A[m,:], x> (x re-read from L2, fp32 4-element partials
+// summed in double, fixed-order workgroup reduction), phase 2 adds t * A[m,:] into the workgroup's
+// partial of A^T (A x) -- NV - NL vectors per thread in registers, NL in LDS (thread-private slots,
+// conflict-free ds_read/write_b128) -- and issues the loads of the next row into each register right
+// after its last use, so the next row streams in behind phase 2.  The G partials (G x N fp32) are
+// summed in a fixed order by normal_final_kernel: deterministic run to run.  HBM traffic: A once
+// (M N 4 B) + 2 G N 4 B of partials (64 MB each way at G = 256, N = 65536) against 2 M N 4 B for
+// the apply + adjoint pair.
+constexpr int kNormThreads = 1024;
+constexpr int kNormMaxN = 65536;
+constexpr int kNormG = 256;  // workgroups (fixed: the partition, hence the rounding, does not depend on the device)
+constexpr int kNormRegAcc = 7;  // accumulator vectors per thread kept in registers
+typedef float nf4 __attribute__((ext_vector_type(4)));
+
+// A row vector, read once: non-temporal (streaming) policy, so that the 8 MB of rows an XCD streams per
+// row-time do not evict x (256 KB, re-read by every row) from its 4 MB L2.
+__device__ inline float4 ld_stream(const float4* p) {
+  const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+template <int NV>
+struct NormPlan {
+  static constexpr int NL = NV > kNormRegAcc ? NV - kNormRegAcc : 0;  // accumulator vectors in LDS
+  static constexpr int NR = NV - NL;
+  static constexpr size_t LDS = (size_t)NL * kNormThreads * 16 + 2 * (kNormThreads / 64) * sizeof(double);
+};
+
+// DIAG != 0: timing probes with a part of the work removed (wrong results; PXA_TUNE_NORMAL_DIAG only):
+// 1 no x loads (the dot uses the row itself), 2 no cross-wave reduction (t = the thread's own dot),
+// 3 no LDS accumulator traffic.
+template <int NV, bool FULL, int DIAG = 0>
+__global__ void __launch_bounds__(kNormThreads) normal_rows_kernel(int64_t M, int N4, const float* __restrict__ A,
+                                                                   const float* __restrict__ x,
+                                                                   float* __restrict__ part) {
+  using P = NormPlan<NV>;
+  extern __shared__ __align__(16) unsigned char nsm[];
+  float4* accl = reinterpret_cast<float4*>(nsm);  // [NL][kNormThreads]
+  double* red = reinterpret_cast<double*>(nsm + (size_t)P::NL * kNormThreads * 16);  // 2 x 16 (parity)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t G = gridDim.x;
+  const float4* A4 = reinterpret_cast<const float4*>(A);
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  float4 row[NV];
+  float4 accr[P::NR];
+#pragma unroll
+  for (int k = 0; k < P::NR; ++k) accr[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < P::NL; ++k) accl[k * kNormThreads + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t m = blockIdx.x;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (m < M) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int j = tid + k * kNormThreads;
+      row[k] = (FULL || j < N4) ? ld_stream(A4 + m * N4 + j) : z4;
+    }
+  }
+  int par = 0;
+  for (; m < M; m += G) {
+    // phase 1: t = <A[m,:], x>.  x is re-read every row (L2 hits): kept live across rows it would take
+    // 4 NV more registers, so its address is laundered per row to stop the compiler from hoisting it.
+    int xo = 0;
+    asm volatile("" : "+s"(xo));
+    const float4* xr = x4 + xo;
+    double d = 0.0;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int j = tid + k * kNormThreads;
+      const float4 xv = DIAG == 1 ? row[k] : ((FULL || j < N4) ? xr[j] : z4);
+      float q = row[k].x * xv.x;
+      q = fmaf(row[k].y, xv.y, q);
+      q = fmaf(row[k].z, xv.z, q);
+      q = fmaf(row[k].w, xv.w, q);
+      d += (double)q;
+    }
+    double tt = d;
+    if (DIAG != 2) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) d += __shfl_down(d, off, 64);
+      if (lane == 0) red[par * 16 + wave] = d;
+      __syncthreads();
+      tt = 0.0;
+#pragma unroll
+      for (int w = 0; w < kNormThreads / 64; ++w) tt += red[par * 16 + w];  // fixed order, same in every thread
+      par ^= 1;  // the next row writes the other half: no second barrier needed
+    }
+    const float t = (float)tt;
+    // phase 2: acc += t * A[m,:]; each register refilled with the next row right after its last use
+    const int64_t mn = m + G;
+    const bool more = mn < M;  // uniform
+    // uniform row base (SGPR) + lane offset; the last row re-reads itself (cache hits) so that the
+    // refills are unconditional
+    const float4* an = A4 + (more ? mn : m) * (int64_t)N4;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int j = tid + k * kNormThreads;
+      if (k < P::NR) {
+        accr[k].x = fmaf(row[k].x, t, accr[k].x);
+        accr[k].y = fmaf(row[k].y, t, accr[k].y);
+        accr[k].z = fmaf(row[k].z, t, accr[k].z);
+        accr[k].w = fmaf(row[k].w, t, accr[k].w);
+      } else if (DIAG == 3) {
+        accr[k % P::NR].x = fmaf(row[k].x, t, accr[k % P::NR].x);
+      } else {
+        float4 a = accl[(k - P::NR) * kNormThreads + tid];
+        a.x = fmaf(row[k].x, t, a.x);
+        a.y = fmaf(row[k].y, t, a.y);
+        a.z = fmaf(row[k].z, t, a.z);
+        a.w = fmaf(row[k].w, t, a.w);
+        accl[(k - P::NR) * kNormThreads + tid] = a;
+      }
+      row[k] = (FULL || j < N4) ? ld_stream(an + j) : z4;
+    }
+  }
+  float4* out = reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * N4 * 4);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int j = tid + k * kNormThreads;
+    if (FULL || j < N4) out[j] = k < P::NR ? accr[k] : accl[(k - P::NR) * kNormThreads + tid];
+  }
+}
+
+// Fixed-order sum of the G workgroup partials in two launches with enough loads in flight: stage 1
+// sums slice y of kNormSlice consecutive partials for one float4 column group per thread (double,
+// g ascending); stage 2 adds the G / kNormSlice slice sums (ascending) and forms s * sum + d * x.
+constexpr int kNormSlice = 32;
+
+__global__ void __launch_bounds__(kBlock) normal_sum_kernel(int N4, int G, const float4* __restrict__ part,
+                                                            double4* __restrict__ sums) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N4) return;
+  const int g0 = blockIdx.y * kNormSlice;
+  const int g1 = g0 + kNormSlice < G ? g0 + kNormSlice : G;
+  double4 acc = make_double4(0.0, 0.0, 0.0, 0.0);
+#pragma unroll 8
+  for (int g = g0; g < g1; ++g) {
+    const float4 v = part[(int64_t)g * N4 + c];
+    acc.x += (double)v.x;
+    acc.y += (double)v.y;
+    acc.z += (double)v.z;
+    acc.w += (double)v.w;
+  }
+  sums[(int64_t)blockIdx.y * N4 + c] = acc;
+}
+
+__global__ void __launch_bounds__(kBlock) normal_final_kernel(int N4, int slices, const double4* __restrict__ sums,
+                                                              const float4* __restrict__ x, float s, float dd,
+                                                              float4* __restrict__ Y) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N4) return;
+  double4 acc = sums[c];
+  for (int y = 1; y < slices; ++y) {
+    const double4 v = sums[(int64_t)y * N4 + c];
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  const float4 xv = x[c];
+  Y[c] = make_float4(fmaf(s, (float)acc.x, dd * xv.x), fmaf(s, (float)acc.y, dd * xv.y),
+                     fmaf(s, (float)acc.z, dd * xv.z), fmaf(s, (float)acc.w, dd * xv.w));
+}
+
+inline int normal_groups(int64_t M) { return (int)(M < kNormG ? M : kNormG); }
+inline int normal_slices(int G) { return (G + kNormSlice - 1) / kNormSlice; }
+inline size_t normal_sums_offset(int G, int64_t N) { return ((size_t)G * (size_t)N * sizeof(float) + 255) / 256 * 256; }
+
+template <int NV>
+int launch_normal(int64_t M, int64_t N, const float* A, const float* x, float s, float d, float* Y, float* work,
+                  hipStream_t st) {
+  using P = NormPlan<NV>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)normal_rows_kernel<NV, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)P::LDS);
+    (void)hipFuncSetAttribute((const void*)normal_rows_kernel<NV, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)P::LDS);
+    attr = true;
+  }
+  const int G = normal_groups(M);
+  const int N4 = (int)(N / 4);
+  const int diag = NV == 16 ? tuning(PXA_TUNE_NORMAL_DIAG) : 0;
+  if (N4 == NV * kNormThreads && diag >= 1 && diag <= 3) {
+    auto kd = diag == 1 ? normal_rows_kernel<NV, true, 1> : diag == 2 ? normal_rows_kernel<NV, true, 2>
+                                                                       : normal_rows_kernel<NV, true, 3>;
+    (void)hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P::LDS);
+    hipLaunchKernelGGL(kd, dim3(G), dim3(kNormThreads), P::LDS, st, M, N4, A, x, work);
+  } else if (N4 == NV * kNormThreads)
+    hipLaunchKernelGGL((normal_rows_kernel<NV, true>), dim3(G), dim3(kNormThreads), P::LDS, st, M, N4, A, x, work);
+  else
+    hipLaunchKernelGGL((normal_rows_kernel<NV, false>), dim3(G), dim3(kNormThreads), P::LDS, st, M, N4, A, x, work);
+  int e = last_launch_status();
+  if (e) return e;
+  const int slices = normal_slices(G);
+  double4* sums = reinterpret_cast<double4*>(reinterpret_cast<unsigned char*>(work) + normal_sums_offset(G, N));
+  const unsigned cb = (unsigned)((N4 + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(normal_sum_kernel, dim3(cb, (unsigned)slices), dim3(kBlock), 0, st, N4, G,
+                     reinterpret_cast<const float4*>(work), sums);
+  e = last_launch_status();
+  if (e) return e;
+  hipLaunchKernelGGL(normal_final_kernel, dim3(cb), dim3(kBlock), 0, st, N4, slices, sums,
+                     reinterpret_cast<const float4*>(x), s, d, reinterpret_cast<float4*>(Y));
+  return last_launch_status();
+}
+
 }  // namespace
 }  // namespace pxa
 
@@ -358,6 +572,34 @@ int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, cons
       return PXA_OK;
     }
   });
+}
+
+size_t pxa_dense_normal_workspace_bytes(int dtype, int64_t M, int64_t N, int64_t B) {
+  if (dtype != PXA_F32 || B != 1 || N % 4 != 0 || N > kNormMaxN || M < 1) return 0;
+  const int G = normal_groups(M);
+  // G fp32 partials, then the slice sums (double4 per column group) at a 256-byte aligned offset
+  return normal_sums_offset(G, N) + (size_t)normal_slices(G) * (size_t)N * sizeof(double);
+}
+
+int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, const void* X, double s, double d,
+                     void* Y, void* work, void* stream) {
+  PXA_CHECK_ARG(M >= 1 && N >= 1 && B >= 0);
+  if (B == 0) return PXA_OK;
+  PXA_CHECK_ARG(A != nullptr && X != nullptr && Y != nullptr && Y != X);
+  if (dtype != PXA_F32 && dtype != PXA_F64) return PXA_ERR_DTYPE;
+  if (pxa_dense_normal_workspace_bytes(dtype, M, N, B) == 0) return PXA_ERR_UNSUPPORTED;
+  PXA_CHECK_ARG(work != nullptr && aligned16(A) && aligned16(X) && aligned16(Y) && aligned16(work));
+  hipStream_t st = as_stream(stream);
+  const float* a = (const float*)A;
+  const float* x = (const float*)X;
+  const float fs = (float)s, fd = (float)d;
+  const int64_t nv = (N / 4 + kNormThreads - 1) / kNormThreads;  // vectors per thread
+  if (nv <= 1) return launch_normal<1>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
+  if (nv <= 2) return launch_normal<2>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
+  if (nv <= 4) return launch_normal<4>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
+  if (nv <= 8) return launch_normal<8>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
+  if (nv <= 12) return launch_normal<12>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
+  return launch_normal<16>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
 }
 
 }  // extern "C"

@@ -4,8 +4,13 @@ import numpy as np
 import pyxu_amd.abc as pxa
 import pyxu_amd.runtime as pxrt
 from pyxu_amd import _dev
+from pyxu_amd.opt.solver._normal import normal_form
 
 __all__ = ["CG"]
+
+# m_state key of row statistics a step has already computed for a state variable:
+# {var: (tensor, norm, host-readable row statistic)}, read by pyxu_amd.opt.stop.AbsError
+_ROWSTAT = "__rowstat__"
 
 
 def _rows2d(x):
@@ -70,19 +75,54 @@ class CG(pxa.Solver):
                 return _dev.copy2d(t, _dev.empty(big.shape, t), rows, n, 0, n)
 
             mst["b"], mst["x"] = bcast(b), bcast(x0)
-        mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(mst["x"]))
+        self._apply = self._make_apply(mst["x"])
+        mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._apply(mst["x"]))
         mst["conjugate_dir"] = _dev.copy(mst["residual"])
         self._rr = None  # ||r||^2 of the current residual, carried from the previous step's beta
+        self._Ap_next = None  # A p of the current p, launched ahead by the previous step (see m_step)
+        mst[_ROWSTAT] = {}
+
+    def _make_apply(self, like):
+        """A.apply, or -- when A = s K^T K + d I for one dense K (ADMM's QuadraticFunc.prox operator,
+        opt/solver/_normal.py) and the vectors fit pxa_dense_normal -- the one-pass normal operator."""
+        nf = normal_form(self._A)
+        if nf is None:
+            return self._A.apply
+        mat, s, d = nf
+        if not _dev.dense_normal_supported(mat, like):
+            return self._A.apply
+        work = [None]
+
+        def apply(v):
+            if not _dev.dense_normal_supported(mat, v):
+                return self._A.apply(v)
+            import torch
+
+            if work[0] is None:
+                wsz = int(_dev.lib.pxa_dense_normal_workspace_bytes(_dev.dtcode(v), mat.shape[0], mat.shape[1], 1))
+                work[0] = torch.empty((wsz,), dtype=torch.uint8, device=v.device)
+            return _dev.dense_normal(mat, v, s, d, work=work[0])
+
+        return apply
 
     def m_step(self):
         """cg.py:125-153.  alpha = ||r||^2 / <p, A p> and beta = ||r'||^2 / ||r||^2 are formed on the
         device (pxa_row_ratio, float64 division then the cast the host path would do) and applied per
         row (pxa_axpy_rows), so a step has ONE host read: ||r||^2 for the eps test, issued as an async
-        copy at the end of the previous step."""
+        copy at the end of the previous step.
+
+        Sub-solver runs (QuadraticFunc.prox -> CG, whose stop criterion is the default AbsError on the
+        residual): the new residual's ||r'||^2 is published for that criterion (the same row statistic
+        it would compute, so the same bits), and A p' of the next direction is launched at the end of
+        the step, before the stop check: the check then waits only for ||r'||^2, and the device works on
+        A p' while the host decides.  A p' of the last step is computed and dropped (no state changes)."""
         mst = self._mstate
         CG.steps_taken += 1
+        mst[_ROWSTAT] = {}
         x, r, p = mst["x"], mst["residual"], mst["conjugate_dir"]
-        Ap = self._A.apply(p)
+        Ap, self._Ap_next = self._Ap_next, None
+        if Ap is None:
+            Ap = self._apply(p)
         pAp = _dev.row_reduce(_dev.RED_DOT, _rows2d(p), _rows2d(Ap))
         if self._rr is not None and self._rr[1] is r:
             rr = self._rr[0]  # ||r||^2 of this r: the previous step's beta numerator (identical bits)
@@ -93,17 +133,21 @@ class CG(pxa.Solver):
         _dev.axpy_rows(alpha, 1.0, _rows2d(p), _rows2d(x), out=_rows2d(x))  # x += alpha p
         eps = pxrt.Width(np.dtype(str(x.dtype).replace("torch.", ""))).eps()
         if np.any(rr.host() <= eps):
-            _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
+            _dev.axpby(1.0, mst["b"], -1.0, self._apply(x), out=r)
         else:
             _dev.axpy_rows(alpha, -1.0, _rows2d(Ap), _rows2d(r), out=_rows2d(r))  # r -= alpha A p
         if self._astate["idx"] % mst["restart_rate"] == 0:
-            _dev.axpby(1.0, mst["b"], -1.0, self._A.apply(x), out=r)
+            _dev.axpby(1.0, mst["b"], -1.0, self._apply(x), out=r)
             _dev.axpby(0.0, p, 1.0, r, out=p)  # beta = 0
         else:
             rr_new = _dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r))
+            hr = _HostRows(rr_new)  # async copy of ||r'||^2, event recorded before beta / p / A p'
             beta = _dev.row_ratio(rr_new, rr.dev, p)
             _dev.axpy_rows(beta, 1.0, _rows2d(p), _rows2d(r), out=_rows2d(p))  # p = r + beta p
-            self._rr = (_HostRows(rr_new), r)
+            self._rr = (hr, r)
+            if self._astate.get("internal"):
+                mst[_ROWSTAT] = {"residual": (r, 2, hr)}
+                self._Ap_next = self._apply(p)
         mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
 
     def default_stop_crit(self):
@@ -113,7 +157,7 @@ class CG(pxa.Solver):
 
     def objective_func(self):
         x, b = self._mstate["x"], self._mstate["b"]
-        f = _dev.axpby(0.5, self._A.apply(x), -1.0, b)
+        f = _dev.axpby(0.5, self._apply(x), -1.0, b)
         r = _dev.row_reduce(_dev.RED_DOT, f.reshape(-1, f.shape[-1]), x.reshape(-1, x.shape[-1]))
         return _dev.cast(r, x).reshape(*x.shape[:-1], 1)
 

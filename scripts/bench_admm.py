@@ -73,6 +73,17 @@ def main():
         e1.record()
         e1.synchronize()
         pair_ms = e0.elapsed_time(e1) / 20
+        # the one-pass normal operator that CG now uses for A p (pxa_dense_normal), same vector
+        normal_ms = None
+        if _dev.dense_normal_supported(Kd, p):
+            for _ in range(3):
+                _dev.dense_normal(Kd, p, 1.0, 1.0)
+            e0.record()
+            for _ in range(20):
+                _dev.dense_normal(Kd, p, 1.0, 1.0)
+            e1.record()
+            e1.synchronize()
+            normal_ms = e0.elapsed_time(e1) / 20
         shutil.rmtree(s.workdir, ignore_errors=True)
     ms_outer = 1e3 * dt / outer
     ms_cg = ms_outer / max(inner, 1e-9)
@@ -82,7 +93,10 @@ def main():
                       "gemv_pair_ms": round(pair_ms, 4),
                       "gemv_pair_gbs": round(2 * M * N * 4 / (pair_ms * 1e-3) / 1e9, 1),
                       "gemv_pair_frac_8tbs": round(2 * M * N * 4 / (pair_ms * 1e-3) / 8e12, 3),
-                      "cg_iter_frac_8tbs": round(2 * M * N * 4 / (ms_cg * 1e-3) / 8e12, 3)}), flush=True)
+                      "cg_iter_frac_8tbs": round(2 * M * N * 4 / (ms_cg * 1e-3) / 8e12, 3),
+                      "normal_ms": None if normal_ms is None else round(normal_ms, 4),
+                      "normal_gbs_of_one_pass": None if normal_ms is None else round(M * N * 4 / (normal_ms * 1e-3) / 1e9, 1)}),
+          flush=True)
 
 
 if __name__ == "__main__":

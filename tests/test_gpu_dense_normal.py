@@ -1,0 +1,151 @@
+"""
+GPU tests of the one-pass normal operator (pxa_dense_normal) and of its use inside CG / ADMM:
+  * the kernel against a float64 NumPy restatement of s * A^T (A x) + d * x (north_star fp32 tolerance
+    1e-5 norm-wise), for every register/LDS split of the row (N = 256 .. 65536, full and ragged last
+    vector blocks, M smaller and larger than the 256-workgroup partition), and bit-identical run to run;
+  * the operator-tree matcher on the operator ADMM builds (reference abc/operator.py:1273-1291,
+    abc/arithmetic.py:1255-1264), and on trees it must reject;
+  * ADMM / CG trajectories through the fused operator against the unfused operator and the oracle.
+"""
+import numpy as np
+import pytest
+
+import oracle as orc
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs an MI355X", allow_module_level=True)
+
+import pyxu_amd.abc as pxa  # noqa: E402
+import pyxu_amd.operator as pxo  # noqa: E402
+import pyxu_amd.opt.solver as pxs  # noqa: E402
+import pyxu_amd.opt.stop as pxst  # noqa: E402
+import pyxu_amd.runtime as pxrt  # noqa: E402
+from pyxu_amd import _dev  # noqa: E402
+from pyxu_amd.opt.solver._normal import normal_form  # noqa: E402
+from pyxu_amd.util import to_device, to_NUMPY  # noqa: E402
+
+
+def _ref(A, x, s, d):
+    A64, x64 = A.astype(np.float64), x.astype(np.float64)
+    return s * (A64.T @ (A64 @ x64)) + d * x64
+
+
+@pytest.mark.parametrize("M,N", [(7, 256), (300, 4096), (1000, 8192), (513, 12288), (64, 40000), (260, 65536),
+                                 (2048, 65536)])
+def test_dense_normal_vs_fp64(M, N):
+    rng = np.random.default_rng(M + N)
+    A = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float32)
+    x = rng.standard_normal(N).astype(np.float32)
+    Ad, xd = to_device(A), to_device(x)
+    assert _dev.dense_normal_supported(Ad, xd)
+    y1 = _dev.dense_normal(Ad, xd, 0.7, 1.3)
+    y2 = _dev.dense_normal(Ad, xd, 0.7, 1.3)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)  # fixed partition and summation order
+    assert rel_err(to_NUMPY(y1), _ref(A, x, 0.7, 1.3)) <= 1e-5
+
+
+def test_dense_normal_refuses_unsupported():
+    A = to_device(np.ones((8, 10), np.float32))  # N % 4 != 0
+    x = to_device(np.ones(10, np.float32))
+    assert not _dev.dense_normal_supported(A, x)
+    A64 = to_device(np.ones((8, 16), np.float64))
+    assert not _dev.dense_normal_supported(A64, to_device(np.ones(16, np.float64)))
+    A2 = to_device(np.ones((8, 16), np.float32))
+    assert not _dev.dense_normal_supported(A2, to_device(np.ones((2, 16), np.float32)))  # stacked rhs
+
+
+def _admm_cg_operator(K, M, tau, w=0.5):
+    f = w * pxo.SquaredL2Norm(dim=M).asloss(to_device(np.zeros(M, np.float32))) * K
+    Q, _, _ = f._quad_spec()
+    return Q + pxo.HomothetyOp(cst=1 / tau, dim=Q.dim)
+
+
+@pytest.mark.parametrize("w,tau", [(0.5, 1.0), (0.5, 0.25), (2.0, 3.0)])
+def test_normal_form_of_admm_operator(w, tau):
+    rng = np.random.default_rng(1)
+    M, N = 24, 64
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        K = pxa.LinOp.from_array(to_device(rng.standard_normal((M, N)).astype(np.float32)))
+        A = _admm_cg_operator(K, M, tau, w)
+        nf = normal_form(A)
+        assert nf is not None
+        mat, s, d = nf
+        assert mat is K._mat
+        assert np.isclose(s, 2 * w) and np.isclose(d, 1 / tau)
+        p = to_device(rng.standard_normal(N).astype(np.float32))
+        assert rel_err(to_NUMPY(_dev.dense_normal(mat, p, s, d)), to_NUMPY(A.apply(p))) <= 1e-5
+
+
+def test_normal_form_rejects_other_operators():
+    rng = np.random.default_rng(2)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        K = pxa.LinOp.from_array(to_device(rng.standard_normal((12, 16)).astype(np.float32)))
+        K2 = pxa.LinOp.from_array(to_device(rng.standard_normal((12, 16)).astype(np.float32)))
+        assert normal_form(K) is None  # not a normal operator
+        assert normal_form(K.T * K2) is None  # two different matrices
+        assert normal_form(K.T * K + K2.T * K2) is None
+        G = pxo.Gradient(arg_shape=(4, 4))
+        assert normal_form(G.T * G) is None  # not a dense matrix
+        nf = normal_form(K.T * K)
+        assert nf is not None and nf[1] == 1.0 and nf[2] == 0.0
+
+
+@pytest.mark.parametrize("M,N", [(48, 160), (256, 2048)])
+def test_admm_fused_normal_matches_generic_and_oracle(M, N):
+    """ADMM C4-style: f = 1/2||K . - y||^2, h = lam L1, x-update = QuadraticFunc.prox -> CG.  The fused
+    operator (one pass over K) gives the trajectory of the rule-by-rule operator within fp32 rounding,
+    and both follow the fp64 oracle (oracle.admm_dense_l1 restating pds.py:1631-1660 + cg.py:125-153)."""
+    rng = np.random.default_rng(M)
+    A = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float32)
+    xs = np.zeros(N, np.float32)
+    xs[rng.choice(N, 8, replace=False)] = rng.standard_normal(8).astype(np.float32)
+    y = (A @ xs + 0.01 * rng.standard_normal(M)).astype(np.float32)
+    lam, tau, iters = 0.05, 1.0, 6
+    out = {}
+    import pyxu_amd.opt.solver.cg as cgm
+
+    for fused in (True, False):
+        saved = cgm.normal_form
+        if not fused:
+            cgm.normal_form = lambda op: None
+        try:
+            with pxrt.Precision(pxrt.Width.SINGLE):
+                K = pxa.LinOp.from_array(to_device(A))
+                f = 0.5 * pxo.SquaredL2Norm(dim=M).asloss(to_device(y)) * K
+                h = lam * pxo.L1Norm(dim=N)
+                s = pxs.ADMM(f=f, h=h, show_progress=False)
+                s.fit(x0=to_device(np.zeros(N, np.float32)), tau=tau, stop_crit=pxst.MaxIter(iters))
+                out[fused] = to_NUMPY(s.solution())
+        finally:
+            cgm.normal_form = saved
+    assert rel_err(out[True], out[False]) <= 1e-5
+    xr, ur, _, _ = orc.admm_dense_l1(A.astype(np.float64), y.astype(np.float64), lam, np.zeros(N), tau, iters)
+    assert rel_err(out[True], xr) <= 1e-4  # solution() = x (primal), fp32 vs the fp64 oracle
+
+
+def test_cg_published_residual_stat_gives_same_stop_decisions():
+    """The inline CG (QuadraticFunc.prox) hands its ||r||^2 to AbsError: same iterations and iterate as
+    a CG whose stop criterion recomputes the norm itself."""
+    rng = np.random.default_rng(3)
+    M, N = 64, 256
+    A = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        K = pxa.LinOp.from_array(to_device(A))
+        Aop = K.T * K + pxo.HomothetyOp(cst=1.0, dim=N)
+        res = {}
+        for internal in (True, False):
+            s = pxs.CG(A=Aop, show_progress=False, _internal=internal)
+            crit = s.default_stop_crit() | pxst.MaxIter(2 * N)
+            if internal:
+                s._solve_inline(b=to_device(b), stop_crit=crit)
+            else:
+                s.fit(b=to_device(b), stop_crit=crit)
+            res[internal] = (s._astate["idx"], to_NUMPY(s.solution()))
+    assert res[True][0] == res[False][0]
+    assert np.array_equal(res[True][1], res[False][1])
