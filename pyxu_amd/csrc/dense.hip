@@ -11,6 +11,16 @@ namespace {
 
 constexpr int kBC = 8;  // stacked right-hand sides per register chunk
 
+// 16-B load of A, which every GEMV reads exactly once: non-temporal (streaming) policy, so the matrix
+// stream does not evict the re-read vectors (x, 256 KB at N = 65536) from the XCD's 4 MB L2.
+template <typename T>
+__device__ inline void ld_stream_vec(const T* p, T (&v)[kVecN<T>]) {
+  typedef T vt __attribute__((ext_vector_type(kVecN<T>)));
+  const vt r = __builtin_nontemporal_load(reinterpret_cast<const vt*>(p));
+#pragma unroll
+  for (int i = 0; i < kVecN<T>; ++i) v[i] = r[i];
+}
+
 // ------------------------------------------------------------------ apply: Y[b, m] = <A[m,:], X[b,:]>
 template <typename T>
 __global__ void __launch_bounds__(kBlock) gemv_rows_kernel(int64_t M, int64_t N, int64_t B, int64_t b0, int nb,
@@ -33,7 +43,7 @@ __global__ void __launch_bounds__(kBlock) gemv_rows_kernel(int64_t M, int64_t N,
       for (; k + (kU - 1) * 64 * V < N; k += kU * 64 * V) {
         T av[kU][V];
 #pragma unroll
-        for (int q = 0; q < kU; ++q) *reinterpret_cast<VT*>(av[q]) = *reinterpret_cast<const VT*>(a + k + q * 64 * V);
+        for (int q = 0; q < kU; ++q) ld_stream_vec<T>(a + k + q * 64 * V, av[q]);  // A read once: streaming policy
 #pragma unroll
         for (int q = 0; q < kU; ++q) {
 #pragma unroll
@@ -51,7 +61,7 @@ __global__ void __launch_bounds__(kBlock) gemv_rows_kernel(int64_t M, int64_t N,
       }
       for (; k < N; k += 64 * V) {
         T av[V];
-        *reinterpret_cast<VT*>(av) = *reinterpret_cast<const VT*>(a + k);
+        ld_stream_vec<T>(a + k, av);
 #pragma unroll
         for (int j = 0; j < kBC; ++j) {
           if (j < nb) {
@@ -105,7 +115,7 @@ __global__ void __launch_bounds__(kBlock) gemv_cols_partial_kernel(int64_t M, in
   for (int64_t m = m_lo; m < m_hi; ++m) {
     T av[V];
     if (vec && n0 + V <= N) {
-      *reinterpret_cast<VT*>(av) = *reinterpret_cast<const VT*>(A + m * N + n0);
+      ld_stream_vec<T>(A + m * N + n0, av);
     } else {
 #pragma unroll
       for (int v = 0; v < V; ++v) av[v] = (n0 + v < N) ? A[m * N + n0 + v] : T(0);
