@@ -100,7 +100,6 @@ __global__ void __launch_bounds__(kBlock) gemv_cols_partial_kernel(int64_t M, in
                                                                    const T* __restrict__ A, const T* __restrict__ X,
                                                                    T* __restrict__ part, bool vec) {
   constexpr int V = kVecN<T>;
-  using VT = typename Vec4<T>::type;
   const int64_t chunk = blockIdx.y;
   const int64_t m_lo = chunk * kRowChunk;
   const int64_t m_hi = m_lo + kRowChunk < M ? m_lo + kRowChunk : M;

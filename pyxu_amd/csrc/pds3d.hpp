@@ -309,12 +309,11 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
     }
   }
   __syncthreads();
-  // ---- pass B: G2 along rows, then the solver's point-wise update
+  // ---- pass B: G2 along rows; results parked in LDS (the PT region, free once every sweep is done)
   constexpr int KB = cdiv(L::NPB, kThreads);
   const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n2 - R);
-  const int64_t hoff = ((s % g.y_images) * g.n0 + plane) * M;
-  const int a_first = 3 - g.D;
-  const T one = T(1), mtau = -p.tau;
+  using S = Stage<T, R>;
+  T st[KB][V][CW];
 #pragma unroll
   for (int k = 0; k < KB; ++k) {
     const int it = tid + k * kThreads;
@@ -326,97 +325,122 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
       sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g2, acc);
       if (edge_cols) ghost_fix<T, R, CW, L::PTP>(tx0 + c0, n2, tx0 - CA, PT + V * a, p.k2, KT + kKT, acc);
 #pragma unroll
+      for (int uu = 0; uu < V; ++uu)
+#pragma unroll
+        for (int w = 0; w < CW; ++w) st[k][uu][w] = acc[w][uu];
+    }
+  }
+  __syncthreads();  // every G2 sweep is done with PT: O may overwrite it
+  T* O = PT;
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int it = tid + k * kThreads;
+    if (it < L::NPB) {
+      int a, cb;
+      L::pass_b_item(it, a, cb);
+#pragma unroll
       for (int uu = 0; uu < V; ++uu) {
-        const int gr = ty0 + V * a + uu, gc = tx0 + c0;
-        if (EDGE && gr >= n1) continue;
-        const int64_t off = img * M + (int64_t)gr * n2 + gc;  // voxel offset in x / u / w / out
-        const int64_t bo = hoff + (int64_t)gr * n2 + gc;
-        bool ok[CW];
+        T* o = O + (V * a + uu) * S::OP + CW * cb;
 #pragma unroll
-        for (int w = 0; w < CW; ++w) ok[w] = !EDGE || gc + w < n2;
-        auto ld = [&](const void* base, int64_t o, T(&v)[CW]) {
-          const T* b = (const T*)base + o;
-          if constexpr (CW == 2) {
-            if (!EDGE || (ok[1] && p.vec_ok)) {
-              ld_pair<T>(b, v);
-              return;
-            }
-          }
-#pragma unroll
-          for (int w = 0; w < CW; ++w) v[w] = ok[w] ? b[w] : T(0);
-        };
-        auto st = [&](void* base, int64_t o, const T(&v)[CW]) {
-          T* b = (T*)base + o;
-          if constexpr (CW == 2) {
-            if (!EDGE || (ok[1] && p.vec_ok)) {
-              if constexpr (sizeof(T) == 4) *reinterpret_cast<float2*>(b) = make_float2(v[0], v[1]);
-              return;
-            }
-          }
-#pragma unroll
-          for (int w = 0; w < CW; ++w)
-            if (ok[w]) b[w] = v[w];
-        };
-        T xv[CW], bv[CW], wv[CW], ov[CW];
-        ld(P.x, off, xv);
-        ld(P.hty, bo, bv);
-        if constexpr (PD3O) {
-          T uv[CW];
-          ld(P.u, off, uv);
-#pragma unroll
-          for (int w = 0; w < CW; ++w) {
-            const T gf = acc[w][uu] - bv[w];          // grad f(x) = G x - S^T y
-            const T ut = one * xv[w] + mtau * gf;      // u_tmp = x - tau grad f(x)
-            wv[w] = one * xv[w] + one * ut + (-one) * uv[w];  // x + u_tmp - u
-            ov[w] = p.omr * uv[w] + p.rho * ut;       // (1 - rho) u + rho u_tmp
-          }
-        } else {
-          // K^T z at the item's pixels: sum over directions of c1 z_d[i - e_a] + c0 z_d[i]
-          T kt[CW];
-#pragma unroll
-          for (int ax = 0; ax < 3; ++ax) {
-            if (ax < a_first) continue;
-            const int64_t zo = (s * g.D + (ax - a_first)) * N + (int64_t)plane * M + (int64_t)gr * n2 + gc;
-            T zc[CW], zm[CW];
-            ld(P.z, zo, zc);
-            if (ax == 0) {
-              if (plane > 0) {
-                ld(P.z, zo - M, zm);
-              } else {
-#pragma unroll
-                for (int w = 0; w < CW; ++w) zm[w] = T(0);
-              }
-            } else if (ax == 1) {
-              if (gr > 0) {
-                ld(P.z, zo - n2, zm);
-              } else {
-#pragma unroll
-                for (int w = 0; w < CW; ++w) zm[w] = T(0);
-              }
-            } else {
-              zm[0] = gc > 0 ? ((const T*)P.z)[zo - 1] : T(0);
-              if constexpr (CW == 2) zm[1] = zc[0];
-            }
-#pragma unroll
-            for (int w = 0; w < CW; ++w) {
-              const T term = g.c1[ax] * zm[w] + g.c0[ax] * zc[w];
-              kt[w] = (ax == a_first) ? term : kt[w] + term;
-            }
-          }
-#pragma unroll
-          for (int w = 0; w < CW; ++w) {
-            const T gf = acc[w][uu] - bv[w];
-            T t = one * xv[w] + mtau * gf;  // x - tau grad f(x)
-            t = one * t + mtau * kt[w];     // - tau K^T z
-            const T xt = apply_prox<T>(p.prox, t, p.pw);
-            wv[w] = T(2) * xt + (-one) * xv[w];   // 2 x_tmp - x
-            ov[w] = p.rho * xt + p.omr * xv[w];  // rho x_tmp + (1 - rho) x
-          }
-        }
-        st(P.w, off, wv);
-        st(P.out, off, ov);
+        for (int w = 0; w < CW; ++w) o[w] = st[k][uu][w];
       }
     }
+  }
+  __syncthreads();
+  // ---- epilogue in row-major order: each V-vector of a tile row is one lane (full 128-B lines for
+  // every stream: x, S^T y, u or z, w, out), the solver's point-wise update per element
+  const int64_t hoff = ((s % g.y_images) * g.n0 + plane) * M;
+  const int a_first = 3 - g.D;
+  const T one = T(1), mtau = -p.tau;
+  const int cq = tid % S::LPR, r0 = tid / S::LPR;
+  constexpr int NS = TY / S::RPS;
+#pragma unroll
+  for (int si = 0; si < NS; ++si) {
+    const int r = r0 + si * S::RPS;
+    const int gr = ty0 + r, gc = tx0 + V * cq;
+    if (EDGE && (gr >= n1 || gc >= n2)) continue;
+    const bool full = !EDGE || (p.vec_ok && gc + V <= n2);
+    const int64_t off = img * M + (int64_t)gr * n2 + gc;  // voxel offset in x / u / w / out
+    const int64_t bo = hoff + (int64_t)gr * n2 + gc;
+    auto ld = [&](const void* base, int64_t o, T(&v)[V]) {
+      const T* b = (const T*)base + o;
+      if (full) {
+        ld_vec<T, V>(b, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] = gc + e < n2 ? b[e] : T(0);
+      }
+    };
+    auto stv = [&](void* base, int64_t o, const T(&v)[V]) {
+      T* b = (T*)base + o;
+      if (full) {
+        st_vec<T, V>(b, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (gc + e < n2) b[e] = v[e];
+      }
+    };
+    T gv[V], xv[V], bv[V], wv[V], ov[V];
+    ld_vec<T, V>(O + r * S::OP + V * cq, gv);
+    ld(P.x, off, xv);
+    ld(P.hty, bo, bv);
+    if constexpr (PD3O) {
+      T uv[V];
+      ld(P.u, off, uv);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const T gf = gv[e] - bv[e];                        // grad f(x) = G x - S^T y
+        const T ut = one * xv[e] + mtau * gf;              // u_tmp = x - tau grad f(x)
+        wv[e] = one * xv[e] + one * ut + (-one) * uv[e];  // x + u_tmp - u
+        ov[e] = p.omr * uv[e] + p.rho * ut;               // (1 - rho) u + rho u_tmp
+      }
+    } else {
+      // K^T z at the lane's pixels: sum over directions of c1 z_d[i - e_a] + c0 z_d[i]
+      T kt[V];
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        if (ax < a_first) continue;
+        const int64_t zo = (s * g.D + (ax - a_first)) * N + (int64_t)plane * M + (int64_t)gr * n2 + gc;
+        T zc[V], zm[V];
+        ld(P.z, zo, zc);
+        if (ax == 0) {
+          if (plane > 0) {
+            ld(P.z, zo - M, zm);
+          } else {
+#pragma unroll
+            for (int e = 0; e < V; ++e) zm[e] = T(0);
+          }
+        } else if (ax == 1) {
+          if (gr > 0) {
+            ld(P.z, zo - n2, zm);
+          } else {
+#pragma unroll
+            for (int e = 0; e < V; ++e) zm[e] = T(0);
+          }
+        } else {
+          zm[0] = gc > 0 ? ((const T*)P.z)[zo - 1] : T(0);
+#pragma unroll
+          for (int e = 1; e < V; ++e) zm[e] = zc[e - 1];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const T term = g.c1[ax] * zm[e] + g.c0[ax] * zc[e];
+          kt[e] = (ax == a_first) ? term : kt[e] + term;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const T gf = gv[e] - bv[e];
+        T t = one * xv[e] + mtau * gf;  // x - tau grad f(x)
+        t = one * t + mtau * kt[e];     // - tau K^T z
+        const T xt = apply_prox<T>(p.prox, t, p.pw);
+        wv[e] = T(2) * xt + (-one) * xv[e];   // 2 x_tmp - x
+        ov[e] = p.rho * xt + p.omr * xv[e];  // rho x_tmp + (1 - rho) x
+      }
+    }
+    stv(P.w, off, wv);
+    stv(P.out, off, ov);
   }
 }
 

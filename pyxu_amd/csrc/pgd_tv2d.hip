@@ -314,16 +314,6 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
 // each 16-B vector of a row is one lane (16 lanes per fp32 row), so H^T y / x loads and x_new stores
 // are full 128-B lines instead of the pass-B item order's 64-B row pieces (measured on MI355X: a
 // 2048^2 fp32 store in the item order 7.2 us, row-major 5.2 us).  yk comes from A.
-template <typename T, int R>
-struct Stage {
-  using L = Layout<T, R>;
-  static constexpr int V = L::V;
-  static constexpr int OP = sizeof(T) == 4 ? TX + 4 : TX + 2;  // conflict-free item-order writes (fp32)
-  static constexpr int LPR = TX / V;                           // lanes per tile row
-  static constexpr int RPS = kThreads / LPR;                   // rows per sweep
-  static_assert(TY * OP <= L::AC * L::PTP, "O must fit in the PT region");
-};
-
 template <typename T, int R, bool EDGE>
 __device__ inline void epilogue_staged(const PgdParams<T>& p, const T* A, const T* O, int ty0, int tx0,
                                        const T* __restrict__ bs, const T* __restrict__ xs, T* __restrict__ xns,

@@ -184,6 +184,21 @@ __device__ inline void ld_pair(const T* __restrict__ p, T (&v)[2]) {
   }
 }
 
+// Staged epilogue geometry: pass B parks its results in O (the PT region, free once all G sweeps are
+// done), then the workgroup finishes the tile in row-major order, each 16-B vector of a tile row one
+// lane (16 lanes per fp32 row): the global loads / stores of the epilogue are full 128-B lines instead
+// of the pass-B item order's 64-B row pieces (measured on MI355X: a 2048^2 fp32 store in the item order
+// 7.2 us, row-major 5.2 us).
+template <typename T, int R>
+struct Stage {
+  using L = Layout<T, R>;
+  static constexpr int V = L::V;
+  static constexpr int OP = sizeof(T) == 4 ? TX + 4 : TX + 2;  // conflict-free item-order writes (fp32)
+  static constexpr int LPR = TX / V;                           // lanes per tile row
+  static constexpr int RPS = kThreads / LPR;                   // rows per sweep
+  static_assert(TY * OP <= L::AC * L::PTP, "O must fit in the PT region");
+};
+
 // XCD-aware tile order (speed only): XCD group g = blockIdx % 8 owns a contiguous band of tiles.
 __device__ inline unsigned xcd_tile(unsigned bid, unsigned nb) {
   const unsigned q8 = nb >> 3, r8 = nb & 7u, g8 = bid & 7u;
