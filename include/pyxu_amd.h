@@ -366,11 +366,17 @@ int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, in
  *   inverse = 0: apply   = fftn(x, axes, norm="backward")  (exp(-2 pi i jk/n), unnormalised)
  *   inverse = 1: adjoint = ifftn(x, axes, norm="forward")  (exp(+2 pi i jk/n), unnormalised)
  * `out` may alias `in`.  Lengths whose prime factors are in {2, 3, 5, 7} run a mixed-radix Stockham
- * FFT in LDS (n <= 4096 in fp32, 2048 in fp64); other lengths an exact DFT (n <= 2048);
- * PXA_ERR_UNSUPPORTED beyond that.
+ * FFT in LDS (n <= 10240 in fp32, 5120 in fp64); other lengths up to 2048 an exact DFT in LDS.  Every
+ * other length (like the reference's scipy.fft) needs a workspace: longer smooth lengths run a
+ * four-step split n = n1 n2, the rest Bluestein's chirp-z on a 2^k-point FFT.  pxa_fft (no workspace)
+ * returns PXA_ERR_UNSUPPORTED for those; pxa_fft_ex takes `work` of pxa_fft_workspace_bytes(...)
+ * bytes (0: none needed; (size_t)-1: unsupported arguments).
  * ------------------------------------------------------------------------------------------- */
 int pxa_fft(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse,
             const void* in, void* out, void* stream);
+size_t pxa_fft_workspace_bytes(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack);
+int pxa_fft_ex(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse,
+               const void* in, void* out, void* work, void* stream);
 /* out[i] = a[i] * b[i % nb] over n complex elements (b conjugated if conj_b): the spectrum product of
  * the FFT path of large zero-boundary stencils (Stencil.apply/adjoint, stencil.py:441-461). */
 int pxa_complex_mul(int dtype, int64_t n, int64_t nb, const void* a, const void* b, int conj_b, void* out,

@@ -760,10 +760,16 @@ def fft(z, shape, axes, stack, inverse, out=None):
     """Unnormalised DFT over `axes` of `stack` complex arrays of `shape`, interleaved (re, im) real
     tensors (pxa_fft).  inverse=False: exp(-2 pi i ..) (fftn, norm="backward"); True: exp(+..)
     (ifftn, norm="forward")."""
+    torch = _torch()
     z = require(z, "z")
     out = empty_like(z) if out is None else out
-    check(lib.pxa_fft(dtcode(z), len(shape), i64_array(shape), len(axes), int_array(axes), int(stack), int(bool(inverse)),
-                      ptr(z), ptr(out), stream()), "pxa_fft")
+    sh, ax = i64_array(shape), int_array(axes)
+    wsz = int(lib.pxa_fft_workspace_bytes(dtcode(z), len(shape), sh, len(axes), ax, int(stack)))
+    if wsz == (1 << 64) - 1:  # (size_t)-1: arguments outside the envelope
+        check(-3, "pxa_fft_workspace_bytes")  # PXA_ERR_UNSUPPORTED
+    work = torch.empty((wsz,), dtype=torch.uint8, device=z.device) if wsz > 0 else None
+    check(lib.pxa_fft_ex(dtcode(z), len(shape), sh, len(axes), ax, int(stack), int(bool(inverse)), ptr(z), ptr(out),
+                         ptr(work) if work is not None else None, stream()), "pxa_fft_ex")
     return out
 
 

@@ -78,6 +78,8 @@ EXPORTS = {
          vp, vp, vp, vp, vp, vp],
     ),
     "pxa_fft": (i32, [i32, i32, P_i64, i32, P_int, i64, i32, vp, vp, vp]),
+    "pxa_fft_workspace_bytes": (sz, [i32, i32, P_i64, i32, P_int, i64]),
+    "pxa_fft_ex": (i32, [i32, i32, P_i64, i32, P_int, i64, i32, vp, vp, vp, vp]),
     "pxa_complex_mul": (i32, [i32, i64, i64, vp, vp, i32, vp, vp]),
     "pxa_real_to_complex": (i32, [i32, i64, vp, vp, vp]),
     "pxa_complex_real_part": (i32, [i32, i64, vp, vp, vp]),

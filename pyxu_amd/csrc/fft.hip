@@ -11,6 +11,10 @@
 // coalesced across lines; the contiguous axis reads whole lines.  Lengths with a prime factor > 7 use
 // an exact O(n^2) DFT of the LDS-resident line (twiddle index j k mod n in integers).
 // Twiddles: sincospi of an exact rational (2 r k / (Ns R)), fp32 or fp64 like the data.
+// Lines longer than LDS holds: smooth lengths by the four-step split n = n1 n2 (n1-point DFTs along
+// the stride-n2 axis, twiddles w_n^(k1 j2), n2-point DFTs stored transposed into a workspace, copied
+// back); other lengths by Bluestein's chirp-z (chirp, 2^k-point FFT convolution with the chirp filter,
+// chirp), so every length runs, as in the reference's scipy.fft.
 #include "common.hpp"
 
 namespace pxa {
@@ -121,10 +125,20 @@ __device__ inline void dft_odd(Cx<T>* v) {
 
 struct FftPlan {
   int64_t n, inner, lines;  // axis length, stride of the axis (elements), number of lines
-  int lpb;                   // lines per workgroup
+  int64_t tn1;              // 0: results back in place of the line; > 0: four-step transposed store (below)
+  int lpb;                  // lines per workgroup
   int nst;
   int radix[kMaxStages];
 };
+
+// Four-step transposed store: the line (o, k1, i) of an (outer, tn1, n, inner) view writes its element
+// k2 to (o, k2, k1, i) of the (outer, n, tn1, inner) view, i.e. offset (o n tn1 + k2 tn1 + k1) inner + i.
+__device__ inline int64_t tstore_offset(int64_t line, int64_t m, const FftPlan& p) {
+  const int64_t per = p.tn1 * p.inner;
+  const int64_t o = line / per, rem = line - o * per;
+  const int64_t k1 = rem / p.inner, i = rem - k1 * p.inner;
+  return (o * p.n * p.tn1 + m * p.tn1 + k1) * p.inner + i;
+}
 
 __device__ inline int64_t line_base(int64_t line, int64_t n, int64_t inner) {
   const int64_t o = line / inner;
@@ -165,6 +179,13 @@ __device__ inline void stage(const Cx<T>* src, Cx<T>* dst, int n, int ns, int lp
 template <typename T>
 __device__ inline void move_lines(const FftPlan& p, int64_t line0, int nl, const Cx<T>* g, Cx<T>* lds, bool to_lds) {
   const int n = (int)p.n;
+  if (!to_lds && p.tn1 > 0) {  // transposed store: adjacent lines land in adjacent elements
+    for (int i = threadIdx.x; i < nl * n; i += kFftThreads) {
+      const int m = i / nl, l = i - m * nl;
+      const_cast<Cx<T>*>(g)[tstore_offset(line0 + l, m, p)] = lds[l * n + m];
+    }
+    return;
+  }
   if (p.inner == 1) {  // contiguous axis: the lines are consecutive blocks
     Cx<T>* gl = const_cast<Cx<T>*>(g) + line0 * n;
     for (int i = threadIdx.x; i < nl * n; i += kFftThreads) {
@@ -237,6 +258,18 @@ __global__ void __launch_bounds__(kFftThreads) fft_direct_kernel(FftPlan p, cons
   move_lines<T>(p, line, 1, dst, x, false);
 }
 
+// out[i] = a[i] * b[i % nb] (b conjugated if CONJ): spectrum product of an FFT convolution
+template <typename T, bool CONJ>
+__global__ void __launch_bounds__(kBlock) cmul_kernel(int64_t n, int64_t nb, const Cx<T>* __restrict__ a,
+                                                      const Cx<T>* __restrict__ b, Cx<T>* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    Cx<T> w = b[i % nb];
+    if (CONJ) w.im = -w.im;
+    out[i] = cmul(a[i], w);
+  }
+}
+
 bool factor(int64_t n, FftPlan& p) {
   p.nst = 0;
   for (int r : {8, 4, 2, 3, 5, 7}) {
@@ -249,55 +282,276 @@ bool factor(int64_t n, FftPlan& p) {
   return n == 1;
 }
 
+bool smooth(int64_t n) {
+  for (int r : {2, 3, 5, 7})
+    while (n % r == 0) n /= r;
+  return n == 1;
+}
+
+// One workgroup may take the whole LDS for a single long line; several lines per workgroup share 64 KB
+// (two workgroups per CU).
+constexpr size_t kFftLdsMax = 160 * 1024;
+constexpr int64_t kDirectMaxN = 8 * kFftThreads;
+
 template <typename T>
-int fft_entry(int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse, const void* in,
-              void* out, hipStream_t st) {
+bool stockham_fits(int64_t n) {
+  return smooth(n) && 2 * (size_t)n * sizeof(Cx<T>) <= kFftLdsMax;
+}
+template <typename T>
+bool direct_fits(int64_t n) {
+  return n <= kDirectMaxN && (size_t)n * sizeof(Cx<T>) <= kFftLdsMax;
+}
+// four-step split n = n1 n2 with both factors Stockham-resident, n1 the largest such divisor <= sqrt(n)
+template <typename T>
+int64_t four_step_n1(int64_t n) {
+  if (!smooth(n)) return 0;
+  for (int64_t n1 = (int64_t)sqrt((double)n) + 1; n1 >= 2; --n1)
+    if (n % n1 == 0 && n1 * n1 <= n && stockham_fits<T>(n1) && stockham_fits<T>(n / n1)) return n1;
+  return 0;
+}
+int64_t next_pow2(int64_t v) {
+  int64_t m = 1;
+  while (m < v) m <<= 1;
+  return m;
+}
+
+// Workspace (complex elements) of one axis transform of `lines` lines of length n; -1: unsupported.
+template <typename T>
+int64_t axis_work(int64_t n, int64_t lines) {
+  if (n == 1 || stockham_fits<T>(n) || (!smooth(n) && direct_fits<T>(n))) return 0;
+  if (smooth(n)) return four_step_n1<T>(n) ? n * lines : -1;
+  const int64_t m = next_pow2(2 * n - 1);  // Bluestein: a (lines x m), b (m), then the FFT_m's own
+  const int64_t inner = axis_work<T>(m, lines);
+  return inner < 0 ? -1 : lines * m + m + inner;
+}
+
+template <typename T>
+int launch_stockham(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_t st) {
+  if (!factor(p.n, p)) return PXA_ERR_UNSUPPORTED;
+  const size_t line_bytes = (size_t)p.n * sizeof(Cx<T>);
+  int lpb = (int)(kFftLds / (2 * line_bytes));
+  if (lpb > 16) lpb = 16;
+  if (lpb < 1) lpb = 1;
+  if (p.inner > 1 && lpb > p.inner) lpb = (int)p.inner;
+  p.lpb = lpb;
+  const int64_t blocks = (p.lines + lpb - 1) / lpb;
+  PXA_CHECK_ARG(blocks <= 0x7fffffff);
+  const size_t smem = 2 * (size_t)lpb * line_bytes;
+  if (smem > kFftLdsMax) return PXA_ERR_UNSUPPORTED;
+  static bool attr = false;  // the dynamic-LDS ceiling is a property of the kernel: set once
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fft_stockham_kernel<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFftLdsMax);
+    (void)hipFuncSetAttribute((const void*)fft_stockham_kernel<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFftLdsMax);
+    attr = true;
+  }
+  auto kern = inv ? fft_stockham_kernel<T, true> : fft_stockham_kernel<T, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kFftThreads), smem, st, p, src, dst);
+  return last_launch_status();
+}
+
+template <typename T>
+int launch_direct(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_t st) {
+  PXA_CHECK_ARG(p.lines <= 0x7fffffff);
+  p.lpb = 1;
+  const size_t line_bytes = (size_t)p.n * sizeof(Cx<T>);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fft_direct_kernel<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFftLdsMax);
+    (void)hipFuncSetAttribute((const void*)fft_direct_kernel<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFftLdsMax);
+    attr = true;
+  }
+  auto kern = inv ? fft_direct_kernel<T, true> : fft_direct_kernel<T, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)p.lines), dim3(kFftThreads), line_bytes, st, p, src, dst);
+  return last_launch_status();
+}
+
+// four-step twiddle: element (o, k1, j2, i) of the (outer, n1, n2, inner) view times w_n^(k1 j2)
+template <typename T, bool INV>
+__global__ void __launch_bounds__(kBlock) four_step_twiddle_kernel(int64_t total, int64_t n1, int64_t n2,
+                                                                   int64_t inner, Cx<T>* __restrict__ z) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n = n1 * n2;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    int64_t t = e / inner;
+    const int64_t j2 = t % n2;
+    t /= n2;
+    const int64_t k1 = t % n1;
+    const int64_t q = (k1 * j2) % n;
+    if (q != 0) {
+      T sn, c;
+      sc_pi((T)(2 * q) / (T)n, &sn, &c);
+      z[e] = cmul(z[e], Cx<T>{c, INV ? sn : -sn});
+    }
+  }
+}
+
+// Bluestein chirp w(j) = exp(-+ i pi j^2 / n) (exact rational phase: j^2 mod 2n)
+template <typename T, bool INV>
+__device__ inline Cx<T> chirp(int64_t j, int64_t n) {
+  const int64_t q = (j * j) % (2 * n);
+  T sn, c;
+  sc_pi((T)q / (T)n, &sn, &c);
+  return Cx<T>{c, INV ? sn : -sn};
+}
+
+// a[l][j] = src(l, j) w(j) for j < n, 0 for n <= j < m (lines gathered from any axis stride)
+template <typename T, bool INV>
+__global__ void __launch_bounds__(kBlock) bluestein_in_kernel(int64_t lines, int64_t n, int64_t inner, int64_t m,
+                                                              const Cx<T>* __restrict__ src, Cx<T>* __restrict__ a) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < lines * m; e += stride) {
+    const int64_t l = e / m, j = e - l * m;
+    a[e] = j < n ? cmul(src[line_base(l, n, inner) + j * inner], chirp<T, INV>(j, n)) : Cx<T>{T(0), T(0)};
+  }
+}
+
+// b[j] = conj w(d), d = j (j < n) or m - j (j > m - n), else 0: the circular chirp filter
+template <typename T, bool INV>
+__global__ void __launch_bounds__(kBlock) bluestein_filter_kernel(int64_t n, int64_t m, Cx<T>* __restrict__ b) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
+    const int64_t d = j < n ? j : (j > m - n ? m - j : -1);
+    b[j] = d < 0 ? Cx<T>{T(0), T(0)} : chirp<T, !INV>(d, n);
+  }
+}
+
+// dst(l, k) = a[l][k] w(k) / m
+template <typename T, bool INV>
+__global__ void __launch_bounds__(kBlock) bluestein_out_kernel(int64_t lines, int64_t n, int64_t inner, int64_t m,
+                                                               const Cx<T>* __restrict__ a, Cx<T>* dst) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const T inv_m = T(1) / (T)m;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < lines * n; e += stride) {
+    const int64_t l = e / n, k = e - l * n;
+    const Cx<T> v = cmul(a[l * m + k], chirp<T, INV>(k, n));
+    dst[line_base(l, n, inner) + k * inner] = Cx<T>{v.re * inv_m, v.im * inv_m};
+  }
+}
+
+// DFT of `lines` lines of length n and element stride `inner` (line l at line_base(l, n, inner)),
+// src -> dst (may alias).  work: axis_work<T>(n, lines) complex elements.
+template <typename T>
+int fft_axis(int64_t n, int64_t inner, int64_t lines, bool inv, const Cx<T>* src, Cx<T>* dst, Cx<T>* work,
+             hipStream_t st) {
+  FftPlan p;
+  p.n = n;
+  p.inner = inner;
+  p.lines = lines;
+  p.tn1 = 0;
+  if (stockham_fits<T>(n)) return launch_stockham<T>(p, inv, src, dst, st);
+  if (!smooth(n) && direct_fits<T>(n)) return launch_direct<T>(p, inv, src, dst, st);
+  if (axis_work<T>(n, lines) < 0) return PXA_ERR_UNSUPPORTED;
+  if (work == nullptr) return PXA_ERR_ARG;
+  const int64_t total = n * lines;
+  if (smooth(n)) {  // four-step: n1-point DFTs, twiddles, n2-point DFTs stored transposed, copy back
+    const int64_t n1 = four_step_n1<T>(n), n2 = n / n1;
+    FftPlan p1 = p;
+    p1.n = n1;
+    p1.inner = n2 * inner;
+    p1.lines = total / n1;
+    int e = launch_stockham<T>(p1, inv, src, dst, st);
+    if (e) return e;
+    if (inv)
+      hipLaunchKernelGGL((four_step_twiddle_kernel<T, true>), dim3(grid_for(total)), dim3(kBlock), 0, st, total, n1,
+                         n2, inner, dst);
+    else
+      hipLaunchKernelGGL((four_step_twiddle_kernel<T, false>), dim3(grid_for(total)), dim3(kBlock), 0, st, total, n1,
+                         n2, inner, dst);
+    e = last_launch_status();
+    if (e) return e;
+    FftPlan p2 = p;
+    p2.n = n2;
+    p2.inner = inner;
+    p2.lines = total / n2;
+    p2.tn1 = n1;
+    e = launch_stockham<T>(p2, inv, dst, work, st);
+    if (e) return e;
+    return (int)hipMemcpyAsync(dst, work, (size_t)total * sizeof(Cx<T>), hipMemcpyDeviceToDevice, st);
+  }
+  // Bluestein: chirp, m-point FFT convolution with the chirp filter (m = 2^k >= 2n - 1), chirp
+  const int64_t m = next_pow2(2 * n - 1);
+  Cx<T>* a = work;
+  Cx<T>* b = a + lines * m;
+  Cx<T>* w2 = b + m;
+  if (inv) {
+    hipLaunchKernelGGL((bluestein_in_kernel<T, true>), dim3(grid_for(lines * m)), dim3(kBlock), 0, st, lines, n,
+                       inner, m, src, a);
+    hipLaunchKernelGGL((bluestein_filter_kernel<T, true>), dim3(grid_for(m)), dim3(kBlock), 0, st, n, m, b);
+  } else {
+    hipLaunchKernelGGL((bluestein_in_kernel<T, false>), dim3(grid_for(lines * m)), dim3(kBlock), 0, st, lines, n,
+                       inner, m, src, a);
+    hipLaunchKernelGGL((bluestein_filter_kernel<T, false>), dim3(grid_for(m)), dim3(kBlock), 0, st, n, m, b);
+  }
+  int e = last_launch_status();
+  if (e) return e;
+  if ((e = fft_axis<T>(m, 1, lines, false, a, a, w2, st))) return e;
+  if ((e = fft_axis<T>(m, 1, 1, false, b, b, w2, st))) return e;
+  hipLaunchKernelGGL((cmul_kernel<T, false>), dim3(grid_for(lines * m)), dim3(kBlock), 0, st, lines * m, m, a, b, a);
+  if ((e = last_launch_status())) return e;
+  if ((e = fft_axis<T>(m, 1, lines, true, a, a, w2, st))) return e;
+  if (inv)
+    hipLaunchKernelGGL((bluestein_out_kernel<T, true>), dim3(grid_for(lines * n)), dim3(kBlock), 0, st, lines, n, inner,
+                       m, a, dst);
+  else
+    hipLaunchKernelGGL((bluestein_out_kernel<T, false>), dim3(grid_for(lines * n)), dim3(kBlock), 0, st, lines, n,
+                       inner, m, a, dst);
+  return last_launch_status();
+}
+
+template <typename T>
+int fft_check(int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int64_t& total) {
   PXA_CHECK_ARG(ndim >= 1 && ndim <= 8 && shape && naxes >= 0 && naxes <= ndim && stack >= 0);
   PXA_CHECK_ARG(naxes == 0 || axes != nullptr);
-  int64_t total = stack;
+  total = stack;
   for (int d = 0; d < ndim; ++d) {
     PXA_CHECK_ARG(shape[d] >= 1);
     total *= shape[d];
   }
-  if (total == 0) return PXA_OK;
-  PXA_CHECK_ARG(in && out);
   for (int i = 0; i < naxes; ++i) {
     PXA_CHECK_ARG(axes[i] >= 0 && axes[i] < ndim);
     for (int j = 0; j < i; ++j) PXA_CHECK_ARG(axes[i] != axes[j]);
   }
+  return PXA_OK;
+}
+
+// complex elements of workspace for the whole transform (max over the axes); -1: unsupported
+template <typename T>
+int64_t fft_work_elems(int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack) {
+  int64_t total = 0;
+  if (fft_check<T>(ndim, shape, naxes, axes, stack, total) != PXA_OK) return -1;
+  int64_t need = 0;
+  for (int i = 0; i < naxes && total > 0; ++i) {
+    const int64_t n = shape[axes[i]];
+    const int64_t w = axis_work<T>(n, total / n);
+    if (w < 0) return -1;
+    need = w > need ? w : need;
+  }
+  return need;
+}
+
+template <typename T>
+int fft_entry(int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse, const void* in,
+              void* out, void* work, hipStream_t st) {
+  int64_t total = 0;
+  const int c = fft_check<T>(ndim, shape, naxes, axes, stack, total);
+  if (c != PXA_OK) return c;
+  if (total == 0) return PXA_OK;
+  PXA_CHECK_ARG(in && out);
   const void* src = in;
   for (int i = 0; i < naxes; ++i) {
     const int a = axes[i];
-    FftPlan p;
-    p.n = shape[a];
-    p.inner = 1;
-    for (int d = a + 1; d < ndim; ++d) p.inner *= shape[d];
-    p.lines = total / p.n;
-    if (p.n == 1) continue;
-    const size_t line_bytes = (size_t)p.n * sizeof(Cx<T>);
-    const bool smooth = factor(p.n, p);
-    if (smooth && 2 * line_bytes <= kFftLds) {
-      int lpb = (int)(kFftLds / (2 * line_bytes));
-      if (lpb > 16) lpb = 16;
-      if (p.inner > 1 && lpb > p.inner) lpb = (int)p.inner;
-      p.lpb = lpb;
-      const int64_t blocks = (p.lines + lpb - 1) / lpb;
-      PXA_CHECK_ARG(blocks <= 0x7fffffff);
-      const size_t smem = 2 * (size_t)lpb * line_bytes;
-      auto kern = inverse ? fft_stockham_kernel<T, true> : fft_stockham_kernel<T, false>;
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kFftThreads), smem, st, p, (const Cx<T>*)src,
-                         (Cx<T>*)out);
-    } else {
-      if (line_bytes > kFftLds || p.n > 8 * kFftThreads) return PXA_ERR_UNSUPPORTED;
-      PXA_CHECK_ARG(p.lines <= 0x7fffffff);
-      p.lpb = 1;
-      auto kern = inverse ? fft_direct_kernel<T, true> : fft_direct_kernel<T, false>;
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)line_bytes);
-      hipLaunchKernelGGL(kern, dim3((unsigned)p.lines), dim3(kFftThreads), line_bytes, st, p, (const Cx<T>*)src,
-                         (Cx<T>*)out);
-    }
-    const int e = last_launch_status();
+    const int64_t n = shape[a];
+    if (n == 1) continue;
+    int64_t inner = 1;
+    for (int d = a + 1; d < ndim; ++d) inner *= shape[d];
+    const int64_t w = axis_work<T>(n, total / n);
+    if (w < 0) return PXA_ERR_UNSUPPORTED;
+    if (w > 0 && work == nullptr) return PXA_ERR_UNSUPPORTED;  // pxa_fft: no workspace given
+    const int e = fft_axis<T>(n, inner, total / n, inverse != 0, (const Cx<T>*)src, (Cx<T>*)out, (Cx<T>*)work, st);
     if (e) return e;
     src = out;
   }
@@ -319,18 +573,6 @@ __global__ void __launch_bounds__(kBlock) complex_real_kernel(int64_t n, const C
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = z[i].re;
 }
 
-// out[i] = a[i] * b[i % nb] (b conjugated if CONJ): spectrum product of an FFT convolution
-template <typename T, bool CONJ>
-__global__ void __launch_bounds__(kBlock) cmul_kernel(int64_t n, int64_t nb, const Cx<T>* __restrict__ a,
-                                                      const Cx<T>* __restrict__ b, Cx<T>* __restrict__ out) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    Cx<T> w = b[i % nb];
-    if (CONJ) w.im = -w.im;
-    out[i] = cmul(a[i], w);
-  }
-}
-
 }  // namespace
 }  // namespace pxa
 
@@ -340,7 +582,22 @@ extern "C" {
 
 int pxa_fft(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse,
             const void* in, void* out, void* stream) {
-  PXA_DISPATCH(dtype, T, return fft_entry<T>(ndim, shape, naxes, axes, stack, inverse, in, out, as_stream(stream)));
+  PXA_DISPATCH(dtype, T,
+               return fft_entry<T>(ndim, shape, naxes, axes, stack, inverse, in, out, nullptr, as_stream(stream)));
+}
+
+size_t pxa_fft_workspace_bytes(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack) {
+  int64_t e = -1;
+  if (dtype == PXA_F32) e = fft_work_elems<float>(ndim, shape, naxes, axes, stack);
+  else if (dtype == PXA_F64) e = fft_work_elems<double>(ndim, shape, naxes, axes, stack);
+  if (e < 0) return (size_t)-1;
+  return (size_t)e * (dtype == PXA_F32 ? sizeof(Cx<float>) : sizeof(Cx<double>));
+}
+
+int pxa_fft_ex(int dtype, int ndim, const int64_t* shape, int naxes, const int* axes, int64_t stack, int inverse,
+               const void* in, void* out, void* work, void* stream) {
+  PXA_DISPATCH(dtype, T,
+               return fft_entry<T>(ndim, shape, naxes, axes, stack, inverse, in, out, work, as_stream(stream)));
 }
 
 int pxa_complex_mul(int dtype, int64_t n, int64_t nb, const void* a, const void* b, int conj_b, void* out,

@@ -41,6 +41,12 @@ EXTRA_CASES = [
     ((3, 96, 210), (1, 2), (3, 96, 210), (1, 2)),  # 96 = 8*4*3, 210 = 2*3*5*7
     ((11, 13, 17), None, (11, 13, 17), (0, 1, 2)),  # primes: exact DFT
     ((7, 1, 1000), (0, 2), (7, 1, 1000), (0, 2)),
+    # beyond one workgroup's LDS: four-step (smooth) and Bluestein (any length), contiguous and strided
+    ((16384,), None, (16384,), (0,)),  # 2^14 = 128 x 128 four-step
+    ((12000, 3), (0,), (12000, 3), (0,)),  # smooth, strided axis
+    ((4099,), None, (4099,), (0,)),  # prime > 2048: Bluestein with m = 8192
+    ((3, 2053), (1,), (3, 2053), (1,)),  # prime just above the direct-DFT envelope
+    ((2, 2*3001), None, (2, 6002), (0, 1)),  # 2 x 3001: Bluestein on a non-smooth composite
 ]
 
 
@@ -49,8 +55,6 @@ EXTRA_CASES = [
 @pytest.mark.parametrize("case", REF_CASES + EXTRA_CASES, ids=lambda c: f"{c[2]}-{c[3]}")
 def test_fft_vs_numpy(case, dt, real):
     user_shape, user_axes, sh, axes = case
-    if dt == np.float64 and max(sh) > 2048:
-        pytest.skip("fp64 lines above 2048 points are outside the LDS envelope")
     rng = np.random.default_rng(26)
     stack = 2
     N = int(np.prod(sh))
