@@ -396,9 +396,24 @@ def bench_c4(ctx, args):
         c0 = CG.steps_taken
         elapsed = timed_steps(ctx, it, 0, args.c4_steps)
         cg_steps = CG.steps_taken - c0  # inner CG iterations of the timed outer iterations
+        # the CG operator's kernel alone (HIP events, after the timed region): K^T K p in one pass over K
+        normal_ms = None
+        from pyxu_amd import _dev
+
+        if ctx.world == 1 and _dev.dense_normal_supported(Kr, y.new_zeros((N,))):
+            p = torch.randn((N,), generator=gen, device="cuda", dtype=torch.float32)
+            for _ in range(3):
+                _dev.dense_normal(Kr, p, 1.0, 1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                _dev.dense_normal(Kr, p, 1.0, 1.0)
+            e1.record()
+            e1.synchronize()
+            normal_ms = e0.elapsed_time(e1) / 10
     per_outer = cg_steps / max(1, args.c4_steps)
     cg_ms = 1e3 * elapsed / max(1.0, per_outer * args.c4_steps)
-    pair_bytes = 2 * (hi - lo) * N * 4  # one K p + one K^T z pass over the local K per CG iteration
+    pair_bytes = 2 * (hi - lo) * N * 4  # SURVEY §8(d): one K p + one K^T z pass over the local K per CG iteration
     rec = {"workload": f"ADMM dense {M}x{N} K + lam*L1 (x-update: QuadraticFunc.prox -> CG), tau=1",
            "rows_per_rank": hi - lo, "scaling": "strong", "steps": args.c4_steps, "warmup": args.c4_warmup,
            "value": round(args.c4_steps / elapsed, 3), "unit": "ADMM outer iterations/s",
@@ -407,6 +422,12 @@ def bench_c4(ctx, args):
            "roofline": {"bound": "hbm", "achieved": round(pair_bytes / (cg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(pair_bytes / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                         "note": "whole CG iteration vs the two compulsory passes over this rank's K (SURVEY §8(d) C4)"}}
+    if normal_ms is not None:  # the fused operator reads K once: its own roofline against one pass
+        one = (hi - lo) * N * 4
+        rec["normal_operator"] = {"kernel": "normal_rows_kernel + normal_sum/final", "kernel_ms": round(normal_ms, 4),
+                                  "achieved": round(one / (normal_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(one / (normal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  "note": "K^T K p + p/tau in ONE pass over K (pxa_dense_normal), alg bytes = M N 4"}
     del s, K, Kr
     torch.cuda.empty_cache()
     return rec

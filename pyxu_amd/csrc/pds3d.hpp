@@ -340,7 +340,7 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
       L::pass_b_item(it, a, cb);
 #pragma unroll
       for (int uu = 0; uu < V; ++uu) {
-        T* o = O + (V * a + uu) * S::OP + CW * cb;
+        T* o = O + S::idx(V * a + uu, CW * cb);
 #pragma unroll
         for (int w = 0; w < CW; ++w) o[w] = st[k][uu][w];
       }
@@ -352,7 +352,8 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
   const int64_t hoff = ((s % g.y_images) * g.n0 + plane) * M;
   const int a_first = 3 - g.D;
   const T one = T(1), mtau = -p.tau;
-  const int cq = tid % S::LPR, r0 = tid / S::LPR;
+  int r0, cq;
+  S::lane(tid, r0, cq);
   constexpr int NS = TY / S::RPS;
 #pragma unroll
   for (int si = 0; si < NS; ++si) {
@@ -382,7 +383,7 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
       }
     };
     T gv[V], xv[V], bv[V], wv[V], ov[V];
-    ld_vec<T, V>(O + r * S::OP + V * cq, gv);
+    ld_vec<T, V>(O + S::idx(r, V * cq), gv);
     ld(P.x, off, xv);
     ld(P.hty, bo, bv);
     if constexpr (PD3O) {

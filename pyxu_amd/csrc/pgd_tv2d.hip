@@ -322,7 +322,8 @@ __device__ inline void epilogue_staged(const PgdParams<T>& p, const T* A, const 
   using S = Stage<T, R>;
   constexpr int V = L::V;
   const int n0 = p.n0, n1 = p.n1;
-  const int cq = threadIdx.x % S::LPR, r0 = threadIdx.x / S::LPR;
+  int r0, cq;
+  S::lane(threadIdx.x, r0, cq);
   constexpr int NS = TY / S::RPS;
   T bv[NS][V];
 #pragma unroll
@@ -339,7 +340,7 @@ __device__ inline void epilogue_staged(const PgdParams<T>& p, const T* A, const 
   for (int s = 0; s < NS; ++s) {
     const int r = r0 + s * S::RPS;
     T g[V], y[V];
-    ld_vec<T, V>(O + r * S::OP + V * cq, g);
+    ld_vec<T, V>(O + S::idx(r, V * cq), g);
     ld_vec<T, V>(A + (r + 2 * R) * L::AP + L::CA + V * cq, y);
     finish_run<T, V, EDGE>(p, ty0 + r, tx0 + V * cq, g, bv[s], y, xs, xns, want_part, part_d, part_x);
   }
@@ -426,7 +427,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
         L::pass_b_item(it, a, cb);
 #pragma unroll
         for (int u = 0; u < V; ++u) {
-          T* o = O + (V * a + u) * S::OP + CW * cb;
+          T* o = O + S::idx(V * a + u, CW * cb);
           if constexpr (CW == 2) {
             const T pr[2] = {st[k][u][0], st[k][u][1]};
             if constexpr (sizeof(T) == 4) *reinterpret_cast<float2*>(o) = make_float2(pr[0], pr[1]);

@@ -193,10 +193,41 @@ template <typename T, int R>
 struct Stage {
   using L = Layout<T, R>;
   static constexpr int V = L::V;
-  static constexpr int OP = sizeof(T) == 4 ? TX + 4 : TX + 2;  // conflict-free item-order writes (fp32)
-  static constexpr int LPR = TX / V;                           // lanes per tile row
-  static constexpr int RPS = kThreads / LPR;                   // rows per sweep
+  static constexpr bool F32 = sizeof(T) == 4;
+  // fp32: 64-dword rows with the 16-B chunks of row r XOR-swizzled by 2 (r / 4): the pass-B item-order
+  // ds_write_b64 (rows 4a + u, column pairs of cb) hit 32 distinct banks per 16-lane group, and a
+  // row-major ds_read_b128 group reads one whole row (64 contiguous dwords, permuted): both
+  // conflict-free under the MI355X_MICROARCH.md §LDS bank model (scripts/ldsbank.py)
+  static constexpr int OP = F32 ? TX : TX + 2;
+  static constexpr int LPR = TX / V;          // lanes per tile row
+  static constexpr int RPS = kThreads / LPR;  // rows per sweep
   static_assert(TY * OP <= L::AC * L::PTP, "O must fit in the PT region");
+  __device__ static inline int idx(int r, int c) {
+    if constexpr (F32) return r * OP + 4 * (((c >> 2) ^ (2 * (r >> 2))) & 15) + (c & 3);
+    else return r * OP + c;
+  }
+  // row-major epilogue lane -> (tile row r0 of the first sweep, 16-B column vector cq).  fp32: each
+  // ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) takes one row, so the reads
+  // of O and of the yk window A are contiguous 64-dword runs whatever the pitch; global accesses of a
+  // wave still cover 4 whole 256-B tile rows
+  __device__ static inline void lane(int tid, int& r0, int& cq) {
+    if constexpr (F32) {
+      static_assert(TX == 64 && kThreads % 64 == 0, "fp32 lane map assumes 64-column tiles");
+      const int ln = tid & 63, w = tid >> 6, h = ln >> 5, l = ln & 31;
+      int g, pos;
+      if (l < 4) g = 0, pos = l;
+      else if (l < 12) g = 1, pos = l - 4;
+      else if (l < 16) g = 0, pos = l - 8;
+      else if (l < 20) g = 1, pos = l - 8;
+      else if (l < 28) g = 0, pos = l - 12;
+      else g = 1, pos = l - 16;
+      r0 = 4 * w + 2 * h + g;
+      cq = pos;
+    } else {
+      cq = tid % LPR;
+      r0 = tid / LPR;
+    }
+  }
 };
 
 // XCD-aware tile order (speed only): XCD group g = blockIdx % 8 owns a contiguous band of tiles.

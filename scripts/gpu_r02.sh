@@ -23,7 +23,7 @@ step shapes 600 $PT tests/test_gpu_bench_shapes.py -m gpu
 [ "$2" = "quick" ] || step pytest 900 $PT tests -x -m gpu --ignore=tests/test_gpu_bench_shapes.py
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 400 python bench.py
-step bench_n2_gloo 400 env PXA_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 0
+step bench_n2_gloo 400 env PXA_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 0 --c4-m 2048
 P=$O/prof
 mkdir -p $P
 step trace 300 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- python3 bench.py --no-sub --cpu-seconds 0 --steps 200 --warmup 20
