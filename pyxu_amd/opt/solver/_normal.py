@@ -14,7 +14,7 @@ caller keeps the generic ``A.apply``: results are the same operator, rounded in 
 """
 import pyxu_amd.abc.arithmetic as _ar
 
-__all__ = ["normal_form"]
+__all__ = ["normal_form", "normal_form_ex"]
 
 
 def _mul(t1, t2):
@@ -65,18 +65,27 @@ def _terms(op, mats, depth):
     name = getattr(node, "_name", None)
     if name == "HomothetyOp":
         return {(): float(node._cst)}
+    group = None
+    if name == "RowShardedLinOp" and getattr(node, "_local", None) is not None:
+        # this rank's row block K_r of a row-sharded K (pyxu_amd.distributed): sum_r K_r^T K_r = K^T K
+        group, node, name = getattr(node, "_group", None), node._local, "_ExplicitLinOp"
+        sharded = True
+    else:
+        sharded = False
     if name == "_ExplicitLinOp" and getattr(node, "_mat", None) is not None:
         mat = node._mat
-        for i, m in enumerate(mats):
+        for i, (m, _, _) in enumerate(mats):
             if m is mat:
                 return {(("K", i),): 1.0}
-        mats.append(mat)
+        mats.append((mat, sharded, group))
         return {(("K", len(mats) - 1),): 1.0}
     return None
 
 
-def normal_form(op):
-    """(K_matrix, s, d) with op = s * K^T K + d * I, or None."""
+def normal_form_ex(op):
+    """(K_matrix, s, d, sharded, group) with op = s * K^T K + d * I, or None.  sharded: K is this rank's
+    row block of a row-sharded operator, and s * K^T K p is the all-reduce (sum over `group`) of the
+    ranks' s * K_r^T K_r p."""
     mats = []
     try:
         t = _terms(op, mats, 0)
@@ -94,4 +103,13 @@ def normal_form(op):
             return None
     if s == 0.0:
         return None
-    return mats[0], s, d
+    mat, sharded, group = mats[0]
+    return mat, s, d, sharded, group
+
+
+def normal_form(op):
+    """(K_matrix, s, d) with op = s * K^T K + d * I for one (unsharded) dense K, or None."""
+    r = normal_form_ex(op)
+    if r is None or r[3]:
+        return None
+    return r[0], r[1], r[2]

@@ -4,7 +4,7 @@ import numpy as np
 import pyxu_amd.abc as pxa
 import pyxu_amd.runtime as pxrt
 from pyxu_amd import _dev
-from pyxu_amd.opt.solver._normal import normal_form
+from pyxu_amd.opt.solver._normal import normal_form_ex
 
 __all__ = ["CG"]
 
@@ -84,11 +84,13 @@ class CG(pxa.Solver):
 
     def _make_apply(self, like):
         """A.apply, or -- when A = s K^T K + d I for one dense K (ADMM's QuadraticFunc.prox operator,
-        opt/solver/_normal.py) and the vectors fit pxa_dense_normal -- the one-pass normal operator."""
-        nf = normal_form(self._A)
+        opt/solver/_normal.py) and the vectors fit pxa_dense_normal -- the one-pass normal operator.  A
+        row-sharded K (pyxu_amd.distributed.RowShardedLinOp): each rank applies s K_r^T K_r in one pass
+        over its rows, one all-reduce sums them (the exchange K.adjoint makes anyway), then + d p."""
+        nf = normal_form_ex(self._A)
         if nf is None:
             return self._A.apply
-        mat, s, d = nf
+        mat, s, d, sharded, group = nf
         if not _dev.dense_normal_supported(mat, like):
             return self._A.apply
         work = [None]
@@ -101,8 +103,14 @@ class CG(pxa.Solver):
             if work[0] is None:
                 wsz = int(_dev.lib.pxa_dense_normal_workspace_bytes(_dev.dtcode(v), mat.shape[0], mat.shape[1], 1))
                 work[0] = torch.empty((wsz,), dtype=torch.uint8, device=v.device)
-            return _dev.dense_normal(mat, v, s, d, work=work[0])
+            if not sharded:
+                return _dev.dense_normal(mat, v, s, d, work=work[0])
+            from pyxu_amd.distributed import allreduce
 
+            y = allreduce(_dev.dense_normal(mat, v, s, 0.0, work=work[0]), "sum", group)
+            return _dev.axpby(1.0, y, d, v, out=y)
+
+        apply.fused = True
         return apply
 
     def m_step(self):

@@ -273,6 +273,11 @@ def gpu_row_sharded_admm(rank, world, M, N, n_iter):
         s = pxs.ADMM(f=f, h=lam * pxo.L1Norm(dim=N), show_progress=False)
         s.fit(x0=to_device(np.zeros(N, np.float32)), tau=tau, stop_crit=pxst.MaxIter(n_iter))
         out = dict(x=to_NUMPY(s.solution()))
+        from pyxu_amd.opt.solver._normal import normal_form_ex
+
+        Q = f._quad_spec()[0]
+        nf = normal_form_ex(Q + pxo.HomothetyOp(cst=1 / tau, dim=N))
+        out["sharded_normal"] = nf is not None and nf[3]
         if rank == 0:
             Kf = pxa.LinOp.from_array(to_device(K))
             f1 = 0.5 * pxo.SquaredL2Norm(dim=M).asloss(to_device(y)) * Kf

@@ -110,9 +110,9 @@ def test_admm_fused_normal_matches_generic_and_oracle(M, N):
     import pyxu_amd.opt.solver.cg as cgm
 
     for fused in (True, False):
-        saved = cgm.normal_form
+        saved = cgm.normal_form_ex
         if not fused:
-            cgm.normal_form = lambda op: None
+            cgm.normal_form_ex = lambda op: None
         try:
             with pxrt.Precision(pxrt.Width.SINGLE):
                 K = pxa.LinOp.from_array(to_device(A))
@@ -122,7 +122,7 @@ def test_admm_fused_normal_matches_generic_and_oracle(M, N):
                 s.fit(x0=to_device(np.zeros(N, np.float32)), tau=tau, stop_crit=pxst.MaxIter(iters))
                 out[fused] = to_NUMPY(s.solution())
         finally:
-            cgm.normal_form = saved
+            cgm.normal_form_ex = saved
     assert rel_err(out[True], out[False]) <= 1e-5
     xr, ur, _, _ = orc.admm_dense_l1(A.astype(np.float64), y.astype(np.float64), lam, np.zeros(N), tau, iters)
     assert rel_err(out[True], xr) <= 1e-4  # solution() = x (primal), fp32 vs the fp64 oracle

@@ -33,6 +33,7 @@ def test_row_sharded_admm_matches_unsharded():
     different order, hence a norm-wise tolerance."""
     res = spawn("gpu_row_sharded_admm", M=96, N=256, n_iter=10)
     for r in (0, 1):
+        assert res[r]["sharded_normal"]  # CG ran K_r^T K_r p in one pass + one all-reduce
         assert rel_err(res[r]["x"], res[0]["x_ref"]) <= 1e-5
     np.testing.assert_array_equal(res[0]["x"], res[1]["x"])
 
