@@ -23,6 +23,13 @@ def _torch():
     return torch
 
 
+def wait_event(ev):
+    """Wait for a recorded HIP event by polling it: a stop check waits a few tens of microseconds, and
+    a blocking hipEventSynchronize wakes the host up later than a poll notices the event."""
+    while not ev.query():
+        pass
+
+
 def dtcode(t) -> int:
     torch = _torch()
     if t.dtype == torch.float32:

@@ -50,6 +50,12 @@ class StoppingCriterion:
     def stop(self, state) -> bool:
         raise NotImplementedError
 
+    def stop_async(self, state):
+        """Two-phase stop(): enqueue the device work of the decision now, return a callable that
+        completes it (same decision, same info()).  Default: decide now."""
+        r = self.stop(state)
+        return lambda: r
+
     def info(self) -> dict:
         raise NotImplementedError
 
@@ -69,6 +75,10 @@ class _StoppingCriteriaComposition(StoppingCriterion):
 
     def stop(self, state) -> bool:
         return self._op(self._lhs.stop(state), self._rhs.stop(state))
+
+    def stop_async(self, state):
+        lhs, rhs = self._lhs.stop_async(state), self._rhs.stop_async(state)
+        return lambda: self._op(lhs(), rhs())
 
     def info(self):
         return {**self._lhs.info(), **self._rhs.info()}
@@ -335,6 +345,46 @@ class Solver:
             raise ValueError("Illegal method call: can only be used if Solver.fit() invoked with mode=Any["
                              + ", ".join(_.name for _ in modes) + "]")
 
+    # ---- speculative stop checks: the next m_step runs on the device while the host decides
+    def _spec_supported(self) -> bool:
+        """True when m_step can be undone (`_spec_begin` / `_spec_rollback`): solvers override."""
+        return False
+
+    def _spec_begin(self):
+        raise NotImplementedError
+
+    def _spec_rollback(self, token):
+        raise NotImplementedError
+
+    def _step_speculative(self, idx, _ml, log_on) -> bool:
+        """A stop check whose decision does not stall the device queue: the criterion enqueues its
+        statistics (stop_async), m_step is launched speculatively, then the decision is read.  If it
+        says stop, m_step is undone (the state is the one the check saw) and the solver ends exactly as
+        the synchronous path would: same iterates, same history records, same log lines."""
+        ast = self._astate
+        resolve = ast["stop_crit"].stop_async(self._mstate)
+        token = self._spec_begin()
+        err = None
+        try:
+            self.m_step()
+        except Exception as e:  # raised only if the check says continue (then the reference calls m_step)
+            err = e
+        if resolve():
+            self._spec_rollback(token)
+            with ast["lock"]:
+                self._record(idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, log_on)
+            if log_on:
+                ast["logger"].info(f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
+            self.writeback()
+            return False
+        ast["idx"] += 1
+        rec = (idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, _ml and log_on)
+        with ast["lock"]:
+            ast["pending"].append(rec)
+        if err is not None:
+            raise err
+        return True
+
     def _step(self) -> bool:
         ast = self._astate
         idx = ast["idx"]
@@ -349,6 +399,8 @@ class Solver:
         try:
             if _ms and ast["track_objective"]:
                 self._mstate["objective_func"] = self.objective_func().reshape(-1)
+            if _ms and not _mw and self._spec_supported():
+                return self._step_speculative(idx, _ml, log_on)
             if _ms and ast["stop_crit"].stop(self._mstate):
                 with ast["lock"]:
                     self._record(idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, log_on)

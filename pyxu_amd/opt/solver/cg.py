@@ -32,7 +32,7 @@ class _HostRows:
         self._ev.record()
 
     def host(self):
-        self._ev.synchronize()
+        _dev.wait_event(self._ev)
         return self._h.numpy()
 
 

@@ -1,5 +1,6 @@
 """Proximal Gradient Descent (mirrors reference opt/solver/pgd.py:14-219)."""
 import itertools
+import os
 import sys
 import math
 import warnings
@@ -11,6 +12,9 @@ from pyxu_amd.opt.solver._fused import match_pgd_deblur
 from pyxu_amd.util import copy_if_unsafe
 
 __all__ = ["PGD"]
+
+# PXA_NO_SPEC=1: synchronous stop checks (A/B measurements of the speculative ones)
+_NO_SPEC = os.environ.get("PXA_NO_SPEC", "0") == "1"
 
 
 class AutoInferenceWarning(UserWarning):
@@ -75,9 +79,27 @@ class PGD(pxa.Solver):
                                           p["lam"], p["mu"], p["prox"], p["prox_scale"])
             self._spare = None
 
+    # speculative stop checks (abc/solver.py _step_speculative): the fused step writes a buffer that is
+    # neither x nor x_prev, so undoing it is restoring (x, x_prev) and the momentum value it consumed
+    def _spec_supported(self):
+        return self._plan is not None and not _NO_SPEC
+
+    def _spec_begin(self):
+        mst = self._mstate
+        self._spec_refs = 1  # the token below holds one more reference to x_prev
+        return (mst["x"], mst["x_prev"])
+
+    def _spec_rollback(self, token):
+        mst = self._mstate
+        mst["x"], mst["x_prev"] = token
+        mst["a"] = itertools.chain([self._last_a], mst["a"])
+        self._spare = None
+        self._spec_refs = 0
+
     def m_step(self):
         mst = self._mstate
         a = next(mst["a"])
+        self._last_a = a
         if self._plan is not None:
             p = self._plan
             x, xp = mst["x"], mst["x_prev"]
@@ -90,7 +112,9 @@ class PGD(pxa.Solver):
             mst["x_prev"], mst["x"] = x, out
             # recycle the old x_prev as the next output buffer iff nobody else holds it (the reference
             # allocates fresh arrays, so user-held results must never be overwritten)
-            self._spare = xp if (sys.getrefcount(xp) == 2 and xp.data_ptr() != x.data_ptr()
+            refs = 2 + getattr(self, "_spec_refs", 0)
+            self._spec_refs = 0
+            self._spare = xp if (sys.getrefcount(xp) == refs and xp.data_ptr() != x.data_ptr()
                                  and _dev.storage_exclusive(xp)) else None
             return
         # generic path: y = (x - x_prev) * a + x ; z = y - tau * grad(y) ; x+ = prox_g(z, tau)

@@ -276,6 +276,47 @@ class RelError(pxa.StoppingCriterion):
     # hook: combine a device row statistic across shards (identity on one process)
     _reduce = None
 
+    def stop_async(self, state):
+        """stop() in two phases: the statistics, the copy of x and an async device->host copy of the
+        statistics are enqueued now; the returned callable waits for that copy only and decides.  Same
+        kernels, same bits, same decision, same info() as stop()."""
+        x = state[self._var]
+        if (isinstance(x, numbers.Real) or self._x_prev is None or self._reduce is not None
+                or self._f is not _identity or self._norm != 2):
+            return super().stop_async(state)
+        import torch
+
+        rows = x.numel() // x.shape[-1]
+        if not (0 < rows <= 65535 and x.dtype == self._x_prev.dtype):
+            return super().stop_async(state)
+        # one device / pinned-host statistics pair and one event per criterion, reused: a check is
+        # resolved before the next one is issued
+        buf = getattr(self, "_async_buf", None)
+        if buf is None or buf[0].shape[1] != rows or buf[0].device != x.device:
+            buf = (_dev.empty_f64((2, rows), x), torch.empty((2, rows), dtype=torch.float64, pin_memory=True),
+                   torch.cuda.Event())
+            self._async_buf = buf
+        st, host, ev = buf
+        x_copy = _dev.relerr_stats(x, self._x_prev, st)
+        host.copy_(st, non_blocking=True)
+        ev.record()
+        shape = x.shape[:-1]
+
+        def resolve():
+            _dev.wait_event(ev)
+            fin = _finish(host.numpy().copy(), self._norm)
+            num = fin[0].reshape(*shape, 1)
+            den = fin[1].reshape(*shape, 1)
+            rule = np.all if self._satisfy_all else np.any
+            decision = bool(rule(num <= self._eps * den))
+            with np.errstate(divide="ignore", invalid="ignore"):  # 0/0 -> nan -> 0 (stop.py:375-379)
+                self._val = num / den
+                self._val[np.isnan(self._val)] = 0
+            self._x_prev = x_copy
+            return decision
+
+        return resolve
+
     def info(self):
         if self._val.size == 1:
             return {f"RelError[{self._var}]": float(self._val.max())}

@@ -87,3 +87,51 @@ def test_async_mode_stats_consistent(tmp_path):
     assert its == list(range(len(its)))
     for snap in seen:
         assert snap == its[: len(snap)]
+
+
+def _pgd_problem(sh=(64, 96), lam=0.02, mu=0.02):
+    rng = np.random.default_rng(4)
+    N = int(np.prod(sh))
+    y = rng.standard_normal(N).astype(np.float32)
+    H = pxo.Gaussian(arg_shape=sh, sigma=1.5)
+    G = pxo.Gradient(arg_shape=sh)
+    f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(to_device(y)) * H + lam * pxo.L21Norm(arg_shape=(2, *sh)).moreau_envelope(mu) * G
+    f.diff_lipschitz = 1 + 8 * lam / mu
+    return f, pxo.PositiveOrthant(dim=N), N
+
+
+@pytest.mark.parametrize("stop_rate", [1, 3])
+@pytest.mark.parametrize("mode", ["BLOCK", "MANUAL"])
+def test_speculative_stop_checks_match_synchronous(stop_rate, mode, monkeypatch):
+    """Speculative stop checks (the next fused PGD step runs while the host reads the RelError
+    statistics, and is undone when the criterion fires) end with the same iterate, iteration count,
+    momentum and history as the synchronous checks of the reference order (solver.py:588-652)."""
+    res = {}
+    for spec in (True, False):
+        if not spec:
+            monkeypatch.setattr(pxs.PGD, "_spec_supported", lambda self: False)
+        with pxrt.Precision(pxrt.Width.SINGLE):
+            f, g, N = _pgd_problem()
+            s = pxs.PGD(f=f, g=g, show_progress=False, stop_rate=stop_rate)
+            crit = pxst.RelError(eps=2e-3) | pxst.MaxIter(400)
+            x0 = to_device(np.zeros(N, np.float32))
+            if mode == "BLOCK":
+                s.fit(x0=x0, stop_crit=crit)
+            else:
+                s.fit(x0=x0, stop_crit=crit, mode=pxa.Mode.MANUAL)
+                for _ in s.steps():
+                    pass
+            data, hist = s.stats()
+            res[spec] = (to_NUMPY(data["x"]), s._astate["idx"], next(s._mstate["a"]),
+                         {k: np.asarray(hist[k]) for k in hist.dtype.names})
+        monkeypatch.undo()
+    xs, idx_s, a_s, h_s = res[True]
+    xn, idx_n, a_n, h_n = res[False]
+    assert 20 < idx_n < 400 * stop_rate  # the relative-error criterion fired (MaxIter counts checks)
+    assert idx_s == idx_n and a_s == a_n
+    assert np.array_equal(xs, xn)
+    assert set(h_s) == set(h_n)
+    for k in h_n:
+        if k == "duration":
+            continue
+        np.testing.assert_array_equal(h_s[k], h_n[k], err_msg=k)
