@@ -52,6 +52,9 @@ extern "C" {
                                  4 tile kernel with the item-order epilogue, 5 persistent LDS-DMA kernel (fp32) */
 #define PXA_TUNE_NORMAL_DIAG 1 /* pxa_dense_normal timing probes (WRONG results, measurement only): 0 off,
                                   1 no x loads, 2 no cross-wave reduction, 3 no LDS accumulator */
+#define PXA_TUNE_PGD_PRIO 2 /* fused PGD tile kernel wave priorities (s_setprio): 0 none, 1 static per
+                               workgroup by (block >> 8) & 3, 2 memory phases high / compute low,
+                               3 static by (block >> 3) & 3, 4 = 1 + 2 */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */

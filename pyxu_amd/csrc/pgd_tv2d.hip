@@ -53,7 +53,18 @@ struct PgdParams {
   int prox;  // 0 none, 1 positive orthant, 2 l1 (uniform branch)
   bool tv;   // lam != 0 (uniform branch)
   bool vec_ok;
+  int prio;  // PXA_TUNE_PGD_PRIO mode (uniform)
 };
+
+// s_setprio with a runtime (wave-uniform) level 0..3
+__device__ inline void set_prio(int lvl) {
+  switch (lvl) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+}
 
 // q-weight: lam / max(|v|, mu)  (so that q = w v = lam (v - prox_{mu L21}(v)) / mu).
 template <typename T>
@@ -406,9 +417,14 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     KT[kKT + tid] = p.k1[tid];
   }
   double part_d = 0.0, part_x = 0.0;
+  const int pm = p.prio;
+  const int base_prio = pm == 1 || pm == 4 ? (int)((blockIdx.x >> 8) & 3u) : pm == 3 ? (int)((blockIdx.x >> 3) & 3u) : 0;
+  const bool phase_prio = pm == 2 || pm == 4;
+  if (pm) set_prio(phase_prio ? 3 : base_prio);
   if constexpr (STAGED) {
     using S = Stage<T, R>;
     load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+    if (phase_prio) set_prio(base_prio);
     __syncthreads();
     pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
     __syncthreads();
@@ -439,6 +455,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       }
     }
     __syncthreads();
+    if (phase_prio) set_prio(3);
     epilogue_staged<T, R, EDGE>(p, A, O, ty0, tx0, bs, xs, xns, partials != nullptr, part_d, part_x);
     if (partials) fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
   } else {
@@ -856,6 +873,7 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new);
   p.tv = lam != 0.0;
   p.prox = prox;
+  p.prio = tuning(PXA_TUNE_PGD_PRIO);
   if constexpr (sizeof(T) == 4) {
     // persistent LDS-DMA kernel (opt-in, PXA_TUNE_PGD_KERNEL = 5): 16-B vectors along rows and 32-bit
   // in-image offsets.  Measured slower than the tile kernel at 2048^2 (50 vs 27 us): see its header.
