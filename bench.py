@@ -320,12 +320,22 @@ def run_pgd(ctx, f, g, stop_rate, warmup, steps, fused, prime_s=0.0, kernel_time
     return elapsed, kern_ms, slvr, (timer.launches if timer is not None else 0)
 
 
-def roofline(pixels, kern_ms, traffic):
+PGD_KERNELS = {1: ("pgd_tv2d_kernel", "tile"), 2: ("pgd_march_kernel", "march")}
+
+
+def last_pgd_kernel():
+    """(rocprof kernel name, short name) of the fused PGD kernel this thread launched last."""
+    from pyxu_amd._lib import lib
+
+    return PGD_KERNELS.get(int(lib.pxa_pgd_tv2d_last_kernel()), (KERNEL, "none"))
+
+
+def roofline(pixels, kern_ms, traffic, kernel=KERNEL):
     alg_bytes = ALG_BYTES_PER_PIXEL * pixels  # SURVEY.md §8(d): 48 B/pixel/iteration
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     comp = FUSED_BYTES_PER_PIXEL * pixels
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": KERNEL,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
             "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes, "fused_compulsory_bytes_per_launch": comp,
             "frac_vs_fused_compulsory": round(comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
@@ -342,13 +352,15 @@ def bench_c5(ctx, args):
     sr = auto_stop_rate(K)
     with pxrt.Precision(pxrt.Width.SINGLE):
         elapsed, kern_ms, slvr, launches = run_pgd(ctx, f, g, sr, args.c5_warmup, K, True)
+    kname, kshort = last_pgd_kernel()
     kern_ms = ctx.max_over_ranks(kern_ms if kern_ms is not None else 0.0)
     rec = {"workload": f"PGD {total} x {n}x{n} batch-as-axis Gaussian(sigma=2) + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
            "images": total, "images_per_rank": hi - lo, "scaling": "strong", "steps": K, "warmup": args.c5_warmup,
            "stop_rate": sr, "value": round(total * K / elapsed, 1), "unit": "image-iterations/s",
-           "ms_per_step": round(1e3 * elapsed / K, 4), "stop_crit": "MaxIter | RelError (global all-reduce)"}
+           "ms_per_step": round(1e3 * elapsed / K, 4), "stop_crit": "MaxIter | RelError (global all-reduce)",
+           "pgd_kernel": kshort}
     if kern_ms > 0:
-        rec["roofline"] = roofline((hi - lo) * n * n, kern_ms, measured_traffic(KERNEL, f"{hi - lo}x{n}x{n}"))
+        rec["roofline"] = roofline((hi - lo) * n * n, kern_ms, measured_traffic(kname, f"{hi - lo}x{n}x{n}"), kname)
         rec["roofline"]["note"] = "per rank (slowest rank's kernel time)"
     del slvr
     return rec
@@ -446,7 +458,7 @@ def main():
     ap.add_argument("--generic", action="store_true", help="disable the fused m_step (rule-by-rule HIP path)")
     ap.add_argument("--no-kernel-timer", action="store_true", help="skip the in-region HIP-event kernel timing (A/B)")
     ap.add_argument("--no-sub", action="store_true", help="headline line only (no stop_rate_1 / c5 / c4 records)")
-    ap.add_argument("--pgd-kernel", type=int, default=0, help="PXA_TUNE_PGD_KERNEL (0 auto = tile kernel, 5 persistent LDS-DMA)")
+    ap.add_argument("--pgd-kernel", type=int, default=0, help="PXA_TUNE_PGD_KERNEL (0 auto, 1 tile kernel, 5 march kernel)")
     ap.add_argument("--c5-images", type=int, default=512)
     ap.add_argument("--c5-n", type=int, default=512)
     ap.add_argument("--c5-steps", type=int, default=20)
@@ -497,6 +509,7 @@ def main():
                                                        prime_s=args.prime_seconds, kernel_timer=not args.no_kernel_timer)
     fused = slvr._plan is not None
     stack = slvr._plan["stack"] if fused else 1
+    kname, kshort = last_pgd_kernel()
     del slvr
 
     sub = {}
@@ -516,7 +529,7 @@ def main():
         value = world * args.steps / elapsed_max
         roof = None
         if kern_ms is not None:
-            roof = roofline(N * stack, kern_ms, measured_traffic(KERNEL, f"{n0}x{n1}"))
+            roof = roofline(N * stack, kern_ms, measured_traffic(kname, f"{n0}x{n1}"), kname)
             roof["launches_timed"] = launches
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
@@ -544,7 +557,7 @@ def main():
             "config": {"workload": f"PGD {n0}x{n1} Gaussian(sigma=2) deblur + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
                        "image": [n0, n1], "images_per_gpu": 1, "stop_rate": sr,
                        "stop_crit": "MaxIter | RelError" + (f" (global, {'RCCL' if backend == 'nccl' else backend} all-reduce)" if world > 1 else ""),
-                       "fused_m_step": fused, "pgd_kernel": "persistent LDS-DMA" if args.pgd_kernel == 5 else "tile",
+                       "fused_m_step": fused, "pgd_kernel": kshort,
                        "parallelism": f"independent images x{world} (one per rank)"},
             "roofline": roof,
             "cpu_baseline": cpu,

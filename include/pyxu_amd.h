@@ -48,13 +48,17 @@ extern "C" {
 #define PXA_MODE_EDGE 4
 
 /* Kernel-selection knobs (pxa_tuning). */
-#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 auto (the tile kernel, staged row-major epilogue),
-                                 4 tile kernel with the item-order epilogue, 5 persistent LDS-DMA kernel (fp32) */
+#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 auto (march kernel where it applies, else the tile
+                                 kernel), 1 tile kernel, 4 tile kernel with the item-order epilogue,
+                                 5 march kernel where it applies */
 #define PXA_TUNE_NORMAL_DIAG 1 /* pxa_dense_normal timing probes (WRONG results, measurement only): 0 off,
                                   1 no x loads, 2 no cross-wave reduction, 3 no LDS accumulator */
 #define PXA_TUNE_PGD_PRIO 2 /* fused PGD tile kernel wave priorities (s_setprio): 0 none, 1 static per
                                workgroup by (block >> 8) & 3, 2 memory phases high / compute low,
                                3 static by (block >> 3) & 3, 4 = 1 + 2 */
+#define PXA_TUNE_PGD_DIAG 3 /* march-kernel timing probes (WRONG results, measurement only): bit 0 no
+                               passes A / B, bit 1 no LDS-DMA */
+#define PXA_TUNE_MARCH_BANDS 4 /* march kernel: 16-row bands per workgroup (0 auto: ~4 workgroups per CU) */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */
@@ -355,8 +359,13 @@ int pxa_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* 
  * alias x or x_prev.  If `partials` is not NULL, each workgroup writes (sum (x_new-x)^2, sum x^2)
  * for RelError into partials[2*blk..] (double) — pxa_pgd_tv2d_partials_count() gives the number of
  * workgroups.  prox codes: 0 none, 1 positive orthant, 2 l1 with weight prox_w.
+ * Two kernels compute the same bits: the march kernel (fp32, blur radius <= 6, n1 % 4 == 0, 16-B
+ * aligned arrays, no partials; 64-column strips marched in 16-row bands with the next band's rows in
+ * flight) and the tile kernel (everything else).  pxa_pgd_tv2d_last_kernel() names the one the
+ * calling thread's last successful pxa_pgd_tv2d_step launched: 1 tile, 2 march (0 before any).
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
+int pxa_pgd_tv2d_last_kernel(void);
 int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
                       const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,

@@ -157,7 +157,8 @@ def storage_exclusive(t) -> bool:
 
 
 TUNE_NORMAL_DIAG = 1  # PXA_TUNE_NORMAL_DIAG: pxa_dense_normal timing probes (wrong results)
-TUNE_PGD_KERNEL = 0  # PXA_TUNE_PGD_KERNEL: 0 auto (tile kernel), 5 persistent LDS-DMA kernel
+TUNE_PGD_KERNEL = 0  # PXA_TUNE_PGD_KERNEL: 0 auto, 1 tile kernel, 4 item-order epilogue, 5 march kernel
+TUNE_MARCH_BANDS = 4  # PXA_TUNE_MARCH_BANDS: march kernel bands per workgroup (0 auto)
 
 
 def tuning(key, value=-1):

@@ -66,6 +66,9 @@ __device__ inline void set_prio(int lvl) {
   }
 }
 
+// The TV stencil's two-product sums are written as explicit fma(a, b, c * d): under fp-contract=fast
+// the compiler may otherwise fuse either product, and then the tile and march kernels (different
+// register blocking, different instruction selection) would round differently.
 // q-weight: lam / max(|v|, mu)  (so that q = w v = lam (v - prox_{mu L21}(v)) / mu).
 template <typename T>
 __device__ inline T tv_weight(T n2, T lam, T mu, T inv_mu) {
@@ -262,9 +265,9 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
       auto qrow = [&](int r, const T(&yr)[CW + 2], const T(&yn)[CW + 2], T(&q0)[CW + 1], T(&q1)[CW + 1]) {
 #pragma unroll
         for (int c = 0; c <= CW; ++c) {
-          const T v0 = p.g0a * yr[c] + p.g0b * yn[c];
-          const T v1 = p.g1a * yr[c] + p.g1b * yr[c + 1];
-          T w = tv_weight<T>(v0 * v0 + v1 * v1, p.lam, p.mu, p.inv_mu);
+          const T v0 = fma(p.g0a, yr[c], p.g0b * yn[c]);
+          const T v1 = fma(p.g1a, yr[c], p.g1b * yr[c + 1]);
+          T w = tv_weight<T>(fma(v0, v0, v1 * v1), p.lam, p.mu, p.inv_mu);
           if (EDGE) {
             const int gr = ty0 + V * a - 1 + r, gc = tx0 + c0 - 1 + c;
             if (!(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) w = T(0);
@@ -294,8 +297,8 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
             // Grad^T q: flipped 2-tap adjoints, (+1/h tap at i - e_d) then (-1/h tap at i), summed over d
 #pragma unroll
             for (int w = 0; w < CW; ++w) {
-              const T t0 = p.g0b * qp0[w + 1] + p.g0a * qc0[w + 1];
-              const T t1 = p.g1b * qc1[w] + p.g1a * qc1[w + 1];
+              const T t0 = fma(p.g0b, qp0[w + 1], p.g0a * qc0[w + 1]);
+              const T t1 = fma(p.g1b, qc1[w], p.g1a * qc1[w + 1]);
               tv[u][w] = t0 + t1;
             }
 #pragma unroll
@@ -528,50 +531,40 @@ int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void*
 }
 
 // =====================================================================================================
-// Persistent LDS-DMA pipelined form (fp32, n1 % 4 == 0, 16-B aligned arrays): the same per-tile
-// arithmetic (load_window's yk, pass_a, pass_b), with the global->on-chip traffic of tile t+1 in
-// flight while tile t computes.
+// March kernel (fp32; R <= 6; n1 % 4 == 0; 16-B aligned arrays; no RelError partials): the tile
+// kernel's per-pixel arithmetic, reorganised so that HBM traffic is in flight while the CU computes.
 //
-// The tile kernel above serialises, per workgroup, window load -> pass A -> pass B (with H^T y loads
-// in its epilogue), and its 2 048 workgroups run as two synchronous rounds of 4 per CU: HBM idles
-// while every CU computes (SQ_WAIT_ANY ~50 % of wave cycles, r02a profiles).  Here 2 workgroups per
-// CU loop over their tiles (XCD-banded order):
-//   top:    own LDS-DMA of x / x_prev windows(t) landed (counted vmcnt) -> barrier
-//           issue H^T y(t) loads into registers (inline asm: counted by hand, see below)
-//           convert raw windows S -> yk in A (the tile kernel's phase-0 arithmetic)   -> barrier
-//           issue LDS-DMA of the x / x_prev windows of tile t+1 into S (global_load_lds_dwordx4)
-//           pass A (A -> PT)                                                         -> barrier
-//           vmcnt(NDW): H^T y(t) registers landed, tile t+1's DMA may stay in flight
-//           pass B (PT, A, H^T y regs -> x_new)
-// hipcc waits vmcnt(0) at the first use of an ordinary global load while an LDS-DMA is in flight
-// (cdna_hip_programming.md §5 "Pipelining across barriers"), which would drain tile t+1's DMA before
-// pass B: the H^T y loads are inline-asm global_load_dwordx2 with a hand-counted wait instead, and
-// barriers are raw s_barrier (a __syncthreads() would also drain the DMA).  Out-of-image window
-// slots DMA from a 16-byte zero page.  Each wave issues exactly NDW DMA instructions per tile (the
-// surplus instruction of the last wave and the tail window re-write slots with identical bytes), so
-// the hand-counted vmcnt values are exact.
+// The tile kernel serialises, per workgroup, window load -> pass A -> pass B -> epilogue, and the
+// 2 048 tiles of a 2048^2 image run as two phase-locked rounds of 4 workgroups per CU: HBM idles while
+// the chip computes and the VALUs idle while it loads (SQ_WAIT_ANY ~44 % of wave cycles), and every
+// tile re-reads a 2R row halo above and below (the x / x_prev window is 2.4x the tile).  Here one
+// workgroup owns a 64-column strip of a run of SB consecutive 16-row BANDS and marches down it:
+//   * the yk window W (16 + 4R rows x the strip's 64 + 2 CA columns) is carried from band to band:
+//     its last 4R rows become the next band's first 4R rows (a shift through registers), so each band
+//     loads only its 16 new rows (x / x_prev read 1.375x, vertical halo once per run);
+//   * those 16 new rows of x and x_prev travel by LDS-DMA (global_load_lds_dwordx4) into a staging
+//     area S one band AHEAD: band k+1's rows are in flight during band k's passes A and B;
+//   * H^T y of band k is loaded into registers at the top of band k and consumed by its epilogue.
+// LDS per workgroup (R = 6): W 14.7 KB + S 11.3 KB + PT 8.4 KB + O 4 KB = 38.7 KB -> 4 per CU, the same
+// occupancy as the tile kernel.  Per band: pass A (4 x 2 register blocks, G0 along rows, transposed
+// into PT), pass B (2 x 2 blocks, G1 along PT rows + the TV stencil of yk, parked in O), and the
+// staged row-major epilogue (one 16-B vector per lane: full 256-B row stores).  Every output gets the
+// same fp32 operations in the same order as in the tile kernel (sweep / ghost-fix tap order, TV and
+// epilogue expressions), so x_new is bit-identical (tests/test_gpu_pgd_variants.py).
+//
+// Hand-counted waits.  hipcc would wait vmcnt(0) at the first use of an ordinary load issued while an
+// LDS-DMA is in flight, and a __syncthreads() drains all memory operations; the DMAs and the H^T y
+// loads are therefore inline asm (invisible to hipcc's counter) and the barriers raw s_barrier.  Per
+// wave and band, in issue order: [H^T y(k): 1 load] [DMA(k+1): NDW] [x_new(k) stores: 1 for interior
+// bands, out-of-image lanes storing to a sink page].  Band k+1's top waits vmcnt(1) (DMA(k+1) landed,
+// the store may stay in flight), the epilogue waits vmcnt(NDW) (H^T y landed, DMA(k+1) may stay in
+// flight).  Every wave issues exactly NDW DMA instructions per band (the surplus
+// instruction of the last wave repeats the last slot range with identical bytes), and out-of-image
+// granules DMA from a zero page (n1 % 4 == 0: a 16-B granule is wholly inside or outside).
 __device__ __attribute__((aligned(16))) float g_zero_page[4];
+__device__ __attribute__((aligned(16))) float g_sink_page[4];  // target of the march epilogue's out-of-image lanes
 
 typedef __attribute__((address_space(3))) void lds_void;
-typedef const __attribute__((address_space(1))) void gbl_void;
-
-template <int R>
-struct V5 {
-  using L = Layout<float, R>;
-  static constexpr int SV = L::AC / 4;             // 16-B vectors per staged window row (unpadded)
-  static constexpr int SSLOTS = L::AR * SV;        // vectors per staged array
-  static constexpr int NSLOT = 2 * SSLOTS;         // x window then x_prev window
-  static constexpr int NDMA = cdiv(NSLOT, 64);     // wave-instructions per tile
-  static constexpr int NDW = cdiv(NDMA, kThreads / 64);  // per wave
-  static constexpr int A_OFF = NSLOT * 4;          // floats
-  static constexpr int PT_OFF = A_OFF + L::AR * L::AP;
-  static constexpr int KT_OFF = PT_OFF + L::AC * L::PTP;
-  static constexpr int RED_OFF = KT_OFF + 2 * kKT; // 2 * 4 doubles
-  static constexpr size_t BYTES = (size_t)(RED_OFF + 2 * 2 * (kThreads / 64)) * 4;
-  static_assert(NSLOT >= 64, "window smaller than one DMA instruction");
-  static_assert(NDW <= 15, "hand-counted vmcnt must fit the 6-bit counter with the b loads");
-  static_assert((A_OFF % 4) == 0 && (PT_OFF % 4) == 0 && (RED_OFF % 2) == 0, "LDS carve alignment");
-};
 
 __device__ inline void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -586,10 +579,7 @@ __device__ inline void wait_vm() {
 }
 
 // One wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane global addresses into the
-// contiguous 1 KiB at `lds_dst` (wave-uniform, passed in M0).  Written as inline asm so that hipcc
-// does not see an LDS-DMA in flight: it would otherwise wait vmcnt(0) before every LDS access of
-// passes A / B (it cannot tell that they touch other LDS bytes) and drain the prefetch.  All waits
-// for these loads are the hand-counted ones of the persistent loop.
+// contiguous 1 KiB at `lds_dst` (wave-uniform, passed in M0).
 __device__ inline void dma16(const float* gsrc, float* lds_dst) {
   const unsigned lds_addr = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((lds_void*)lds_dst));
   unsigned keep;
@@ -604,216 +594,454 @@ __device__ inline void dma16(const float* gsrc, float* lds_dst) {
       : "memory");
 }
 
-// this wave's NDW LDS-DMA instructions for the raw x / x_prev windows of the tile at (ty0, tx0)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline void asm_load_b4(f32x4& v, const float* ptr) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+}
+
+template <int R>
+struct March {
+  static constexpr int TB = 16;                       // band rows
+  static constexpr int CA = rup(2 * R, 4);            // column halo (16-B granules)
+  static constexpr int AC = TX + 2 * CA;              // window columns = PT rows
+  static constexpr int SH = 4 * R;                    // window rows carried to the next band
+  static constexpr int WR = TB + SH;                  // window rows
+  static constexpr int AP = AC % 8 == 4 ? AC : AC + 4;  // W pitch = 4 mod 8 (see march_pass_a / _b)
+  static constexpr int PTP = 24;                      // PT pitch (see march_pass_a / _b)
+  static constexpr int OP = TX;                       // O rows (rotated, see oidx)
+  static constexpr int SV = AC / 4;                   // 16-B granules per window row
+  static constexpr int SSLOTS = TB * SV;              // granules per staged array
+  static constexpr int NSLOT = 2 * SSLOTS;            // x rows then x_prev rows
+  static constexpr int NDMA = cdiv(NSLOT, 64);        // wave-instructions per band
+  static constexpr int NDW = cdiv(NDMA, kThreads / 64);  // per wave
+  static constexpr int W_OFF = 0;
+  static constexpr int S_OFF = W_OFF + WR * AP;
+  static constexpr int PT_OFF = S_OFF + NSLOT * 4;
+  static constexpr int O_OFF = PT_OFF + AC * PTP;
+  static constexpr int KT_OFF = O_OFF + TB * OP;
+  static constexpr size_t BYTES = (size_t)(KT_OFF + 2 * kKT) * 4;
+  static constexpr int NPA = (TB / 4) * (AC / 2);     // pass-A items: 4 rows x 2 columns
+  static constexpr int NPB = (TB / 2) * (TX / 2);     // pass-B items: 2 rows x 2 columns
+  static_assert(R >= 1 && R <= 6, "march kernel radius");
+  static_assert(BYTES <= 40960, "4 workgroups per CU");
+  static_assert(AC / 2 <= 48 && NPB == kThreads, "pass item maps");
+  static_assert(NSLOT >= 64 && NDW <= 8, "DMA slots");
+  static_assert((S_OFF % 4) == 0 && (PT_OFF % 4) == 0 && (O_OFF % 4) == 0, "16-B carve");
+  // O: 64-dword rows, row r rotated by 4 (r / 2) dwords: the pass-B ds_write_b64 of 16 lanes (8 row
+  // pairs x 2 column pairs) hit 32 distinct banks; a row-major epilogue lane group reads one row.
+  __device__ static inline int oidx(int r, int c) { return r * OP + ((c + 4 * (r >> 1)) & (OP - 1)); }
+};
+
+// the kernel's PgdParams read in place from the kernel-argument segment (scalar loads at their uses)
+using KP = const __attribute__((address_space(4))) PgdParams<float>*;
+
+// out[o][w] = sum_{t=0}^{4R} g[t] src[(o + t) * PS + w], w = 0, 1: the tap order of sweep()
+template <int R, int NO, int PS, typename GP>
+__device__ inline void sweep2(const float* __restrict__ src, GP g, float (&out)[NO][2]) {
+  using P = Pk<float>::type;
+  P acc[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) acc[o] = Pk<float>::splat(0.0f);
+#pragma unroll
+  for (int j = 0; j < NO + 4 * R; ++j) {
+    // volatile: keeps each row a ds_read_b64 (full LDS rate; the compiler would pair them into
+    // ds_read2_b64, half rate, and bank-conflicting under the mod-32 rule of that instruction)
+    const P row = *(const volatile __attribute__((address_space(3))) P*)(src + j * PS);
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int k = j - o;
+      if (k >= 0 && k <= 4 * R) acc[o] = Pk<float>::splat(g[k]) * row + acc[o];
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+    out[o][0] = acc[o][0];
+    out[o][1] = acc[o][1];
+  }
+}
+
+// ghost_fix() for a 2-wide vector across the sweep axis (same terms, same order)
+template <int R, int NO, int PS, typename GP>
+__device__ inline void ghost_fix2(int i0, int n, int q0, const float* __restrict__ src, GP k, const float* __restrict__ kt,
+                                  float (&acc)[NO][2]) {
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    const int pg = side == 0 ? -R : n;
+    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
+    if (!hit) continue;
+    float gh[R][2];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      const int pp = pg + m;
+      gh[m][0] = gh[m][1] = 0.0f;
+      if (pp >= i0 - R && pp <= i0 + NO - 1 + R) {
+#pragma unroll
+        for (int s = -R; s <= R; ++s) {
+          const float2 w = *reinterpret_cast<const float2*>(src + (pp + s - q0) * PS);
+          gh[m][0] = k[s + R] * w.x + gh[m][0];
+          gh[m][1] = k[s + R] * w.y + gh[m][1];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = i0 + o;
+      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        const int t = i - (pg + m);
+        if (t < -R || t > R) continue;
+        const float kk = kt[t + R];
+        acc[o][0] = acc[o][0] - kk * gh[m][0];
+        acc[o][1] = acc[o][1] - kk * gh[m][1];
+      }
+    }
+  }
+}
+
+// this wave's NDW LDS-DMA instructions: x / x_prev rows row0 .. row0 + TB - 1 of the strip -> S
 template <int R, bool EDGE>
-__device__ inline void issue_windows(float* S, const float* xs, const float* xps, int ty0, int tx0, int n0, int n1) {
-  using P = V5<R>;
-  constexpr int CA = P::L::CA;
+__device__ inline void march_issue(float* S, const float* xs, const float* xps, int row0, int tx0, int n0, int n1) {
+  using M = March<R>;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-  for (int i = 0; i < P::NDW; ++i) {
+  for (int i = 0; i < M::NDW; ++i) {
     int ins = wave + (kThreads / 64) * i;
-    if (ins > P::NDMA - 1) ins = P::NDMA - 1;  // surplus: repeat the last instruction (same bytes)
+    if (ins > M::NDMA - 1) ins = M::NDMA - 1;
     int base = ins * 64;
-    if (base > P::NSLOT - 64) base = P::NSLOT - 64;  // tail window ends at the last slot
+    if (base > M::NSLOT - 64) base = M::NSLOT - 64;
     const int s = base + lane;
-    const int arr = s >= P::SSLOTS;
-    const int q = s - arr * P::SSLOTS;
-    const int r = q / P::SV, g = q - r * P::SV;
-    const int gr = ty0 - 2 * R + r, gc = tx0 - CA + 4 * g;
+    const int arr = s >= M::SSLOTS;
+    const int q = s - arr * M::SSLOTS;
+    const int r = q / M::SV, g = q - r * M::SV;
+    const int gr = row0 + r, gc = tx0 - M::CA + 4 * g;
     const float* img = arr ? xps : xs;
     const float* src;
     if (!EDGE) {
       src = img + (unsigned)(gr * n1 + gc);
     } else {
       const bool in = gr >= 0 && gr < n0 && gc >= 0 && gc < n1;
-      src = in ? img + (int64_t)gr * n1 + gc : g_zero_page;
+      src = in ? img + (unsigned)(gr * n1 + gc) : g_zero_page;
     }
     dma16(src, S + 4 * base);
   }
 }
 
-__device__ inline void asm_load_b2(float2& v, const float* ptr) {
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
-}
-
+// pass A of one band: PT[c][r] = (G0 yk)[r0 + r][c] for the 16 band rows and all AC window columns
 template <int R, bool EDGE>
-__device__ inline void issue_b(float2 (&bq)[4], const float* bs, int ty0, int tx0, int n0, int n1) {
-  using L = Layout<float, R>;
-  int a, cb;
-  L::pass_b_item(threadIdx.x, a, cb);
-  const int gc = tx0 + 2 * cb;
+__device__ inline void march_pass_a(KP p, const float* W, float* PT, const float* KT, int r0) {
+  using M = March<R>;
+  // lane -> (row group a = lane & 3, column pair b): 11 column pairs per wave.  A 32-lane ds_read_b64
+  // group spans a = 0..3 x 8 consecutive b: rows 4 AP = 16 or 48 mod 64 dwords apart, conflict-free; an
+  // 8-lane ds_write_b128 group a = 0..3 x 2 consecutive b: PT columns 2 PTP = 16 mod 32 apart, conflict-free
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int a = l & 3, q = l >> 2, b = 11 * w + q;  // rows 4a .. 4a+3, columns 2b, 2b+1
+  if (q < 11 && b < M::AC / 2) {
+    float acc[4][2];
+    sweep2<R, 4, M::AP>(W + (4 * a) * M::AP + 2 * b, p->g0, acc);
+    const int n0 = p->n0;
+    const bool edge_rows = EDGE && (r0 < R || r0 + M::TB > n0 - R);
+    if (edge_rows) ghost_fix2<R, 4, M::AP>(r0 + 4 * a, n0, r0 - 2 * R, W + 2 * b, KT, KT, acc);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int gr = ty0 + 4 * a + u;
-    const float* ptr;
-    if (!EDGE) ptr = bs + (unsigned)(gr * n1 + gc);
-    else ptr = (gr < n0 && gc < n1) ? bs + (int64_t)gr * n1 + gc : g_zero_page;  // n1 even: gc < n1 => gc+1 < n1
-    asm_load_b2(bq[u], ptr);
-  }
-}
-
-// raw windows -> yk in A (bit-identical to load_window's arithmetic; zero page => yk = 0 outside)
-template <int R>
-__device__ inline void convert_windows(const float* S, float* A, float a) {
-  using P = V5<R>;
-  using L = typename P::L;
-  const float* Sa = static_cast<const float*>(__builtin_assume_aligned(S, 16));
-  float* Aa = static_cast<float*>(__builtin_assume_aligned(A, 16));
-#pragma unroll
-  for (int k = 0; k < cdiv(P::SSLOTS, kThreads); ++k) {
-    const int it = threadIdx.x + k * kThreads;
-    if (it >= P::SSLOTS) break;
-    const int r = it / P::SV, g = it - r * P::SV;
-    float xv[4], pv[4], out[4];
-    ld_vec<float, 4>(Sa + 4 * it, xv);
-    ld_vec<float, 4>(Sa + 4 * (P::SSLOTS + it), pv);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      float d = xv[v] - pv[v];
-      d = d * a;
-      out[v] = d + xv[v];
+    for (int w = 0; w < 2; ++w) {
+      const float colv[4] = {acc[0][w], acc[1][w], acc[2][w], acc[3][w]};
+      st_vec<float, 4>(PT + (2 * b + w) * M::PTP + 4 * a, colv);
     }
-    st_vec<float, 4>(Aa + r * L::AP + 4 * g, out);
   }
 }
 
-struct TileOf {
-  unsigned tile, s;
-  int ty0, tx0;
-};
+// pass B of one band: g = G1 (PT rows) + Grad^T q at 2 x 2 pixels per thread, parked in O
+template <int R, bool EDGE>
+__device__ inline void march_pass_b(KP p, const float* W, const float* PT, const float* KT, float* O, int r0,
+                                    int tx0) {
+  using M = March<R>;
+  constexpr int CA = M::CA;
+  const int n0 = p->n0, n1 = p->n1;
+  // lane -> (row pair i = lane & 7, column pair j): a 32-lane ds_read_b64 group spans i = 0..7 x 4
+  // consecutive j.  PT reads: columns 2 PTP = 48 mod 64 dwords apart -> 16-dword blocks, conflict-free;
+  // TV reads of W (full 8-B pairs): row pairs 2 AP = 8 x odd mod 64 apart -> conflict-free; O writes:
+  // rows rotated by 4 (r / 2) -> conflict-free
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int i = l & 7, j = 8 * w + (l >> 3);  // band rows 2i, 2i+1; strip columns 2j, 2j+1
+  const int c0 = 2 * j;
+  auto yrow = [&](int r, float(&y)[4]) {  // yk at band row 2i - 1 + r, strip columns c0 - 1 .. c0 + 2
+    // three full 8-B pairs (volatile: the compiler would shrink the outer two to ds_read_b32, which
+    // bank-conflict 2-way under the mod-32 rule of 4-B reads)
+    using P = Pk<float>::type;
+    using LP = const volatile __attribute__((address_space(3))) P*;
+    const float* arow = W + (2 * i - 1 + r + 2 * R) * M::AP + CA + c0;
+    const P lo = *(LP)(arow - 2), mid = *(LP)arow, hi = *(LP)(arow + 2);
+    y[0] = lo[1];
+    y[1] = mid[0];
+    y[2] = mid[1];
+    y[3] = hi[0];
+  };
+  auto qrow = [&](int r, const float(&yr)[4], const float(&yn)[4], float(&q0)[3], float(&q1)[3]) {
+#pragma unroll
+    for (int c = 0; c <= 2; ++c) {
+      const float v0 = fma(p->g0a, yr[c], p->g0b * yn[c]);
+      const float v1 = fma(p->g1a, yr[c], p->g1b * yr[c + 1]);
+      float w = tv_weight<float>(fma(v0, v0, v1 * v1), p->lam, p->mu, p->inv_mu);
+      if (EDGE) {
+        const int gr = r0 + 2 * i - 1 + r, gc = tx0 + c0 - 1 + c;
+        if (!(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) w = 0.0f;
+      }
+      q0[c] = v0 * w;
+      q1[c] = v1 * w;
+    }
+  };
+  float tv[2][2];
+  if (p->tv) {
+    float yr[4], yn[4];
+    yrow(0, yr);
+    yrow(1, yn);
+    float qp0[3], qp1[3];
+    qrow(0, yr, yn, qp0, qp1);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) yr[c] = yn[c];
+      yrow(u + 2, yn);
+      float qc0[3], qc1[3];
+      qrow(u + 1, yr, yn, qc0, qc1);
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const float t0 = fma(p->g0b, qp0[w + 1], p->g0a * qc0[w + 1]);
+        const float t1 = fma(p->g1b, qc1[w], p->g1a * qc1[w + 1]);
+        tv[u][w] = t0 + t1;
+      }
+#pragma unroll
+      for (int c = 0; c <= 2; ++c) qp0[c] = qc0[c];
+    }
+  }
+  float acc[2][2];  // acc[w][u]: column c0 + w, band row 2i + u
+  sweep2<R, 2, M::PTP>(PT + (CA - 2 * R + c0) * M::PTP + 2 * i, p->g1, acc);
+  const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n1 - R);
+  if (edge_cols) ghost_fix2<R, 2, M::PTP>(tx0 + c0, n1, tx0 - CA, PT + 2 * i, KT + kKT, KT + kKT, acc);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float g0 = acc[0][u], g1 = acc[1][u];
+    if (p->tv) {
+      g0 = g0 + tv[u][0];
+      g1 = g1 + tv[u][1];
+    }
+    *reinterpret_cast<float2*>(O + M::oidx(2 * i + u, c0)) = make_float2(g0, g1);
+  }
+}
 
-template <int R>
-__global__ void __launch_bounds__(kThreads, 2) pgd_tv2d_persistent(PgdParams<float> p, const float* __restrict__ x,
-                                                                 const float* __restrict__ xp,
-                                                                 const float* __restrict__ b, float* __restrict__ xn,
-                                                                 double* __restrict__ partials) {
-  using P = V5<R>;
-  using L = typename P::L;
-  extern __shared__ __attribute__((aligned(16))) float smem5[];
-  float* S = smem5;
-  float* A = smem5 + P::A_OFF;
-  float* PT = smem5 + P::PT_OFF;
-  float* KT = smem5 + P::KT_OFF;
-  double* red = reinterpret_cast<double*>(smem5 + P::RED_OFF);
+// One workgroup's run of nb bands of one strip.  EDGE: some band of the run touches the image border
+// (zero-page DMA granules, boundary corrections, masked TV weights and stores); the interior runs -- all
+// but the first / last strips and runs of a large image -- take the branch-free instantiation.
+template <int R, bool EDGE>
+__device__ inline void march_run(const PgdParams<float>& p, float* smem, int kb0, int nb, int tx0, const float* xs,
+                                 const float* xps, const float* bs, float* xns, int diag) {
+  using M = March<R>;
+  float* W = smem + M::W_OFF;
+  float* S = smem + M::S_OFF;
+  float* PT = smem + M::PT_OFF;
+  float* O = smem + M::O_OFF;
+  float* KT = smem + M::KT_OFF;
   const int tid = threadIdx.x;
   const int n0 = p.n0, n1 = p.n1;
+  auto issue_band = [&](int r0) {  // the band's 16 new window rows: image rows r0 + 2R ..
+    if (diag & 2) return;
+    march_issue<R, EDGE>(S, xs, xps, r0 + 2 * R, tx0, n0, n1);
+  };
+  const float a = p.a;
+  // prologue: DMA of band 0's new rows, then the first SH window rows (image rows r0 - 2R ..) as yk
+  int r0 = kb0 * M::TB;
+  issue_band(r0);
+  {
+    constexpr int NV = M::SH * M::SV;
+#pragma unroll
+    for (int k = 0; k < cdiv(NV, kThreads); ++k) {
+      const int q = tid + k * kThreads;
+      if (q < NV) {
+        const int r = q / M::SV, g = q - r * M::SV;
+        const int gr = r0 - 2 * R + r, gc = tx0 - M::CA + 4 * g;
+        float xv[4] = {0.f, 0.f, 0.f, 0.f}, pv[4] = {0.f, 0.f, 0.f, 0.f}, out[4];
+        if (!EDGE || (gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) {
+          ld_vec<float, 4>(xs + (unsigned)(gr * n1 + gc), xv);
+          ld_vec<float, 4>(xps + (unsigned)(gr * n1 + gc), pv);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float d = xv[v] - pv[v];
+          d = d * a;
+          out[v] = d + xv[v];
+        }
+        st_vec<float, 4>(W + (M::TB + r) * M::AP + 4 * g, out);  // where band 0's shift picks them up
+      }
+    }
+  }
+  int el = 0, eq = 0;  // row-major epilogue lane: band row el, 16-B column vector eq
+  Stage<float, 6>::lane(tid, el, eq);
+  const KP kp = (KP)__builtin_amdgcn_kernarg_segment_ptr();  // p is the first kernel argument
+  for (int k = 0; k < nb; ++k, r0 += M::TB) {
+    const bool has_next = k + 1 < nb;
+    // shift sources (W rows TB .. TB + SH - 1; band 0: the prologue's rows) into registers before the barrier
+    constexpr int NSH = M::SH * M::SV;
+    constexpr int KSH = cdiv(NSH, kThreads);
+    f32x4 shv[KSH];
+#pragma unroll
+    for (int q = 0; q < KSH; ++q) {
+      const int t = tid + q * kThreads;
+      shv[q] = *reinterpret_cast<const f32x4*>(W + (M::TB + (t < NSH ? t / M::SV : 0)) * M::AP + 4 * (t < NSH ? t % M::SV : 0));
+    }
+    if (k > 0) wait_vm<1>();  // this wave's DMA(k) landed; band k-1's x_new store may stay in flight
+    else wait_vm<0>();
+    lds_barrier();  // B1: every wave's DMA(k) landed; band k-1 is done with W / PT / O
+    // H^T y of this band's epilogue pixels, into registers (counted by hand)
+    f32x4 bq;
+    {
+      const int gr = r0 + el, gc = tx0 + 4 * eq;
+      const float* ptr = (!EDGE || (gr < n0 && gc < n1)) ? bs + (unsigned)(gr * n1 + gc) : g_zero_page;
+      asm_load_b4(bq, ptr);
+    }
+#pragma unroll
+    for (int q = 0; q < KSH; ++q) {
+      const int t = tid + q * kThreads;
+      if (t < NSH) {
+        const int r = t / M::SV, g = t - r * M::SV;
+        *reinterpret_cast<f32x4*>(W + r * M::AP + 4 * g) = shv[q];
+      }
+    }
+    {  // S -> yk rows SH .. SH + TB - 1 of W
+#pragma unroll
+      for (int q = 0; q < cdiv(M::SSLOTS, kThreads); ++q) {
+        const int t = tid + q * kThreads;
+        if (t < M::SSLOTS) {
+          const int r = t / M::SV, g = t - r * M::SV;
+          float xv[4], pv[4], out[4];
+          ld_vec<float, 4>(S + 4 * t, xv);
+          ld_vec<float, 4>(S + 4 * (M::SSLOTS + t), pv);
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            float d = xv[v] - pv[v];
+            d = d * a;
+            out[v] = d + xv[v];
+          }
+          st_vec<float, 4>(W + (M::SH + r) * M::AP + 4 * g, out);
+        }
+      }
+    }
+    lds_barrier();  // B2: W complete, S read by every wave
+    if (has_next) issue_band(r0 + M::TB);
+    if (!(diag & 1)) march_pass_a<R, EDGE>(kp, W, PT, KT, r0);
+    lds_barrier();  // B3: PT complete
+    if (!(diag & 1)) march_pass_b<R, EDGE>(kp, W, PT, KT, O, r0, tx0);
+    lds_barrier();  // B4: O complete
+    if (has_next) wait_vm<M::NDW>();  // H^T y landed; DMA(k+1) may stay in flight
+    else wait_vm<0>();
+    asm volatile("" : "+v"(bq));
+    {
+      float g[4], y[4];
+      ld_vec<float, 4>(O + M::oidx(el, 4 * eq), g);
+      ld_vec<float, 4>(W + (el + 2 * R) * M::AP + M::CA + 4 * eq, y);
+      const float bv[4] = {bq[0], bq[1], bq[2], bq[3]};
+      const float tau = kp->tau, pw = kp->pw;
+      const int prox = kp->prox;
+      float xo[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {  // finish_run's arithmetic
+        float gsum = g[w] - bv[w];
+        float z = gsum * (-tau);
+        z = z + y[w];
+        xo[w] = apply_prox<float>(prox, z, pw);
+      }
+      const int gr = r0 + el, gc = tx0 + 4 * eq;
+      // exactly ONE store instruction per lane and band, whatever the lane's position (the top-of-band
+      // wait counts it): out-of-image lanes write the sink page (n1 % 4 == 0: a vector is wholly in or out)
+      float* dst = (!EDGE || (gr < n0 && gc < n1)) ? xns + (unsigned)(gr * n1 + gc) : g_sink_page;
+      *reinterpret_cast<float4*>(dst) = make_float4(xo[0], xo[1], xo[2], xo[3]);
+    }
+  }
+}
+
+template <int R>
+__global__ void __launch_bounds__(kThreads, 4) pgd_march_kernel(PgdParams<float> p, const float* __restrict__ x,
+                                                              const float* __restrict__ xp,
+                                                              const float* __restrict__ b, float* __restrict__ xn,
+                                                              int sb, int nseg, int nstrips, unsigned nunits,
+                                                              int diag) {
+  using M = March<R>;
+  extern __shared__ __attribute__((aligned(16))) float smem_m[];
+  const int tid = threadIdx.x;
+  const int n0 = p.n0, n1 = p.n1;
+  const unsigned unit = xcd_tile(blockIdx.x, nunits);
+  const unsigned per_img = (unsigned)nseg * (unsigned)nstrips;
+  const unsigned s = unit / per_img;
+  const unsigned rem = unit - s * per_img;
+  const int seg = (int)(rem / (unsigned)nstrips);
+  const int tx0 = (int)(rem - (unsigned)seg * (unsigned)nstrips) * TX;
+  const int nbands = (n0 + M::TB - 1) / M::TB;
+  const int kb0 = seg * sb;
+  const int nb = (kb0 + sb <= nbands ? sb : nbands - kb0);
   const int64_t img = (int64_t)n0 * n1;
-  const unsigned tpi = (unsigned)p.tiles0 * (unsigned)p.tiles1;
-  // XCD-banded tile order: workgroup group g8 = blockIdx % 8 owns a contiguous band of tiles and its
-  // G/8 workgroups sweep that band together (halo re-reads of neighbouring tiles hit the XCD's L2)
-  const unsigned G8 = gridDim.x >> 3, g8 = blockIdx.x & 7u, j = blockIdx.x >> 3;
-  const unsigned q8 = p.ntiles >> 3, r8 = p.ntiles & 7u;
-  const unsigned band_lo = g8 * q8 + (g8 < r8 ? g8 : r8);
-  const unsigned band_hi = band_lo + q8 + (g8 < r8 ? 1u : 0u);
-  auto tile_at = [&](unsigned t) {
-    TileOf o;
-    o.tile = t;
-    o.s = t / tpi;
-    const unsigned tr = t - o.s * tpi;
-    const unsigned trow = tr / (unsigned)p.tiles1;
-    o.ty0 = (int)trow * TY;
-    o.tx0 = (int)(tr - trow * (unsigned)p.tiles1) * TX;
-    return o;
-  };
-  auto interior_at = [&](const TileOf& o) {
-    return o.ty0 - 2 * R >= 0 && o.ty0 + TY + 2 * R <= n0 && o.tx0 - L::CA >= 0 && o.tx0 + TX + L::CA <= n1;
-  };
-  auto issue_tile = [&](const TileOf& o) {
-    const float* xs = x + (int64_t)o.s * img;
-    const float* xps = xp + (int64_t)o.s * img;
-    if (interior_at(o)) issue_windows<R, false>(S, xs, xps, o.ty0, o.tx0, n0, n1);
-    else issue_windows<R, true>(S, xs, xps, o.ty0, o.tx0, n0, n1);
-  };
+  const float* xs = x + (int64_t)s * img;
+  const float* xps = xp + (int64_t)s * img;
+  const float* bs = b + (int64_t)(s % (unsigned)p.y_images) * img;
+  float* xns = xn + (int64_t)s * img;
+  float* KT = smem_m + M::KT_OFF;
   if (tid < 2 * R + 1) {
     KT[tid] = p.k0[tid];
     KT[kKT + tid] = p.k1[tid];
   }
-  unsigned t = band_lo + j;
-  if (t < band_hi) issue_tile(tile_at(t));
-  bool prev_interior = false;  // stores of the previous tile: a known count only for interior tiles
-  const PgdParams<float>* pp = &p;
-  for (; t < band_hi; t += G8) {
-    // re-read the solver constants (taps, lam, tau, ...) from the kernel-argument segment in every
-    // iteration: hoisted out of the loop they would pin ~100 SGPRs and spill to VGPR lanes
-    asm volatile("" : "+s"(pp));
-    const PgdParams<float>& q = *pp;
-    const TileOf o = tile_at(t);
-    const bool interior = interior_at(o);
-    const unsigned tn = t + G8;
-    const bool has_next = tn < band_hi;
-    // 1. this wave's DMA of tile t landed (only the previous tile's 4 x_new stores may stay in flight)
-    if (prev_interior) wait_vm<4>();
-    else wait_vm<0>();
-    lds_barrier();  // every wave's DMA landed; the previous pass B is done with A / PT / red
-    const float* xs = x + (int64_t)o.s * img;
-    const float* bs = b + (int64_t)(o.s % (unsigned)p.y_images) * img;
-    float* xns = xn + (int64_t)o.s * img;
-    // 2. H^T y of this tile into registers (4 x dwordx2 per thread), counted by hand
-    float2 bq[4];
-    if (interior) issue_b<R, false>(bq, bs, o.ty0, o.tx0, n0, n1);
-    else issue_b<R, true>(bq, bs, o.ty0, o.tx0, n0, n1);
-    // 3. raw windows -> yk
-    convert_windows<R>(S, A, q.a);
-    lds_barrier();  // A complete; S free
-    // 4. next tile's windows in flight during passes A and B
-    if (has_next) issue_tile(tile_at(tn));
-    double part_d = 0.0, part_x = 0.0;
-    if (interior) {
-      pass_a<float, R, false>(q, A, PT, KT, o.ty0);
-      lds_barrier();
-      if (has_next) wait_vm<P::NDW>();
-      else wait_vm<0>();
-      asm volatile("" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
-      const bool want = partials != nullptr;
-      pass_b<float, R, false>(q, A, PT, KT, o.ty0, o.tx0,
-                           [&](int, int u, int gr, int gc, const float(&g)[2], const float(&y)[2]) {
-                             const float bv[2] = {bq[u].x, bq[u].y};
-                             finish_run<float, 2, false>(q, gr, gc, g, bv, y, xs, xns, want, part_d, part_x);
-                           });
-    } else {
-      pass_a<float, R, true>(q, A, PT, KT, o.ty0);
-      lds_barrier();
-      if (has_next) wait_vm<P::NDW>();
-      else wait_vm<0>();
-      asm volatile("" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
-      const bool want = partials != nullptr;
-      pass_b<float, R, true>(q, A, PT, KT, o.ty0, o.tx0,
-                           [&](int, int u, int gr, int gc, const float(&g)[2], const float(&y)[2]) {
-                             const float bv[2] = {bq[u].x, bq[u].y};
-                             finish_run<float, 2, true>(q, gr, gc, g, bv, y, xs, xns, want, part_d, part_x);
-                           });
-    }
-    if (partials) fold_partials(part_d, part_x, red, partials, o.tile, [] { lds_barrier(); });
-    prev_interior = interior && partials == nullptr;
+  const bool interior = tx0 - M::CA >= 0 && tx0 + TX + M::CA <= n1 && kb0 * M::TB - 2 * R >= 0 &&
+                        (kb0 + nb) * M::TB + 2 * R <= n0;
+  if (interior) march_run<R, false>(p, smem_m, kb0, nb, tx0, xs, xps, bs, xns, diag);
+  else march_run<R, true>(p, smem_m, kb0, nb, tx0, xs, xps, bs, xns, diag);
+}
+
+struct MarchPlan {
+  int sb, nseg, nstrips;
+  unsigned nunits;
+};
+
+// bands per workgroup: enough units for ~4 workgroups per CU, whole strips at most
+inline int march_plan(int64_t stack, int n0, int n1, MarchPlan& mp) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return PXA_ERR_UNSUPPORTED;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
   }
+  const int64_t nbands = (n0 + 15) / 16;
+  mp.nstrips = (n1 + TX - 1) / TX;
+  const int64_t total = stack * nbands * mp.nstrips;
+  int64_t sb = (total + 4 * (int64_t)cus - 1) / (4 * (int64_t)cus);
+  if (tuning(PXA_TUNE_MARCH_BANDS) > 0) sb = tuning(PXA_TUNE_MARCH_BANDS);
+  sb = sb < 1 ? 1 : (sb > nbands ? nbands : sb);
+  mp.sb = (int)sb;
+  mp.nseg = (int)((nbands + sb - 1) / sb);
+  const int64_t nu = stack * mp.nseg * mp.nstrips;
+  if (nu > 0x7fffffff) return PXA_ERR_UNSUPPORTED;
+  mp.nunits = (unsigned)nu;
+  return PXA_OK;
 }
 
 template <int R>
-int launch_pgd_persistent(const PgdParams<float>& p, const void* x, const void* xp, const void* b, void* xn,
-                          double* partials, hipStream_t s) {
-  using P = V5<R>;
-  auto kern = pgd_tv2d_persistent<R>;
-  static int grid_cap = 0;  // resident workgroups on this device (2 per CU by LDS), multiple of 8
-  if (grid_cap == 0) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P::BYTES);
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return PXA_ERR_UNSUPPORTED;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return PXA_ERR_UNSUPPORTED;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kern, kThreads, P::BYTES) != hipSuccess)
-      return PXA_ERR_UNSUPPORTED;
-    if (per < 1) per = 1;
-    if (per > 2) per = 2;
-    grid_cap = cus * per;
+int launch_pgd_march(const PgdParams<float>& p, const void* x, const void* xp, const void* b, void* xn,
+                     hipStream_t s) {
+  using M = March<R>;
+  auto kern = pgd_march_kernel<R>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::BYTES);
+    attr_set = true;
   }
-  int grid = grid_cap;
-  if ((int64_t)grid > (int64_t)p.ntiles) grid = (int)p.ntiles;
-  grid = grid < 8 ? 8 : (grid & ~7);  // the XCD banding needs a multiple of 8 (idle groups just exit)
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), P::BYTES, s, p, (const float*)x, (const float*)xp,
-                     (const float*)b, (float*)xn, partials);
+  MarchPlan mp;
+  const int st = march_plan(p.stack, p.n0, p.n1, mp);
+  if (st != PXA_OK) return st;
+  hipLaunchKernelGGL(kern, dim3(mp.nunits), dim3(kThreads), M::BYTES, s, p, (const float*)x, (const float*)xp,
+                     (const float*)b, (float*)xn, mp.sb, mp.nseg, mp.nstrips, mp.nunits, tuning(PXA_TUNE_PGD_DIAG));
   return last_launch_status();
 }
+
+
+thread_local int g_last_pgd_kernel = 0;  // pxa_pgd_tv2d_last_kernel
 
 template <typename T>
 int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
@@ -875,31 +1103,36 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.prox = prox;
   p.prio = tuning(PXA_TUNE_PGD_PRIO);
   if constexpr (sizeof(T) == 4) {
-    // persistent LDS-DMA kernel (opt-in, PXA_TUNE_PGD_KERNEL = 5): 16-B vectors along rows and 32-bit
-  // in-image offsets.  Measured slower than the tile kernel at 2048^2 (50 vs 27 us): see its header.
-    if (p.vec_ok && n0 * n1 <= 0x7fffffff && tuning(PXA_TUNE_PGD_KERNEL) == 5) {
+    // march kernel (PXA_TUNE_PGD_KERNEL = 5 forces it where it applies): fp32, R <= 6, 16-B rows,
+    // 32-bit in-image offsets, no RelError partials
+    const int knob = tuning(PXA_TUNE_PGD_KERNEL);
+    if (p.vec_ok && n0 * n1 <= 0x7fffffff && R <= 6 && partials == nullptr && knob == 5) {
+      int st;
       switch (R) {
-        case 1: return launch_pgd_persistent<1>(p, x, x_prev, hty, x_new, partials, s);
-        case 2: return launch_pgd_persistent<2>(p, x, x_prev, hty, x_new, partials, s);
-        case 3: return launch_pgd_persistent<3>(p, x, x_prev, hty, x_new, partials, s);
-        case 4: return launch_pgd_persistent<4>(p, x, x_prev, hty, x_new, partials, s);
-        case 5: return launch_pgd_persistent<5>(p, x, x_prev, hty, x_new, partials, s);
-        case 6: return launch_pgd_persistent<6>(p, x, x_prev, hty, x_new, partials, s);
-        case 7: return launch_pgd_persistent<7>(p, x, x_prev, hty, x_new, partials, s);
-        default: return launch_pgd_persistent<8>(p, x, x_prev, hty, x_new, partials, s);
+        case 1: st = launch_pgd_march<1>(p, x, x_prev, hty, x_new, s); break;
+        case 2: st = launch_pgd_march<2>(p, x, x_prev, hty, x_new, s); break;
+        case 3: st = launch_pgd_march<3>(p, x, x_prev, hty, x_new, s); break;
+        case 4: st = launch_pgd_march<4>(p, x, x_prev, hty, x_new, s); break;
+        case 5: st = launch_pgd_march<5>(p, x, x_prev, hty, x_new, s); break;
+        default: st = launch_pgd_march<6>(p, x, x_prev, hty, x_new, s); break;
       }
+      if (st == PXA_OK) g_last_pgd_kernel = 2;
+      return st;
     }
   }
+  int st;
   switch (R) {
-    case 1: return launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s);
-    case 2: return launch_pgd<T, 2>(p, x, x_prev, hty, x_new, partials, s);
-    case 3: return launch_pgd<T, 3>(p, x, x_prev, hty, x_new, partials, s);
-    case 4: return launch_pgd<T, 4>(p, x, x_prev, hty, x_new, partials, s);
-    case 5: return launch_pgd<T, 5>(p, x, x_prev, hty, x_new, partials, s);
-    case 6: return launch_pgd<T, 6>(p, x, x_prev, hty, x_new, partials, s);
-    case 7: return launch_pgd<T, 7>(p, x, x_prev, hty, x_new, partials, s);
-    default: return launch_pgd<T, 8>(p, x, x_prev, hty, x_new, partials, s);
+    case 1: st = launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 2: st = launch_pgd<T, 2>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 3: st = launch_pgd<T, 3>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 4: st = launch_pgd<T, 4>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 5: st = launch_pgd<T, 5>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 6: st = launch_pgd<T, 6>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 7: st = launch_pgd<T, 7>(p, x, x_prev, hty, x_new, partials, s); break;
+    default: st = launch_pgd<T, 8>(p, x, x_prev, hty, x_new, partials, s); break;
   }
+  if (st == PXA_OK) g_last_pgd_kernel = 1;
+  return st;
 }
 
 }  // namespace
@@ -908,6 +1141,8 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
 using namespace pxa;
 
 extern "C" {
+
+int pxa_pgd_tv2d_last_kernel(void) { return g_last_pgd_kernel; }
 
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1) {
   int64_t t = stack * ((n0 + TY - 1) / TY) * ((n1 + TX - 1) / TX);
