@@ -57,7 +57,8 @@ extern "C" {
                                workgroup by (block >> 8) & 3, 2 memory phases high / compute low,
                                3 static by (block >> 3) & 3, 4 = 1 + 2 */
 #define PXA_TUNE_PGD_DIAG 3 /* march-kernel timing probes (WRONG results, measurement only): bit 0 no
-                               passes A / B, bit 1 no LDS-DMA */
+                               passes A / B, bit 1 no LDS-DMA, bit 2 no pass A, bit 3 no pass B,
+                               bit 4 no TV term */
 #define PXA_TUNE_MARCH_BANDS 4 /* march kernel: 16-row bands per workgroup (0 auto: ~4 workgroups per CU) */
 #define PXA_TUNE_COUNT 8
 

@@ -66,9 +66,10 @@ __device__ inline void set_prio(int lvl) {
   }
 }
 
-// The TV stencil's two-product sums are written as explicit fma(a, b, c * d): under fp-contract=fast
-// the compiler may otherwise fuse either product, and then the tile and march kernels (different
-// register blocking, different instruction selection) would round differently.
+// Every multiply-add outside the Toeplitz sweeps is written as an explicit fma (the TV stencil's
+// two-product sums as fma(a, b, c * d)): under fp-contract=fast the compiler fuses or not, and picks
+// which product to fuse, per code position, so the tile and march kernels (different blocking, code
+// layout per radius) would otherwise round differently at a few pixels.
 // q-weight: lam / max(|v|, mu)  (so that q = w v = lam (v - prox_{mu L21}(v)) / mu).
 template <typename T>
 __device__ inline T tv_weight(T n2, T lam, T mu, T inv_mu) {
@@ -129,9 +130,7 @@ __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0
       T out[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        T d = xv[k][v] - pv[k][v];
-        d = d * p.a;
-        out[v] = d + xv[k][v];
+        out[v] = fma(xv[k][v] - pv[k][v], p.a, xv[k][v]);  // (x - x_prev) * a + x, one rounding site
       }
       st_vec<T, V>(A + r * L::AP + V * g, out);
     }
@@ -176,8 +175,7 @@ __device__ inline void finish_run(const PgdParams<T>& p, int gr, int gc, const T
 #pragma unroll
   for (int w = 0; w < CW; ++w) {
     T gsum = g[w] - bv[w];  // (G yk + Grad^T q) - H^T y
-    T z = gsum * (-p.tau);
-    z = z + yc[w];
+    T z = fma(gsum, -p.tau, yc[w]);
     xo[w] = apply_prox<T>(p.prox, z, p.pw);
   }
   if (!EDGE) {
@@ -679,8 +677,8 @@ __device__ inline void ghost_fix2(int i0, int n, int q0, const float* __restrict
 #pragma unroll
         for (int s = -R; s <= R; ++s) {
           const float2 w = *reinterpret_cast<const float2*>(src + (pp + s - q0) * PS);
-          gh[m][0] = k[s + R] * w.x + gh[m][0];
-          gh[m][1] = k[s + R] * w.y + gh[m][1];
+          gh[m][0] = fma(k[s + R], w.x, gh[m][0]);
+          gh[m][1] = fma(k[s + R], w.y, gh[m][1]);
         }
       }
     }
@@ -693,8 +691,8 @@ __device__ inline void ghost_fix2(int i0, int n, int q0, const float* __restrict
         const int t = i - (pg + m);
         if (t < -R || t > R) continue;
         const float kk = kt[t + R];
-        acc[o][0] = acc[o][0] - kk * gh[m][0];
-        acc[o][1] = acc[o][1] - kk * gh[m][1];
+        acc[o][0] = fma(-kk, gh[m][0], acc[o][0]);
+        acc[o][1] = fma(-kk, gh[m][1], acc[o][1]);
       }
     }
   }
@@ -730,8 +728,8 @@ __device__ inline void march_issue(float* S, const float* xs, const float* xps, 
 }
 
 // pass A of one band: PT[c][r] = (G0 yk)[r0 + r][c] for the 16 band rows and all AC window columns
-template <int R, bool EDGE>
-__device__ inline void march_pass_a(KP p, const float* W, float* PT, const float* KT, int r0) {
+template <int R, bool EDGE, typename PP>
+__device__ inline void march_pass_a(PP p, const float* W, float* PT, const float* KT, int r0) {
   using M = March<R>;
   // lane -> (row group a = lane & 3, column pair b): 11 column pairs per wave.  A 32-lane ds_read_b64
   // group spans a = 0..3 x 8 consecutive b: rows 4 AP = 16 or 48 mod 64 dwords apart, conflict-free; an
@@ -753,9 +751,9 @@ __device__ inline void march_pass_a(KP p, const float* W, float* PT, const float
 }
 
 // pass B of one band: g = G1 (PT rows) + Grad^T q at 2 x 2 pixels per thread, parked in O
-template <int R, bool EDGE>
-__device__ inline void march_pass_b(KP p, const float* W, const float* PT, const float* KT, float* O, int r0,
-                                    int tx0) {
+template <int R, bool EDGE, typename PP>
+__device__ inline void march_pass_b(PP p, const float* W, const float* PT, const float* KT, float* O, int r0,
+                                    int tx0, bool tv_on = true) {
   using M = March<R>;
   constexpr int CA = M::CA;
   const int n0 = p->n0, n1 = p->n1;
@@ -793,7 +791,8 @@ __device__ inline void march_pass_b(KP p, const float* W, const float* PT, const
     }
   };
   float tv[2][2];
-  if (p->tv) {
+  const bool use_tv = p->tv && tv_on;
+  if (use_tv) {
     float yr[4], yn[4];
     yrow(0, yr);
     yrow(1, yn);
@@ -823,7 +822,7 @@ __device__ inline void march_pass_b(KP p, const float* W, const float* PT, const
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     float g0 = acc[0][u], g1 = acc[1][u];
-    if (p->tv) {
+    if (use_tv) {
       g0 = g0 + tv[u][0];
       g1 = g1 + tv[u][1];
     }
@@ -868,9 +867,7 @@ __device__ inline void march_run(const PgdParams<float>& p, float* smem, int kb0
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          float d = xv[v] - pv[v];
-          d = d * a;
-          out[v] = d + xv[v];
+          out[v] = fma(xv[v] - pv[v], a, xv[v]);
         }
         st_vec<float, 4>(W + (M::TB + r) * M::AP + 4 * g, out);  // where band 0's shift picks them up
       }
@@ -918,20 +915,16 @@ __device__ inline void march_run(const PgdParams<float>& p, float* smem, int kb0
           ld_vec<float, 4>(S + 4 * t, xv);
           ld_vec<float, 4>(S + 4 * (M::SSLOTS + t), pv);
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            float d = xv[v] - pv[v];
-            d = d * a;
-            out[v] = d + xv[v];
-          }
+          for (int v = 0; v < 4; ++v) out[v] = fma(xv[v] - pv[v], a, xv[v]);
           st_vec<float, 4>(W + (M::SH + r) * M::AP + 4 * g, out);
         }
       }
     }
     lds_barrier();  // B2: W complete, S read by every wave
     if (has_next) issue_band(r0 + M::TB);
-    if (!(diag & 1)) march_pass_a<R, EDGE>(kp, W, PT, KT, r0);
+    if (!(diag & 5)) march_pass_a<R, EDGE>(kp, W, PT, KT, r0);
     lds_barrier();  // B3: PT complete
-    if (!(diag & 1)) march_pass_b<R, EDGE>(kp, W, PT, KT, O, r0, tx0);
+    if (!(diag & 9)) march_pass_b<R, EDGE>(kp, W, PT, KT, O, r0, tx0, (diag & 16) == 0);
     lds_barrier();  // B4: O complete
     if (has_next) wait_vm<M::NDW>();  // H^T y landed; DMA(k+1) may stay in flight
     else wait_vm<0>();
@@ -947,8 +940,7 @@ __device__ inline void march_run(const PgdParams<float>& p, float* smem, int kb0
 #pragma unroll
       for (int w = 0; w < 4; ++w) {  // finish_run's arithmetic
         float gsum = g[w] - bv[w];
-        float z = gsum * (-tau);
-        z = z + y[w];
+        float z = fma(gsum, -tau, y[w]);
         xo[w] = apply_prox<float>(prox, z, pw);
       }
       const int gr = r0 + el, gc = tx0 + 4 * eq;

@@ -151,7 +151,7 @@ __device__ inline void ghost_fix(int i0, int n, int q0, const T* __restrict__ sr
           const VT t = *reinterpret_cast<const VT*>(src + (pp + s - q0) * PS);
           __builtin_memcpy(&w[0], &t, sizeof(VT));
 #pragma unroll
-          for (int v = 0; v < V; ++v) gh[m][v] = k[s + R] * w[v] + gh[m][v];
+          for (int v = 0; v < V; ++v) gh[m][v] = fma(k[s + R], w[v], gh[m][v]);
         }
       }
     }
@@ -165,7 +165,7 @@ __device__ inline void ghost_fix(int i0, int n, int q0, const T* __restrict__ sr
         if (t < -R || t > R) continue;
         const T kk = kt[t + R];
 #pragma unroll
-        for (int v = 0; v < V; ++v) acc[o][v] = acc[o][v] - kk * gh[m][v];
+        for (int v = 0; v < V; ++v) acc[o][v] = fma(-kk, gh[m][v], acc[o][v]);
       }
     }
   }
