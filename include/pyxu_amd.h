@@ -58,7 +58,7 @@ extern "C" {
                                3 static by (block >> 3) & 3, 4 = 1 + 2 */
 #define PXA_TUNE_PGD_DIAG 3 /* march-kernel timing probes (WRONG results, measurement only): bit 0 no
                                passes A / B, bit 1 no LDS-DMA, bit 2 no pass A, bit 3 no pass B,
-                               bit 4 no TV term */
+                               bit 4 no TV term, bit 5 timing trace (pxa_pgd_march_trace) */
 #define PXA_TUNE_MARCH_BANDS 4 /* march kernel: 16-row bands per workgroup (0 auto: ~4 workgroups per CU) */
 #define PXA_TUNE_COUNT 8
 
@@ -367,6 +367,9 @@ int pxa_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* 
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
 int pxa_pgd_tv2d_last_kernel(void);
+/* Diagnostics: s_memtime stamps of the march kernel's last launch under PXA_TUNE_PGD_DIAG bit 5
+ * (workgroups 0 and grid/2, waves 0..3, bands 0..15, 8 points per band; n <= 1024 words). */
+int pxa_pgd_march_trace(uint64_t* host_out, int n);
 int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
                       const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,

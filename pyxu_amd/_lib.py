@@ -73,6 +73,7 @@ EXPORTS = {
     "pxa_transpose": (i32, [i32, i64, i64, vp, vp, vp]),
     "pxa_pgd_tv2d_partials_count": (i32, [i64, i64, i64]),
     "pxa_pgd_tv2d_last_kernel": (i32, []),
+    "pxa_pgd_march_trace": (i32, [vp, i32]),
     "pxa_pgd_tv2d_step": (
         i32,
         [i32, i64, i64, i64, i64, i32, P_i32, P_f64, i32, P_i32, P_f64, f64, f64, f64, f64, f64, f64, i32, f64,

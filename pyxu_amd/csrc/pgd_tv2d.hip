@@ -560,7 +560,11 @@ int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void*
 // instruction of the last wave repeats the last slot range with identical bytes), and out-of-image
 // granules DMA from a zero page (n1 % 4 == 0: a 16-B granule is wholly inside or outside).
 __device__ __attribute__((aligned(16))) float g_zero_page[4];
-__device__ __attribute__((aligned(16))) float g_sink_page[4];  // target of the march epilogue's out-of-image lanes
+__device__ __attribute__((aligned(16))) float g_sink_page[4];
+// march-kernel timing trace (PXA_TUNE_PGD_DIAG bit 5): s_memtime of wave w of two workgroups at 8 points of
+// each of their first 16 bands, staged in LDS beyond the kernel's own carve, dumped at exit
+constexpr int kTraceWords = 2 * 4 * 16 * 8;
+__device__ unsigned long long g_march_trace[kTraceWords];  // target of the march epilogue's out-of-image lanes
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -618,7 +622,8 @@ struct March {
   static constexpr int PT_OFF = S_OFF + NSLOT * 4;
   static constexpr int O_OFF = PT_OFF + AC * PTP;
   static constexpr int KT_OFF = O_OFF + TB * OP;
-  static constexpr size_t BYTES = (size_t)(KT_OFF + 2 * kKT) * 4;
+  static constexpr int GH_OFF = KT_OFF + 2 * kKT;    // boundary-column ghost terms (march_ghost_cols)
+  static constexpr size_t BYTES = (size_t)(GH_OFF + 2 * R * TB) * 4;
   static constexpr int NPA = (TB / 4) * (AC / 2);     // pass-A items: 4 rows x 2 columns
   static constexpr int NPB = (TB / 2) * (TX / 2);     // pass-B items: 2 rows x 2 columns
   static_assert(R >= 1 && R <= 6, "march kernel radius");
@@ -698,6 +703,54 @@ __device__ inline void ghost_fix2(int i0, int n, int q0, const float* __restrict
   }
 }
 
+// Boundary columns of pass B, computed cooperatively (edge strips only): GH[side][m][r] = sum_s k1[s]
+// PT[ghost column pg + m + s][band row r], the (H1 G0 yk) values at the R zero-padded ghost columns on
+// each side -- ghost_fix2's gh[m] with the same fma order.  ghost_fix2 would have the few lanes that own
+// columns within R of the border compute all of them (one 13-tap sum per ghost column per lane), which
+// held one wave ~6 500 cycles per band while the others waited at the next barrier.
+template <int R, typename PP>
+__device__ inline void march_ghost_cols(PP p, const float* PT, float* GH, int tx0, int n1) {
+  using M = March<R>;
+  const int t = threadIdx.x;
+  if (t < 2 * R * M::TB) {
+    const int side = t / (R * M::TB), m = (t / M::TB) % R, r = t % M::TB;
+    const int row = (side == 0 ? -R : n1) + m - (tx0 - M::CA);  // PT row of the ghost column
+    float g = 0.0f;
+    if (row - R >= 0 && row + R < M::AC) {  // else no output of this strip uses it
+#pragma unroll
+      for (int q = -R; q <= R; ++q) g = fma(p->k1[q + R], PT[(row + q) * M::PTP + r], g);
+    }
+    GH[(side * R + m) * M::TB + r] = g;
+  }
+}
+
+// ghost_fix2's correction step for pass B with the ghost terms read from GH (same terms, same order)
+template <int R, int NO>
+__device__ inline void ghost_cols_fix(int i0, int n, int rr, const float* __restrict__ GH, const float* __restrict__ kt,
+                                      float (&acc)[NO][2]) {
+  using M = March<R>;
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    const int pg = side == 0 ? -R : n;
+    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
+    if (!hit) continue;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = i0 + o;
+      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        const int t = i - (pg + m);
+        if (t < -R || t > R) continue;
+        const float kk = kt[t + R];
+        const float2 gh = *reinterpret_cast<const float2*>(GH + (side * R + m) * M::TB + rr);
+        acc[o][0] = fma(-kk, gh.x, acc[o][0]);
+        acc[o][1] = fma(-kk, gh.y, acc[o][1]);
+      }
+    }
+  }
+}
+
 // this wave's NDW LDS-DMA instructions: x / x_prev rows row0 .. row0 + TB - 1 of the strip -> S
 template <int R, bool EDGE>
 __device__ inline void march_issue(float* S, const float* xs, const float* xps, int row0, int tx0, int n0, int n1) {
@@ -741,7 +794,7 @@ __device__ inline void march_pass_a(PP p, const float* W, float* PT, const float
     sweep2<R, 4, M::AP>(W + (4 * a) * M::AP + 2 * b, p->g0, acc);
     const int n0 = p->n0;
     const bool edge_rows = EDGE && (r0 < R || r0 + M::TB > n0 - R);
-    if (edge_rows) ghost_fix2<R, 4, M::AP>(r0 + 4 * a, n0, r0 - 2 * R, W + 2 * b, KT, KT, acc);
+    if (edge_rows) ghost_fix2<R, 4, M::AP>(r0 + 4 * a, n0, r0 - 2 * R, W + 2 * b, p->k0, KT, acc);
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
       const float colv[4] = {acc[0][w], acc[1][w], acc[2][w], acc[3][w]};
@@ -818,7 +871,7 @@ __device__ inline void march_pass_b(PP p, const float* W, const float* PT, const
   float acc[2][2];  // acc[w][u]: column c0 + w, band row 2i + u
   sweep2<R, 2, M::PTP>(PT + (CA - 2 * R + c0) * M::PTP + 2 * i, p->g1, acc);
   const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n1 - R);
-  if (edge_cols) ghost_fix2<R, 2, M::PTP>(tx0 + c0, n1, tx0 - CA, PT + 2 * i, KT + kKT, KT + kKT, acc);
+  if (edge_cols) ghost_cols_fix<R, 2>(tx0 + c0, n1, 2 * i, KT + M::GH_OFF - M::KT_OFF, KT + kKT, acc);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     float g0 = acc[0][u], g1 = acc[1][u];
@@ -876,8 +929,14 @@ __device__ inline void march_run(const PgdParams<float>& p, float* smem, int kb0
   int el = 0, eq = 0;  // row-major epilogue lane: band row el, 16-B column vector eq
   Stage<float, 6>::lane(tid, el, eq);
   const KP kp = (KP)__builtin_amdgcn_kernarg_segment_ptr();  // p is the first kernel argument
+  unsigned long long* ts = reinterpret_cast<unsigned long long*>(smem + M::BYTES / 4);
+  const bool tracing = (diag & 32) != 0;
+  auto mark = [&](int k, int pt) {
+    if (tracing && (tid & 63) == 0 && k < 16) ts[((tid >> 6) * 16 + k) * 8 + pt] = clock64();
+  };
   for (int k = 0; k < nb; ++k, r0 += M::TB) {
     const bool has_next = k + 1 < nb;
+    mark(k, 0);
     // shift sources (W rows TB .. TB + SH - 1; band 0: the prologue's rows) into registers before the barrier
     constexpr int NSH = M::SH * M::SV;
     constexpr int KSH = cdiv(NSH, kThreads);
@@ -890,6 +949,7 @@ __device__ inline void march_run(const PgdParams<float>& p, float* smem, int kb0
     if (k > 0) wait_vm<1>();  // this wave's DMA(k) landed; band k-1's x_new store may stay in flight
     else wait_vm<0>();
     lds_barrier();  // B1: every wave's DMA(k) landed; band k-1 is done with W / PT / O
+    mark(k, 1);
     // H^T y of this band's epilogue pixels, into registers (counted by hand)
     f32x4 bq;
     {
@@ -921,13 +981,22 @@ __device__ inline void march_run(const PgdParams<float>& p, float* smem, int kb0
       }
     }
     lds_barrier();  // B2: W complete, S read by every wave
+    mark(k, 2);
     if (has_next) issue_band(r0 + M::TB);
     if (!(diag & 5)) march_pass_a<R, EDGE>(kp, W, PT, KT, r0);
+    mark(k, 3);
     lds_barrier();  // B3: PT complete
+    if (EDGE && (tx0 < R || tx0 + TX > n1 - R)) {  // edge strips: the boundary-column ghost terms
+      march_ghost_cols<R>(kp, PT, smem + M::GH_OFF, tx0, n1);
+      lds_barrier();
+    }
+    mark(k, 4);
     if (!(diag & 9)) march_pass_b<R, EDGE>(kp, W, PT, KT, O, r0, tx0, (diag & 16) == 0);
+    mark(k, 5);
     lds_barrier();  // B4: O complete
     if (has_next) wait_vm<M::NDW>();  // H^T y landed; DMA(k+1) may stay in flight
     else wait_vm<0>();
+    mark(k, 6);
     asm volatile("" : "+v"(bq));
     {
       float g[4], y[4];
@@ -949,6 +1018,12 @@ __device__ inline void march_run(const PgdParams<float>& p, float* smem, int kb0
       float* dst = (!EDGE || (gr < n0 && gc < n1)) ? xns + (unsigned)(gr * n1 + gc) : g_sink_page;
       *reinterpret_cast<float4*>(dst) = make_float4(xo[0], xo[1], xo[2], xo[3]);
     }
+    mark(k, 7);
+  }
+  if (tracing && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2)) {
+    lds_barrier();
+    const int base = blockIdx.x == 0 ? 0 : kTraceWords / 2;
+    for (int q = tid; q < kTraceWords / 2; q += kThreads) g_march_trace[base + q] = ts[q];
   }
 }
 
@@ -1020,15 +1095,18 @@ int launch_pgd_march(const PgdParams<float>& p, const void* x, const void* xp, c
   using M = March<R>;
   auto kern = pgd_march_kernel<R>;
   static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::BYTES);
+  if (!attr_set) {  // room for the timing trace (diag bit 5) beyond the kernel's own carve
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(M::BYTES + kTraceWords / 2 * 8));
     attr_set = true;
   }
+  const int diag = tuning(PXA_TUNE_PGD_DIAG);
+  const size_t smem = M::BYTES + ((diag & 32) ? kTraceWords / 2 * 8 : 0);
   MarchPlan mp;
   const int st = march_plan(p.stack, p.n0, p.n1, mp);
   if (st != PXA_OK) return st;
-  hipLaunchKernelGGL(kern, dim3(mp.nunits), dim3(kThreads), M::BYTES, s, p, (const float*)x, (const float*)xp,
-                     (const float*)b, (float*)xn, mp.sb, mp.nseg, mp.nstrips, mp.nunits, tuning(PXA_TUNE_PGD_DIAG));
+  hipLaunchKernelGGL(kern, dim3(mp.nunits), dim3(kThreads), smem, s, p, (const float*)x, (const float*)xp,
+                     (const float*)b, (float*)xn, mp.sb, mp.nseg, mp.nstrips, mp.nunits, diag);
   return last_launch_status();
 }
 
@@ -1135,6 +1213,13 @@ using namespace pxa;
 extern "C" {
 
 int pxa_pgd_tv2d_last_kernel(void) { return g_last_pgd_kernel; }
+
+int pxa_pgd_march_trace(uint64_t* host_out, int n) {
+  if (!host_out || n < 0 || n > kTraceWords) return PXA_ERR_ARG;
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_march_trace), (size_t)n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return PXA_ERR_UNSUPPORTED;
+  return PXA_OK;
+}
 
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1) {
   int64_t t = stack * ((n0 + TY - 1) / TY) * ((n1 + TX - 1) / TX);
