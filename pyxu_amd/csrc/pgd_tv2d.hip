@@ -56,6 +56,10 @@ struct PgdParams {
   int prio;  // PXA_TUNE_PGD_PRIO mode (uniform)
 };
 
+// byte offset of the tile kernel's boundary-column ghost terms (after the shared tile2d Layout)
+template <typename T, int R>
+constexpr size_t kGhOff = (Layout<T, R>::BYTES + 15) / 16 * 16;
+
 // s_setprio with a runtime (wave-uniform) level 0..3
 __device__ inline void set_prio(int lvl) {
   switch (lvl) {
@@ -219,12 +223,60 @@ __device__ inline void finish_run(const PgdParams<T>& p, int gr, int gc, const T
   }
 }
 
+// ---- boundary columns of pass B, computed cooperatively (edge-column tiles only): GH[side][m][r] =
+// sum_s k1[s] PT[ghost column pg + m + s][tile row r], the (H1 G0 yk) values at the R zero-padded ghost
+// columns on each side -- ghost_fix()'s gh with the same fma order.  ghost_fix() has the few lanes that
+// own columns within R of the border compute all of them, one 2R+1-tap sum per ghost column and lane:
+// one wave then runs thousands of cycles past the others (measured on the march kernel's trace).
+template <typename T, int R>
+__device__ inline void ghost_cols_tile(const PgdParams<T>& p, const T* PT, T* GH, int tx0, int n1) {
+  using L = Layout<T, R>;
+  for (int t = threadIdx.x; t < 2 * R * TY; t += kThreads) {
+    const int side = t / (R * TY), m = (t / TY) % R, r = t % TY;
+    const int row = (side == 0 ? -R : n1) + m - (tx0 - L::CA);  // PT row of the ghost column
+    T g = T(0);
+    if (row - R >= 0 && row + R < L::AC) {  // else no output of this tile uses it
+#pragma unroll
+      for (int q = -R; q <= R; ++q) g = fma(p.k1[q + R], PT[(row + q) * L::PTP + r], g);
+    }
+    GH[(side * R + m) * TY + r] = g;
+  }
+}
+
+// ghost_fix()'s correction step for pass B, V rows from tile row rr on, with the ghost terms from GH
+template <typename T, int R, int NO>
+__device__ inline void ghost_cols_fix_tile(int i0, int n, int rr, const T* __restrict__ GH, const T* __restrict__ kt,
+                                           T (&acc)[NO][kVecN<T>]) {
+  constexpr int V = kVecN<T>;
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    const int pg = side == 0 ? -R : n;
+    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
+    if (!hit) continue;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = i0 + o;
+      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        const int t = i - (pg + m);
+        if (t < -R || t > R) continue;
+        const T kk = kt[t + R];
+        T gh[V];
+        ld_vec<T, V>(GH + (side * R + m) * TY + rr, gh);
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[o][v] = fma(-kk, gh[v], acc[o][v]);
+      }
+    }
+  }
+}
+
 // ---- pass B: G1 along rows + Grad^T q, handed per output row-run to
 // `emit(k, u, gr, gc, g, yc)`: g = (G yk + Grad^T q) at row gr, columns gc .. gc + CW - 1 of item k,
 // yc = yk there.  The emitter finishes the pixels in place (finish_run) or stages g for the
 // coalesced epilogue (epilogue_staged).
 template <typename T, int R, bool EDGE, typename Emit>
-__device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, const T* KT, int ty0, int tx0,
+__device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, const T* KT, const T* GH, int ty0, int tx0,
                               Emit&& emit) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
@@ -306,7 +358,7 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
       }
       T acc[CW][V];            // acc[w][u]: column c0 + w, row V a + u
       sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g1, acc);
-      if (edge_cols) ghost_fix<T, R, CW, L::PTP>(tx0 + c0, n1, tx0 - CA, PT + V * a, p.k1, KT + kKT, acc);
+      if (edge_cols) ghost_cols_fix_tile<T, R, CW>(tx0 + c0, n1, V * a, GH, KT + kKT, acc);
 #pragma unroll
       for (int u = 0; u < V; ++u) {
         T g[CW], y[CW];
@@ -411,7 +463,9 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   T* A = reinterpret_cast<T*>(smem);
   T* PT = A + L::AR * L::AP;
   T* KT = PT + L::AC * L::PTP;  // H taps for runtime-indexed reads (boundary corrections)
+  T* GH = reinterpret_cast<T*>(smem + kGhOff<T, R>);  // boundary-column ghost terms (edge-column tiles)
   const int n0 = p.n0, n1 = p.n1;
+  const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n1 - R);
   const int tid = threadIdx.x;
   if (EDGE && tid < 2 * R + 1) {
     KT[tid] = p.k0[tid];
@@ -429,8 +483,12 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     __syncthreads();
     pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
     __syncthreads();
+    if (edge_cols) {
+      ghost_cols_tile<T, R>(p, PT, GH, tx0, n1);
+      __syncthreads();
+    }
     T st[KB][V][CW];
-    pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
+    pass_b<T, R, EDGE>(p, A, PT, KT, GH, ty0, tx0, [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
 #pragma unroll
       for (int w = 0; w < CW; ++w) st[k][u][w] = g[w];
     });
@@ -464,8 +522,12 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     __syncthreads();
     pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
     __syncthreads();
+    if (edge_cols) {
+      ghost_cols_tile<T, R>(p, PT, GH, tx0, n1);
+      __syncthreads();
+    }
     const bool want = partials != nullptr;
-    pass_b<T, R, EDGE>(p, A, PT, KT, ty0, tx0, [&](int, int, int gr, int gc, const T(&g)[CW], const T(&y)[CW]) {
+    pass_b<T, R, EDGE>(p, A, PT, KT, GH, ty0, tx0, [&](int, int, int gr, int gc, const T(&g)[CW], const T(&y)[CW]) {
       T bv[CW];
       load_b<T, CW, EDGE>(bs, gr, gc, n0, n1, bv);
       finish_run<T, CW, EDGE>(p, gr, gc, g, bv, y, xs, xns, want, part_d, part_x);
@@ -507,8 +569,7 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
 template <typename T, int R, bool STAGED>
 int launch_pgd_v(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
                  hipStream_t s) {
-  using L = Layout<T, R>;
-  const size_t smem = L::BYTES;
+  const size_t smem = kGhOff<T, R> + (size_t)2 * R * TY * sizeof(T);  // Layout + the ghost terms
   auto kern = pgd_tv2d_kernel<T, R, STAGED>;
   static bool attr_set = false;
   if (!attr_set) {
