@@ -54,11 +54,22 @@ struct PgdParams {
   bool tv;   // lam != 0 (uniform branch)
   bool vec_ok;
   int prio;  // PXA_TUNE_PGD_PRIO mode (uniform)
+  int diag;  // PXA_TUNE_PGD_DIAG (timing probes; bit 5: phase trace)
 };
+
+// Timing trace (PXA_TUNE_PGD_DIAG bit 5, read by pxa_pgd_march_trace): s_memtime stamps of waves 0-3 of
+// a few workgroups.  March kernel: workgroups 0 and grid/2, 8 points of each of their first 16 bands.
+// Tile kernel: workgroups 0, 1, grid/2 and grid-1, 8 points of their tile.  Staged in LDS beyond the
+// kernels' own carve, dumped at exit.
+constexpr int kTraceWords = 2 * 4 * 16 * 8;
+__device__ unsigned long long g_march_trace[kTraceWords];
 
 // byte offset of the tile kernel's boundary-column ghost terms (after the shared tile2d Layout)
 template <typename T, int R>
 constexpr size_t kGhOff = (Layout<T, R>::BYTES + 15) / 16 * 16;
+// bytes of that region: the pass-B column ghost terms (2 R x TY)
+template <typename T, int R>
+constexpr size_t kGhBytes = (size_t)2 * R * TY * sizeof(T);
 
 // s_setprio with a runtime (wave-uniform) level 0..3
 __device__ inline void set_prio(int lvl) {
@@ -137,6 +148,35 @@ __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0
         out[v] = fma(xv[k][v] - pv[k][v], p.a, xv[k][v]);  // (x - x_prev) * a + x, one rounding site
       }
       st_vec<T, V>(A + r * L::AP + V * g, out);
+    }
+  }
+}
+
+// ghost_fix()'s correction step with precomputed ghost terms: outputs i0 .. i0 + NO - 1 along the sweep
+// axis (n positions), one V-vector across it from position cc of the GH rows (pitch GP)
+template <typename T, int R, int NO, int GP>
+__device__ inline void ghost_fix_pre(int i0, int n, int cc, const T* __restrict__ GH, const T* __restrict__ kt,
+                                     T (&acc)[NO][kVecN<T>]) {
+  constexpr int V = kVecN<T>;
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    const int pg = side == 0 ? -R : n;
+    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
+    if (!hit) continue;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = i0 + o;
+      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        const int t = i - (pg + m);
+        if (t < -R || t > R) continue;
+        const T kk = kt[t + R];
+        T gh[V];
+        ld_vec<T, V>(GH + (side * R + m) * GP + cc, gh);
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[o][v] = fma(-kk, gh[v], acc[o][v]);
+      }
     }
   }
 }
@@ -243,34 +283,6 @@ __device__ inline void ghost_cols_tile(const PgdParams<T>& p, const T* PT, T* GH
   }
 }
 
-// ghost_fix()'s correction step for pass B, V rows from tile row rr on, with the ghost terms from GH
-template <typename T, int R, int NO>
-__device__ inline void ghost_cols_fix_tile(int i0, int n, int rr, const T* __restrict__ GH, const T* __restrict__ kt,
-                                           T (&acc)[NO][kVecN<T>]) {
-  constexpr int V = kVecN<T>;
-#pragma unroll
-  for (int side = 0; side < 2; ++side) {
-    const int pg = side == 0 ? -R : n;
-    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
-    if (!hit) continue;
-#pragma unroll
-    for (int o = 0; o < NO; ++o) {
-      const int i = i0 + o;
-      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
-#pragma unroll
-      for (int m = 0; m < R; ++m) {
-        const int t = i - (pg + m);
-        if (t < -R || t > R) continue;
-        const T kk = kt[t + R];
-        T gh[V];
-        ld_vec<T, V>(GH + (side * R + m) * TY + rr, gh);
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[o][v] = fma(-kk, gh[v], acc[o][v]);
-      }
-    }
-  }
-}
-
 // ---- pass B: G1 along rows + Grad^T q, handed per output row-run to
 // `emit(k, u, gr, gc, g, yc)`: g = (G yk + Grad^T q) at row gr, columns gc .. gc + CW - 1 of item k,
 // yc = yk there.  The emitter finishes the pixels in place (finish_run) or stages g for the
@@ -358,7 +370,7 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
       }
       T acc[CW][V];            // acc[w][u]: column c0 + w, row V a + u
       sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g1, acc);
-      if (edge_cols) ghost_cols_fix_tile<T, R, CW>(tx0 + c0, n1, V * a, GH, KT + kKT, acc);
+      if (edge_cols) ghost_fix_pre<T, R, CW, TY>(tx0 + c0, n1, V * a, GH, KT + kKT, acc);
 #pragma unroll
       for (int u = 0; u < V; ++u) {
         T g[CW], y[CW];
@@ -476,22 +488,33 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   const int base_prio = pm == 1 || pm == 4 ? (int)((blockIdx.x >> 8) & 3u) : pm == 3 ? (int)((blockIdx.x >> 3) & 3u) : 0;
   const bool phase_prio = pm == 2 || pm == 4;
   if (pm) set_prio(phase_prio ? 3 : base_prio);
+  const bool tracing = (p.diag & 32) != 0;
+  unsigned long long* ts = reinterpret_cast<unsigned long long*>(smem + kGhOff<T, R> + kGhBytes<T, R>);
+  auto tmark = [&](int pt) {
+    if (tracing && (tid & 63) == 0) ts[(tid >> 6) * 8 + pt] = clock64();
+  };
+  tmark(0);
   if constexpr (STAGED) {
     using S = Stage<T, R>;
     load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+    tmark(1);
     if (phase_prio) set_prio(base_prio);
     __syncthreads();
+    tmark(2);
     pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
+    tmark(3);
     __syncthreads();
     if (edge_cols) {
       ghost_cols_tile<T, R>(p, PT, GH, tx0, n1);
       __syncthreads();
     }
+    tmark(4);
     T st[KB][V][CW];
     pass_b<T, R, EDGE>(p, A, PT, KT, GH, ty0, tx0, [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
 #pragma unroll
       for (int w = 0; w < CW; ++w) st[k][u][w] = g[w];
     });
+    tmark(5);
     __syncthreads();  // every G1 sweep is done with PT: O may overwrite it
     T* O = PT;
 #pragma unroll
@@ -514,9 +537,17 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       }
     }
     __syncthreads();
+    tmark(6);
     if (phase_prio) set_prio(3);
     epilogue_staged<T, R, EDGE>(p, A, O, ty0, tx0, bs, xs, xns, partials != nullptr, part_d, part_x);
+    tmark(7);
     if (partials) fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
+    const unsigned nb = gridDim.x, bid = blockIdx.x;
+    if (tracing && (bid == 0 || bid == 1 || bid == nb / 2 || bid == nb - 1)) {
+      __syncthreads();
+      const int slot = bid == 0 ? 0 : bid == 1 ? 1 : bid == nb / 2 ? 2 : 3;
+      if (tid < 32) g_march_trace[slot * 32 + tid] = ts[tid];
+    }
   } else {
     load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
     __syncthreads();
@@ -569,11 +600,13 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
 template <typename T, int R, bool STAGED>
 int launch_pgd_v(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
                  hipStream_t s) {
-  const size_t smem = kGhOff<T, R> + (size_t)2 * R * TY * sizeof(T);  // Layout + the ghost terms
+  // Layout + the ghost terms (+ the timing trace under PXA_TUNE_PGD_DIAG bit 5)
+  const size_t smem = kGhOff<T, R> + kGhBytes<T, R> + ((p.diag & 32) ? 256 : 0);
   auto kern = pgd_tv2d_kernel<T, R, STAGED>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(kGhOff<T, R> + kGhBytes<T, R> + 256));
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3(p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp, (const T*)b,
@@ -622,10 +655,7 @@ int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void*
 // granules DMA from a zero page (n1 % 4 == 0: a 16-B granule is wholly inside or outside).
 __device__ __attribute__((aligned(16))) float g_zero_page[4];
 __device__ __attribute__((aligned(16))) float g_sink_page[4];
-// march-kernel timing trace (PXA_TUNE_PGD_DIAG bit 5): s_memtime of wave w of two workgroups at 8 points of
-// each of their first 16 bands, staged in LDS beyond the kernel's own carve, dumped at exit
-constexpr int kTraceWords = 2 * 4 * 16 * 8;
-__device__ unsigned long long g_march_trace[kTraceWords];  // target of the march epilogue's out-of-image lanes
+  // target of the march epilogue's out-of-image lanes
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -1233,6 +1263,7 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.tv = lam != 0.0;
   p.prox = prox;
   p.prio = tuning(PXA_TUNE_PGD_PRIO);
+  p.diag = tuning(PXA_TUNE_PGD_DIAG);
   if constexpr (sizeof(T) == 4) {
     // march kernel (PXA_TUNE_PGD_KERNEL = 5 forces it where it applies): fp32, R <= 6, 16-B rows,
     // 32-bit in-image offsets, no RelError partials
