@@ -175,7 +175,8 @@ int pxa_row_reduce_pow(int dtype, int64_t rows, int64_t n, double p, const void*
 
 /* RelError.stop in one pass (opt/stop.py:353-382, norm=2): out[0:rows] = sum (x - x_prev)^2 and
  * out[rows:2 rows] = sum x_prev^2 per row (same bits as pxa_row_reduce DIFFSQ / SUMSQ), and, when
- * x_copy is not NULL, x_copy = x (the `x.copy()` the criterion keeps, stop.py:381).
+ * x_copy is not NULL, x_copy = x (the `x.copy()` the criterion keeps, stop.py:381).  `out` may be
+ * device memory or device-mapped pinned host memory (RelError.stop_async reads it after an event).
  * `work` must hold pxa_relerr_stats_workspace_bytes(rows, n) bytes of device memory. */
 size_t pxa_relerr_stats_workspace_bytes(int64_t rows, int64_t n);
 int pxa_relerr_stats(int dtype, int64_t rows, int64_t n, const void* x, const void* x_prev, void* x_copy, double* out,

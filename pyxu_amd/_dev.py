@@ -468,8 +468,8 @@ def transpose(x):
 # ------------------------------------------------------------------ reductions
 def relerr_stats(x, x_prev, out, copy=True):
     """RelError statistics in one pass (pxa_relerr_stats): out[0] = sum (x - x_prev)^2 and
-    out[1] = sum x_prev^2 per row (out: contiguous float64 (2, rows) device buffer); returns the copy
-    of x the criterion keeps (or None with copy=False)."""
+    out[1] = sum x_prev^2 per row (out: contiguous float64 (2, rows) buffer, device or pinned host);
+    returns the copy of x the criterion keeps (or None with copy=False)."""
     torch = _torch()
     x = require(x)
     x_prev = require(x_prev)

@@ -277,8 +277,8 @@ class RelError(pxa.StoppingCriterion):
     _reduce = None
 
     def stop_async(self, state):
-        """stop() in two phases: the statistics, the copy of x and an async device->host copy of the
-        statistics are enqueued now; the returned callable waits for that copy only and decides.  Same
+        """stop() in two phases: the statistics (written by the device into pinned host memory) and the
+        copy of x are enqueued now; the returned callable waits for them only and decides.  Same
         kernels, same bits, same decision, same info() as stop()."""
         x = state[self._var]
         if (isinstance(x, numbers.Real) or self._x_prev is None or self._reduce is not None
@@ -292,13 +292,13 @@ class RelError(pxa.StoppingCriterion):
         # one device / pinned-host statistics pair and one event per criterion, reused: a check is
         # resolved before the next one is issued
         buf = getattr(self, "_async_buf", None)
-        if buf is None or buf[0].shape[1] != rows or buf[0].device != x.device:
-            buf = (_dev.empty_f64((2, rows), x), torch.empty((2, rows), dtype=torch.float64, pin_memory=True),
-                   torch.cuda.Event())
+        if buf is None or buf[0].shape[1] != rows:
+            buf = (torch.empty((2, rows), dtype=torch.float64, pin_memory=True), torch.cuda.Event())
             self._async_buf = buf
-        st, host, ev = buf
-        x_copy = _dev.relerr_stats(x, self._x_prev, st)
-        host.copy_(st, non_blocking=True)
+        host, ev = buf
+        # the final fold writes the statistics straight into the pinned host buffer (device-mapped):
+        # no device -> host copy launch between the statistics and the event
+        x_copy = _dev.relerr_stats(x, self._x_prev, host)
         ev.record()
         shape = x.shape[:-1]
 
