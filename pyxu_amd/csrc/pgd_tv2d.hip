@@ -188,6 +188,11 @@ __device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T*
   constexpr int V = L::V;
   const int tid = threadIdx.x;
   constexpr int KA = cdiv(L::NPA, kThreads);
+  // one item per thread (fp32): items spread over all 4 waves in chunks of a multiple of NA, so each
+  // lane keeps it % NA == lane % NA (the conflict-free lane pattern) -- e.g. 48 / 48 / 48 / 32 for the
+  // 176 items of R = 6, where consecutive numbering leaves wave 3 idle through pass A
+  constexpr int CH = KA == 1 ? rup(cdiv(L::NPA, kThreads / 64), L::NA) : 64;
+  static_assert(KA > 1 || CH <= 64, "pass-A chunk fits a wave");
   const bool edge_rows = EDGE && (ty0 < R || ty0 + TY > p.n0 - R);
 #pragma unroll
   for (int k = 0; k < KA; ++k) {
@@ -390,35 +395,50 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
 // each 16-B vector of a row is one lane (16 lanes per fp32 row), so H^T y / x loads and x_new stores
 // are full 128-B lines instead of the pass-B item order's 64-B row pieces (measured on MI355X: a
 // 2048^2 fp32 store in the item order 7.2 us, row-major 5.2 us).  yk comes from A.
+// H^T y of this thread's staged-epilogue pixels (NS row-major 16-B vectors), zero outside the image;
+// issued before the O staging so that its latency overlaps the staging and its barrier
+template <typename T, int R>
+struct StagedB {
+  static constexpr int NS = TY / Stage<T, R>::RPS;
+  T v[NS][kVecN<T>];
+};
+
+template <typename T, int R, bool EDGE>
+__device__ inline void load_b_staged(const PgdParams<T>& p, int ty0, int tx0, const T* __restrict__ bs,
+                                     StagedB<T, R>& b) {
+  using S = Stage<T, R>;
+  constexpr int V = kVecN<T>;
+  const int n0 = p.n0, n1 = p.n1;
+  int r0, cq;
+  S::lane(threadIdx.x, r0, cq);
+#pragma unroll
+  for (int s = 0; s < StagedB<T, R>::NS; ++s) {  // all H^T y loads first: one round trip
+    const int gr = ty0 + r0 + s * S::RPS, gc = tx0 + V * cq;
+    if (!EDGE) {
+      ld_vec<T, V>(bs + (unsigned)(gr * n1 + gc), b.v[s]);
+    } else {
+#pragma unroll
+      for (int v = 0; v < V; ++v) b.v[s][v] = (gr < n0 && gc + v < n1) ? bs[(int64_t)gr * n1 + gc + v] : T(0);
+    }
+  }
+}
+
 template <typename T, int R, bool EDGE>
 __device__ inline void epilogue_staged(const PgdParams<T>& p, const T* A, const T* O, int ty0, int tx0,
-                                       const T* __restrict__ bs, const T* __restrict__ xs, T* __restrict__ xns,
+                                       const StagedB<T, R>& b, const T* __restrict__ xs, T* __restrict__ xns,
                                        bool want_part, double& part_d, double& part_x) {
   using L = Layout<T, R>;
   using S = Stage<T, R>;
   constexpr int V = L::V;
-  const int n0 = p.n0, n1 = p.n1;
   int r0, cq;
   S::lane(threadIdx.x, r0, cq);
-  constexpr int NS = TY / S::RPS;
-  T bv[NS][V];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {  // all H^T y loads first: one round trip
-    const int gr = ty0 + r0 + s * S::RPS, gc = tx0 + V * cq;
-    if (!EDGE) {
-      ld_vec<T, V>(bs + (unsigned)(gr * n1 + gc), bv[s]);
-    } else {
-#pragma unroll
-      for (int v = 0; v < V; ++v) bv[s][v] = (gr < n0 && gc + v < n1) ? bs[(int64_t)gr * n1 + gc + v] : T(0);
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
+  for (int s = 0; s < StagedB<T, R>::NS; ++s) {
     const int r = r0 + s * S::RPS;
     T g[V], y[V];
     ld_vec<T, V>(O + S::idx(r, V * cq), g);
     ld_vec<T, V>(A + (r + 2 * R) * L::AP + L::CA + V * cq, y);
-    finish_run<T, V, EDGE>(p, ty0 + r, tx0 + V * cq, g, bv[s], y, xs, xns, want_part, part_d, part_x);
+    finish_run<T, V, EDGE>(p, ty0 + r, tx0 + V * cq, g, b.v[s], y, xs, xns, want_part, part_d, part_x);
   }
 }
 
@@ -514,6 +534,8 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
 #pragma unroll
       for (int w = 0; w < CW; ++w) st[k][u][w] = g[w];
     });
+    StagedB<T, R> hb;
+    load_b_staged<T, R, EDGE>(p, ty0, tx0, bs, hb);  // in flight during the O staging
     tmark(5);
     __syncthreads();  // every G1 sweep is done with PT: O may overwrite it
     T* O = PT;
@@ -539,7 +561,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     __syncthreads();
     tmark(6);
     if (phase_prio) set_prio(3);
-    epilogue_staged<T, R, EDGE>(p, A, O, ty0, tx0, bs, xs, xns, partials != nullptr, part_d, part_x);
+    epilogue_staged<T, R, EDGE>(p, A, O, ty0, tx0, hb, xs, xns, partials != nullptr, part_d, part_x);
     tmark(7);
     if (partials) fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
     const unsigned nb = gridDim.x, bid = blockIdx.x;
