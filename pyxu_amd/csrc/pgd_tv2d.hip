@@ -598,7 +598,15 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  const unsigned tile = xcd_tile(blockIdx.x, p.ntiles);
+  unsigned tile = xcd_tile(blockIdx.x, p.ntiles);
+  {  // the last XCD band walks backwards: an image's bottom-edge tiles (slower: boundary corrections)
+     // are dispatched first instead of last, longest-first scheduling (2048^2: 29.2-29.3 -> 28.9-29.0 us)
+    const unsigned nb = p.ntiles, q8 = nb >> 3, r8 = nb & 7u, g8 = blockIdx.x & 7u;
+    if (g8 == 7u) {
+      const unsigned lo = 7u * q8 + (r8 < 7u ? r8 : 7u), len = q8 + (7u < r8 ? 1u : 0u);
+      tile = lo + (len - 1u - (tile - lo));
+    }
+  }
   const unsigned tpi = (unsigned)p.tiles0 * (unsigned)p.tiles1;
   const unsigned s = tile / tpi;
   const unsigned tr = tile - s * tpi;
