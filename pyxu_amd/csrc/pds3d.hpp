@@ -252,6 +252,7 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
   T* A = reinterpret_cast<T*>(smem);
   T* PT = A + L::AR * L::AP;
   T* KT = PT + L::AC * L::PTP;
+  T* GH = reinterpret_cast<T*>(smem + kGhOff<T, R>);  // boundary-column ghost terms (edge-column tiles)
   const PdsGeom<T>& g = p.g;
   const int n1 = g.n1, n2 = g.n2;
   const int64_t M = (int64_t)n1 * n2;
@@ -312,6 +313,10 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
   // ---- pass B: G2 along rows; results parked in LDS (the PT region, free once every sweep is done)
   constexpr int KB = cdiv(L::NPB, kThreads);
   const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n2 - R);
+  if (edge_cols) {  // the ghost terms of the border columns, by the whole workgroup
+    ghost_cols_coop<T, R>(p.k2, PT, GH, tx0, n2);
+    __syncthreads();
+  }
   using S = Stage<T, R>;
   T st[KB][V][CW];
 #pragma unroll
@@ -323,7 +328,7 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
       const int c0 = CW * cb;
       T acc[CW][V];
       sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g2, acc);
-      if (edge_cols) ghost_fix<T, R, CW, L::PTP>(tx0 + c0, n2, tx0 - CA, PT + V * a, p.k2, KT + kKT, acc);
+      if (edge_cols) ghost_fix_pre<T, R, CW, TY>(tx0 + c0, n2, V * a, GH, KT + kKT, acc);
 #pragma unroll
       for (int uu = 0; uu < V; ++uu)
 #pragma unroll
@@ -496,14 +501,15 @@ int dispatch_a(int R0, const PdsA<T>& pa, int np, int64_t M, int nseg, const voi
 
 template <typename T, int R, bool PD3O>
 int launch_b(const PdsB<T>& pb, const PdsPtrs& P, hipStream_t st) {
-  using L = Layout<T, R>;
   auto kern = pds_plane_kernel<T, R, PD3O>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BYTES);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(kGhOff<T, R> + kGhBytes<T, R>));
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(pb.ntiles), dim3(kThreads), L::BYTES, st, pb, P);
+  const size_t smem = kGhOff<T, R> + kGhBytes<T, R>;  // Layout + the boundary-column ghost terms
+  hipLaunchKernelGGL(kern, dim3(pb.ntiles), dim3(kThreads), smem, st, pb, P);
   return last_launch_status();
 }
 

@@ -64,13 +64,6 @@ struct PgdParams {
 constexpr int kTraceWords = 2 * 4 * 16 * 8;
 __device__ unsigned long long g_march_trace[kTraceWords];
 
-// byte offset of the tile kernel's boundary-column ghost terms (after the shared tile2d Layout)
-template <typename T, int R>
-constexpr size_t kGhOff = (Layout<T, R>::BYTES + 15) / 16 * 16;
-// bytes of that region: the pass-B column ghost terms (2 R x TY)
-template <typename T, int R>
-constexpr size_t kGhBytes = (size_t)2 * R * TY * sizeof(T);
-
 // s_setprio with a runtime (wave-uniform) level 0..3
 __device__ inline void set_prio(int lvl) {
   switch (lvl) {
@@ -148,35 +141,6 @@ __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0
         out[v] = fma(xv[k][v] - pv[k][v], p.a, xv[k][v]);  // (x - x_prev) * a + x, one rounding site
       }
       st_vec<T, V>(A + r * L::AP + V * g, out);
-    }
-  }
-}
-
-// ghost_fix()'s correction step with precomputed ghost terms: outputs i0 .. i0 + NO - 1 along the sweep
-// axis (n positions), one V-vector across it from position cc of the GH rows (pitch GP)
-template <typename T, int R, int NO, int GP>
-__device__ inline void ghost_fix_pre(int i0, int n, int cc, const T* __restrict__ GH, const T* __restrict__ kt,
-                                     T (&acc)[NO][kVecN<T>]) {
-  constexpr int V = kVecN<T>;
-#pragma unroll
-  for (int side = 0; side < 2; ++side) {
-    const int pg = side == 0 ? -R : n;
-    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
-    if (!hit) continue;
-#pragma unroll
-    for (int o = 0; o < NO; ++o) {
-      const int i = i0 + o;
-      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
-#pragma unroll
-      for (int m = 0; m < R; ++m) {
-        const int t = i - (pg + m);
-        if (t < -R || t > R) continue;
-        const T kk = kt[t + R];
-        T gh[V];
-        ld_vec<T, V>(GH + (side * R + m) * GP + cc, gh);
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[o][v] = fma(-kk, gh[v], acc[o][v]);
-      }
     }
   }
 }
@@ -265,26 +229,6 @@ __device__ inline void finish_run(const PgdParams<T>& p, int gr, int gc, const T
         }
       }
     }
-  }
-}
-
-// ---- boundary columns of pass B, computed cooperatively (edge-column tiles only): GH[side][m][r] =
-// sum_s k1[s] PT[ghost column pg + m + s][tile row r], the (H1 G0 yk) values at the R zero-padded ghost
-// columns on each side -- ghost_fix()'s gh with the same fma order.  ghost_fix() has the few lanes that
-// own columns within R of the border compute all of them, one 2R+1-tap sum per ghost column and lane:
-// one wave then runs thousands of cycles past the others (measured on the march kernel's trace).
-template <typename T, int R>
-__device__ inline void ghost_cols_tile(const PgdParams<T>& p, const T* PT, T* GH, int tx0, int n1) {
-  using L = Layout<T, R>;
-  for (int t = threadIdx.x; t < 2 * R * TY; t += kThreads) {
-    const int side = t / (R * TY), m = (t / TY) % R, r = t % TY;
-    const int row = (side == 0 ? -R : n1) + m - (tx0 - L::CA);  // PT row of the ghost column
-    T g = T(0);
-    if (row - R >= 0 && row + R < L::AC) {  // else no output of this tile uses it
-#pragma unroll
-      for (int q = -R; q <= R; ++q) g = fma(p.k1[q + R], PT[(row + q) * L::PTP + r], g);
-    }
-    GH[(side * R + m) * TY + r] = g;
   }
 }
 
@@ -525,7 +469,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     tmark(3);
     __syncthreads();
     if (edge_cols) {
-      ghost_cols_tile<T, R>(p, PT, GH, tx0, n1);
+      ghost_cols_coop<T, R>(p.k1, PT, GH, tx0, n1);
       __syncthreads();
     }
     tmark(4);
@@ -576,7 +520,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
     __syncthreads();
     if (edge_cols) {
-      ghost_cols_tile<T, R>(p, PT, GH, tx0, n1);
+      ghost_cols_coop<T, R>(p.k1, PT, GH, tx0, n1);
       __syncthreads();
     }
     const bool want = partials != nullptr;

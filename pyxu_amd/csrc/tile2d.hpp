@@ -171,6 +171,64 @@ __device__ inline void ghost_fix(int i0, int n, int q0, const T* __restrict__ sr
   }
 }
 
+// Boundary columns of the in-plane pass B (edge-column tiles), computed cooperatively into LDS:
+// GH[side][m][r] = sum_s k[s] PT[ghost column pg + m + s][tile row r] for the R zero-padded ghost
+// columns pg + m on each side (pg = -R, n) -- ghost_fix()'s gh with the same fma order.  With ghost_fix()
+// the few lanes owning columns within R of the border compute them all, one 2R+1-tap sum per ghost
+// column and lane: one wave then runs thousands of cycles past the others (measured by the PGD
+// kernels' s_memtime trace).  Followed by a barrier, then ghost_fix_pre() in pass B.
+template <typename T, int R>
+__device__ inline void ghost_cols_coop(const T* __restrict__ k, const T* PT, T* GH, int tx0, int n) {
+  using L = Layout<T, R>;
+  for (int t = threadIdx.x; t < 2 * R * TY; t += kThreads) {
+    const int side = t / (R * TY), m = (t / TY) % R, r = t % TY;
+    const int row = (side == 0 ? -R : n) + m - (tx0 - L::CA);  // PT row of the ghost column
+    T g = T(0);
+    if (row - R >= 0 && row + R < L::AC) {  // else no output of this tile uses it
+#pragma unroll
+      for (int q = -R; q <= R; ++q) g = fma(k[q + R], PT[(row + q) * L::PTP + r], g);
+    }
+    GH[(side * R + m) * TY + r] = g;
+  }
+}
+
+// ghost_fix()'s correction step with precomputed ghost terms: outputs i0 .. i0 + NO - 1 along the sweep
+// axis (n positions), one V-vector across it from position cc of the GH rows (pitch GP)
+template <typename T, int R, int NO, int GP>
+__device__ inline void ghost_fix_pre(int i0, int n, int cc, const T* __restrict__ GH, const T* __restrict__ kt,
+                                     T (&acc)[NO][kVecN<T>]) {
+  constexpr int V = kVecN<T>;
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    const int pg = side == 0 ? -R : n;
+    const bool hit = side == 0 ? (i0 < R) : (i0 + NO - 1 >= n - R && i0 < n);
+    if (!hit) continue;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = i0 + o;
+      if (i >= n || (side == 0 ? i >= R : i < n - R)) continue;
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        const int t = i - (pg + m);
+        if (t < -R || t > R) continue;
+        const T kk = kt[t + R];
+        T gh[V];
+        const auto* src = GH + (side * R + m) * GP + cc;
+#pragma unroll
+        for (int v = 0; v < V; ++v) gh[v] = src[v];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[o][v] = fma(-kk, gh[v], acc[o][v]);
+      }
+    }
+  }
+}
+
+// byte offset / size of the ghost-term region the tile kernels append to the Layout carve
+template <typename T, int R>
+constexpr size_t kGhOff = (Layout<T, R>::BYTES + 15) / 16 * 16;
+template <typename T, int R>
+constexpr size_t kGhBytes = (size_t)2 * R * TY * sizeof(T);
+
 // Global V-vector load at an element offset whose alignment is known at compile time.
 template <typename T>
 __device__ inline void ld_pair(const T* __restrict__ p, T (&v)[2]) {
