@@ -19,10 +19,18 @@ doubles per stop check) -> weak scaling; value = total image-iterations/s = rank
 
 Sub-records on the same line (north_star):
   "stop_rate_1": the headline workload at the reference's default stop_rate = 1;
+  "c2_4096": the same PGD at 4096^2 (SURVEY §7's stand-in for the infeasible 4096^3 north_star volume);
   "c5": configs[4], 512 independent 512^2 TV-deblur images as ONE (512, 512, 512) batch-as-axis
         problem sharded over the ranks (512 / N images each: strong scaling), global RelError;
   "c4": configs[3], ADMM with a dense 8192 x 65536 K (MFMA/GEMV dense path) + lam L1; K row-sharded
-        over the ranks (one RCCL all-reduce of the 65536-vector per CG iteration).
+        over the ranks (one RCCL all-reduce of the 65536-vector per CG iteration);
+  "c3": configs[2], PD3O and Condat-Vu on a 1024^3 volume (Gaussian S, anisotropic TV), with the
+        per-kernel times of the fused three-launch step (single GPU: replicas only at N > 1).
+
+Roofline convention.  `frac` is the dominant kernel's time against ITS OWN compulsory bytes (every array
+it must read or write, once): the y-state PGD launch reads y, x, H^T y and writes x_new, y_next =
+20 B/pixel.  `frac_survey` keeps SURVEY §8(d)'s 48 B/pixel figure for the same time; that model is not a
+bound on a one-launch kernel (it charges intermediates this kernel never materialises).
 """
 import argparse
 import json
@@ -39,9 +47,11 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 KERNEL = "pgd_tv2d_kernel"
-ALG_BYTES_PER_PIXEL = 48  # 8 reads + 4 writes of fp32 per pixel per PGD iteration
-FUSED_BYTES_PER_PIXEL = 16  # compulsory traffic of the one-launch step: x, x_prev, H^T y read + x_new write
+SURVEY_BYTES_PER_PIXEL = 48  # 8 reads + 4 writes of fp32 per pixel per PGD iteration
 CPU_THREADS_MAX = 16  # the GPU box's CPU share per GPU (gpurun: 16)
+# pxa_pgd_tv2d_last_kernel() -> (mode name, own compulsory bytes per pixel): the arrays the launch reads / writes
+PGD_MODES = {1: ("classic: x, x_prev, H^T y -> x_new", 16), 2: ("seed: x, x_prev, H^T y -> x_new, y_next", 20),
+             3: ("y-state: y, x, H^T y -> x_new, y_next", 20)}
 
 
 # ----------------------------------------------------------------------------- launcher (no GPU here)
@@ -167,17 +177,21 @@ def cpu_model():
 
 
 def measured_traffic(kernel, key):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic.json,
-    written by scripts/pmc_traffic.py: (2 * FETCH_SIZE + WRITE_SIZE) * 1024, the gfx950 correction of
-    MI355X_MICROARCH.md §HBM), or None when no profile of this workload exists."""
+    """(HBM bytes per launch, provenance) of `kernel` on workload `key` from the committed rocprofv3 PMC
+    passes (profiles/traffic.json, written by scripts/pmc_traffic.py: (2 * FETCH_SIZE + WRITE_SIZE) * 1024,
+    the gfx950 correction of MI355X_MICROARCH.md §HBM), or (None, reason).  NOT measured in this run: the
+    counters need their own profiler passes (scripts/gpu_r03.sh)."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as fh:
             tab = json.load(fh)
     except (OSError, ValueError):
-        return None
+        return None, "no profiles/traffic.json"
     ent = tab.get(f"{kernel}@{key}")
-    return None if ent is None else ent.get("hbm_bytes_per_launch")
+    if ent is None:
+        return None, f"no PMC profile of {kernel}@{key} in profiles/traffic.json"
+    return ent.get("hbm_bytes_per_launch"), (f"profiles/traffic.json[{kernel}@{key}] (rocprofv3 PMC pass "
+                                             f"{ent.get('tag', '?')}, not this run)")
 
 
 def cpu_baseline(n0, n1, seed, budget_s, threads, lam=0.01, mu=0.01, sigma=2.0):
@@ -320,24 +334,136 @@ def run_pgd(ctx, f, g, stop_rate, warmup, steps, fused, prime_s=0.0, kernel_time
     return elapsed, kern_ms, slvr, (timer.launches if timer is not None else 0)
 
 
-PGD_KERNELS = {1: ("pgd_tv2d_kernel", "tile"), 2: ("pgd_march_kernel", "march")}
-
-
-def last_pgd_kernel():
-    """(rocprof kernel name, short name) of the fused PGD kernel this thread launched last."""
+def last_pgd_mode():
+    """(mode name, own bytes per pixel) of the fused PGD launch this thread made last."""
     from pyxu_amd._lib import lib
 
-    return PGD_KERNELS.get(int(lib.pxa_pgd_tv2d_last_kernel()), (KERNEL, "none"))
+    return PGD_MODES.get(int(lib.pxa_pgd_tv2d_last_kernel()), ("none", 16))
 
 
-def roofline(pixels, kern_ms, traffic, kernel=KERNEL):
-    alg_bytes = ALG_BYTES_PER_PIXEL * pixels  # SURVEY.md §8(d): 48 B/pixel/iteration
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    comp = FUSED_BYTES_PER_PIXEL * pixels
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
-            "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes, "fused_compulsory_bytes_per_launch": comp,
-            "frac_vs_fused_compulsory": round(comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+def roofline(pixels, kern_ms, own_bpp, traffic_key, kernel=KERNEL, mode=""):
+    """The dominant kernel against its own compulsory bytes (frac) and SURVEY §8(d)'s figure (frac_survey)."""
+    own = own_bpp * pixels
+    achieved = own / (kern_ms * 1e-3) / 1e9
+    surv = SURVEY_BYTES_PER_PIXEL * pixels
+    traffic, src = measured_traffic(kernel, traffic_key)
+    rec = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src, "kernel": kernel,
+           "mode": mode, "kernel_ms": round(kern_ms, 5), "bytes_per_launch": own,
+           "bytes_model": f"own compulsory streams, {own_bpp} B/pixel",
+           "frac_survey": round(surv / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "survey_bytes_per_launch": surv}
+    if achieved > HBM_PEAK_GBS:  # only possible when the working set is served from the Infinity Cache
+        rec["note"] = "above the HBM peak: working set resident in the 256 MiB Infinity Cache"
+    return rec
+
+
+def bench_c2_4096(ctx, args):
+    """SURVEY §7's 4096^2 stand-in for the infeasible 4096^3 north_star volume: the headline PGD problem at
+    4096 x 4096 (one image per rank), same solver loop and stop criteria."""
+    import pyxu_amd.runtime as pxrt
+
+    n = 4096
+    f, g, _ = build_problem(n, n, seed=4321 + ctx.rank)
+    K = args.c4096_steps
+    sr = auto_stop_rate(K)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        elapsed, kern_ms, slvr, launches = run_pgd(ctx, f, g, sr, 5, K, True)
+    mode, bpp = last_pgd_mode()
+    rec = {"workload": f"PGD {n}x{n} Gaussian(sigma=2) deblur + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
+           "scaling": "weak", "steps": K, "warmup": 5, "stop_rate": sr, "value": round(ctx.world * K / elapsed, 2),
+           "unit": "image-iterations/s", "ms_per_step": round(1e3 * elapsed / K, 4)}
+    if kern_ms is not None:
+        kern_ms = ctx.max_over_ranks(kern_ms)
+        rec["roofline"] = roofline(n * n, kern_ms, bpp, f"{n}x{n}", mode=mode)
+        rec["roofline"]["launches_timed"] = launches
+    del slvr, f, g
+    return rec
+
+
+C3_BYTES = {"pd3o": (76, 80), "cv": (68, 68)}  # (own compulsory B/voxel of the fused step, SURVEY §8(d) B/voxel)
+C3_KERNELS = ("pds_axis0_kernel (A: axis-0 march of S0 / S0^T)", "pds_plane_kernel (B: in-plane G + point-wise update)",
+              "pds_dual_kernel (C: z + sigma grad w, fenchel prox, relaxation)")
+# own compulsory bytes per voxel of each kernel (DESIGN.md §4): PD3O A u,z(3) in x,Q out; B Q,x,u,S^T y in w,u+ out;
+# C w,z(3) in z+(3) out.  CV: A x in Q out; B Q,x,S^T y,z(3) in w,x+ out; C as PD3O.
+C3_KERNEL_BYTES = {"pd3o": (24, 24, 28), "cv": (8, 32, 28)}
+
+
+def bench_c3(ctx, args):
+    """configs[2]: PD3O and Condat-Vu on an n^3 volume, S = Gaussian(sigma=2) (13 taps/axis, zero boundary),
+    K = Gradient (3 directions), h = lam L1 (anisotropic TV), g = None, fp32; the phantom and the noise are
+    generated on the device.  Driven through the Solver API (MANUAL mode, one stop check per window);
+    per-kernel times from HIP events recorded inside pxa_pds_step (TUNE_PDS_EVENTS)."""
+    import shutil
+
+    import torch
+
+    import pyxu_amd.abc as pxa
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.opt.solver as pxs
+    import pyxu_amd.opt.stop as pxst
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd import _dev
+
+    n, K = args.c3_n, args.c3_steps
+    sh = (n, n, n)
+    N = n ** 3
+    out = {"workload": f"{n}^3 volume, S = Gaussian(sigma=2), K = Gradient (3 dirs), h = 0.01 L1 (anisotropic TV), g = None",
+           "scaling": "replicas (one volume per GPU)", "steps": K}
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    x_gt = torch.zeros(sh, device="cuda", dtype=torch.float32)
+    rng = np.random.default_rng(7)
+    for _ in range(12):  # piecewise-constant phantom (SURVEY §8(d)), written on the device
+        lo = [int(rng.integers(0, n // 2)) for _ in sh]
+        hi = [l + int(rng.integers(n // 8 + 1, n // 2 + 1)) for l in lo]
+        x_gt[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] = float(rng.uniform(0.2, 1.0))
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        S = pxo.Gaussian(arg_shape=sh, sigma=2.0, truncate=3.0)
+        y = S.apply(x_gt.reshape(-1))
+        del x_gt
+        y = _dev.axpby(1.0, y, 0.01, torch.randn(N, device="cuda", dtype=torch.float32, generator=gen), out=y)
+        f = 0.5 * pxo.SquaredL2Norm(dim=N).asloss(y) * S
+        f.diff_lipschitz = 1.0  # ||S||^2 <= 1 for the normalised Gaussian (set analytically, §8(d))
+        Kop = pxo.Gradient(arg_shape=sh)
+        h = 0.01 * pxo.L1Norm(dim=3 * N)
+        for algo, klass in (("pd3o", pxs.PD3O), ("cv", pxs.CondatVu)):
+            s = klass(f=f, g=None, h=h, K=Kop, show_progress=False, stop_rate=K)
+            s.fit(x0=torch.zeros(N, device="cuda", dtype=torch.float32), stop_crit=pxst.MaxIter(10 ** 9) | pxst.RelError(eps=1e-30),
+                  mode=pxa.Mode.MANUAL)
+            it = s.steps()
+            for _ in range(2):
+                next(it)
+            torch.cuda.synchronize()
+            prev = _dev.tuning(_dev.TUNE_PDS_EVENTS, 1)
+            _dev.pds_kernel_ms(reset=True)
+            try:
+                elapsed = timed_steps(ctx, it, 0, K)
+                nrec, ms = _dev.pds_kernel_ms(reset=True)
+            finally:
+                _dev.tuning(_dev.TUNE_PDS_EVENTS, prev)
+            own, surv = C3_BYTES[algo]
+            step_ms = 1e3 * elapsed / K
+            rec = {"value": round(K / elapsed, 3), "unit": "iterations/s", "ms_per_step": round(step_ms, 3),
+                   "fused_m_step": s._plan is not None, "stop_rate": K,
+                   "frac_step_own": round(own * N / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "frac_step_survey": round(surv * N / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            if nrec > 0:
+                kms = [m / nrec for m in ms]
+                rec["kernels"] = []
+                for name, t, b in zip(C3_KERNELS, kms, C3_KERNEL_BYTES[algo]):
+                    ach = b * N / (t * 1e-3) / 1e9 if t > 0 else 0.0
+                    rec["kernels"].append({"kernel": name, "kernel_ms": round(t, 4), "bytes_per_voxel": b,
+                                           "achieved": round(ach, 1), "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)})
+                kt = sum(kms)
+                rec["roofline"] = {"bound": "hbm", "achieved": round(own * N / (kt * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": round(own * N / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "traffic": None, "kernel_ms": round(kt, 4), "bytes_model": f"{own} B/voxel, the fused step's own compulsory bytes",
+                                   "frac_survey": round(surv * N / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            out[algo] = rec
+            shutil.rmtree(s.workdir, ignore_errors=True)
+            del s, it
+            torch.cuda.empty_cache()
+    del f, S, y, Kop, h
+    return out
 
 
 def bench_c5(ctx, args):
@@ -352,16 +478,15 @@ def bench_c5(ctx, args):
     sr = auto_stop_rate(K)
     with pxrt.Precision(pxrt.Width.SINGLE):
         elapsed, kern_ms, slvr, launches = run_pgd(ctx, f, g, sr, args.c5_warmup, K, True)
-    kname, kshort = last_pgd_kernel()
+    mode, bpp = last_pgd_mode()
     kern_ms = ctx.max_over_ranks(kern_ms if kern_ms is not None else 0.0)
     rec = {"workload": f"PGD {total} x {n}x{n} batch-as-axis Gaussian(sigma=2) + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
            "images": total, "images_per_rank": hi - lo, "scaling": "strong", "steps": K, "warmup": args.c5_warmup,
            "stop_rate": sr, "value": round(total * K / elapsed, 1), "unit": "image-iterations/s",
-           "ms_per_step": round(1e3 * elapsed / K, 4), "stop_crit": "MaxIter | RelError (global all-reduce)",
-           "pgd_kernel": kshort}
+           "ms_per_step": round(1e3 * elapsed / K, 4), "stop_crit": "MaxIter | RelError (global all-reduce)"}
     if kern_ms > 0:
-        rec["roofline"] = roofline((hi - lo) * n * n, kern_ms, measured_traffic(kname, f"{hi - lo}x{n}x{n}"), kname)
-        rec["roofline"]["note"] = "per rank (slowest rank's kernel time)"
+        rec["roofline"] = roofline((hi - lo) * n * n, kern_ms, bpp, f"{hi - lo}x{n}x{n}", mode=mode)
+        rec["roofline"]["per_rank"] = "slowest rank's kernel time"
     del slvr
     return rec
 
@@ -425,15 +550,17 @@ def bench_c4(ctx, args):
             normal_ms = e0.elapsed_time(e1) / 10
     per_outer = cg_steps / max(1, args.c4_steps)
     cg_ms = 1e3 * elapsed / max(1.0, per_outer * args.c4_steps)
-    pair_bytes = 2 * (hi - lo) * N * 4  # one K p + one K^T z pass over the local K per CG iteration
+    one_pass = (hi - lo) * N * 4  # CG's A p reads the local K ONCE (pxa_dense_normal)
     rec = {"workload": f"ADMM dense {M}x{N} K + lam*L1 (x-update: QuadraticFunc.prox -> CG), tau=1",
            "rows_per_rank": hi - lo, "scaling": "strong", "steps": args.c4_steps, "warmup": args.c4_warmup,
            "value": round(args.c4_steps / elapsed, 3), "unit": "ADMM outer iterations/s",
            "ms_per_step": round(1e3 * elapsed / args.c4_steps, 3), "cg_iters_per_outer": round(per_outer, 2),
            "ms_per_cg_iter": round(cg_ms, 4),
-           "roofline": {"bound": "hbm", "achieved": round(pair_bytes / (cg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(pair_bytes / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                        "note": "whole CG iteration vs the two compulsory passes over this rank's K (SURVEY §8(d) C4)"}}
+           "roofline": {"bound": "hbm", "achieved": round(one_pass / (cg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(one_pass / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "bytes_model": "one compulsory pass over this rank's K per CG iteration (the one-pass normal operator)",
+                        "frac_survey": round(2 * one_pass / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "note": "whole CG iteration (operator + CG vector updates + the outer iteration amortised)"}}
     if normal_ms is not None:  # the fused operator reads K once: its own roofline against one pass
         one = (hi - lo) * N * 4
         rec["normal_operator"] = {"kernel": "normal_rows_kernel + normal_sum/final", "kernel_ms": round(normal_ms, 4),
@@ -458,7 +585,10 @@ def main():
     ap.add_argument("--generic", action="store_true", help="disable the fused m_step (rule-by-rule HIP path)")
     ap.add_argument("--no-kernel-timer", action="store_true", help="skip the in-region HIP-event kernel timing (A/B)")
     ap.add_argument("--no-sub", action="store_true", help="headline line only (no stop_rate_1 / c5 / c4 records)")
-    ap.add_argument("--pgd-kernel", type=int, default=0, help="PXA_TUNE_PGD_KERNEL (0 auto, 1 tile kernel, 5 march kernel)")
+    ap.add_argument("--only", default="", help="run only this sub-record (c2_4096 | c5 | c4 | c3) and print it (profiling)")
+    ap.add_argument("--c4096-steps", type=int, default=50, help="c2_4096 record: timed PGD steps at 4096^2 (0 = skip)")
+    ap.add_argument("--c3-n", type=int, default=1024, help="c3 record: volume edge (0 = skip)")
+    ap.add_argument("--c3-steps", type=int, default=10)
     ap.add_argument("--c5-images", type=int, default=512)
     ap.add_argument("--c5-n", type=int, default=512)
     ap.add_argument("--c5-steps", type=int, default=20)
@@ -489,17 +619,27 @@ def main():
     backend = None
     if distributed:
         backend = os.environ.get("PXA_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI; gloo for rehearsals
+        import datetime
+
+        tmo = datetime.timedelta(seconds=float(os.environ.get("PXA_DIST_TIMEOUT", "120")))  # a hung rendezvous fails
         if backend == "nccl":
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", dev))
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", dev), timeout=tmo)
         else:
-            dist.init_process_group(backend=backend)
+            dist.init_process_group(backend=backend, timeout=tmo)
     if not pyxu_amd.native_loaded():
         raise RuntimeError("libpyxu_amd.so not loaded")
     from pyxu_amd import _dev
 
-    _dev.tuning(_dev.TUNE_PGD_KERNEL, args.pgd_kernel)
     ctx = Ctx(world, rank, dist, coll_device="cpu" if backend == "gloo" else "cuda")
 
+    if args.only:
+        fn = {"c2_4096": bench_c2_4096, "c5": bench_c5, "c4": bench_c4, "c3": bench_c3}[args.only]
+        rec = fn(ctx, args)
+        if rank == 0:
+            print(json.dumps({"only": args.only, **rec}), flush=True)
+        if distributed:
+            dist.destroy_process_group()
+        return
     n0 = n1 = args.n
     N = n0 * n1
     sr = args.stop_rate or auto_stop_rate(args.steps)
@@ -509,7 +649,7 @@ def main():
                                                        prime_s=args.prime_seconds, kernel_timer=not args.no_kernel_timer)
     fused = slvr._plan is not None
     stack = slvr._plan["stack"] if fused else 1
-    kname, kshort = last_pgd_kernel()
+    mode, bpp = last_pgd_mode()
     del slvr
 
     sub = {}
@@ -521,15 +661,22 @@ def main():
                               "ms_per_step": round(1e3 * e1 / args.steps, 4), "stop_rate": 1, "steps": args.steps}
         del f, g
         torch.cuda.empty_cache()
+        if args.c4096_steps > 0:
+            sub["c2_4096"] = bench_c2_4096(ctx, args)
+            torch.cuda.empty_cache()
         sub["c5"] = bench_c5(ctx, args)
         torch.cuda.empty_cache()
         sub["c4"] = bench_c4(ctx, args)
+        torch.cuda.empty_cache()
+        if args.c3_n > 0:
+            sub["c3"] = bench_c3(ctx, args)
+            torch.cuda.empty_cache()
 
     if rank == 0:
         value = world * args.steps / elapsed_max
         roof = None
         if kern_ms is not None:
-            roof = roofline(N * stack, kern_ms, measured_traffic(kname, f"{n0}x{n1}"), kname)
+            roof = roofline(N * stack, kern_ms, bpp, f"{n0}x{n1}", mode=mode)
             roof["launches_timed"] = launches
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
@@ -557,7 +704,7 @@ def main():
             "config": {"workload": f"PGD {n0}x{n1} Gaussian(sigma=2) deblur + lam*env_mu(L21 o Grad) TV, PositiveOrthant",
                        "image": [n0, n1], "images_per_gpu": 1, "stop_rate": sr,
                        "stop_crit": "MaxIter | RelError" + (f" (global, {'RCCL' if backend == 'nccl' else backend} all-reduce)" if world > 1 else ""),
-                       "fused_m_step": fused, "pgd_kernel": kshort,
+                       "fused_m_step": fused, "pgd_launch": mode,
                        "parallelism": f"independent images x{world} (one per rank)"},
             "roofline": roof,
             "cpu_baseline": cpu,

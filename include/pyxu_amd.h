@@ -48,18 +48,14 @@ extern "C" {
 #define PXA_MODE_EDGE 4
 
 /* Kernel-selection knobs (pxa_tuning). */
-#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 auto (march kernel where it applies, else the tile
-                                 kernel), 1 tile kernel, 4 tile kernel with the item-order epilogue,
-                                 5 march kernel where it applies */
+#define PXA_TUNE_PGD_KERNEL 0 /* reserved (round 2's kernel variants were removed; 0 = the tile kernel) */
 #define PXA_TUNE_NORMAL_DIAG 1 /* pxa_dense_normal timing probes (WRONG results, measurement only): 0 off,
                                   1 no x loads, 2 no cross-wave reduction, 3 no LDS accumulator */
-#define PXA_TUNE_PGD_PRIO 2 /* fused PGD tile kernel wave priorities (s_setprio): 0 none, 1 static per
-                               workgroup by (block >> 8) & 3, 2 memory phases high / compute low,
-                               3 static by (block >> 3) & 3, 4 = 1 + 2 */
-#define PXA_TUNE_PGD_DIAG 3 /* march-kernel timing probes (WRONG results, measurement only): bit 0 no
-                               passes A / B, bit 1 no LDS-DMA, bit 2 no pass A, bit 3 no pass B,
-                               bit 4 no TV term, bit 5 timing trace (pxa_pgd_march_trace) */
-#define PXA_TUNE_MARCH_BANDS 4 /* march kernel: 16-row bands per workgroup (0 auto: ~4 workgroups per CU) */
+#define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel: bit 5 s_memtime phase trace (pxa_pgd_tile_trace) */
+#define PXA_TUNE_PGD_STAGGER 6 /* fused PGD tile kernel A/B probe: v = (sel << 8) | n delays the workgroups
+                                  picked by `sel` in the first dispatch round by n x 1024 cycles (s_sleep) */
+#define PXA_TUNE_PDS_EVENTS 5 /* measurement hook: > 0 makes pxa_pds_step record HIP events around each
+                                 of its kernels (pxa_pds_kernel_ms) */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */
@@ -173,6 +169,12 @@ int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, co
 int pxa_row_reduce_pow(int dtype, int64_t rows, int64_t n, double p, const void* x, const void* y, double* out,
                        void* work, void* stream);
 
+/* RelError statistics from the fused PGD step's per-tile partials (pxa_pgd_tv2d_step[_y] with
+ * `partials`): out[0 * rows + r] = sum (x_new - x)^2 and out[1 * rows + r] = sum x^2 over the per_row
+ * consecutive tiles of stack row r, fixed summation order.  At stop_rate 1 the criterion's stored x_prev
+ * IS the step's x, so this replaces the separate pass over x and x_prev (stop.py:353-382).  `out` may
+ * be device or pinned (device-mapped) host memory. */
+int pxa_tile_partials_fold(int64_t rows, int64_t per_row, const double* partials, double* out, void* stream);
 /* RelError.stop in one pass (opt/stop.py:353-382, norm=2): out[0:rows] = sum (x - x_prev)^2 and
  * out[rows:2 rows] = sum x_prev^2 per row (same bits as pxa_row_reduce DIFFSQ / SUMSQ), and, when
  * x_copy is not NULL, x_copy = x (the `x.copy()` the criterion keeps, stop.py:381).  `out` may be
@@ -342,6 +344,16 @@ int pxa_set_diag(int dtype, int64_t rows, int64_t ld, int64_t off, double value,
 /* dst (cols x rows) = src (rows x cols)^T (LinOp.asarray / TransposeRule.asarray, arithmetic.py:1496). */
 int pxa_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* dst, void* stream);
 
+/* Directional contraction of a stacked derivative output: Sum o DiagonalOp o {Gradient, Hessian} of
+ * DirectionalDerivative / DirectionalGradient / DirectionalLaplacian / DirectionalHessian
+ * (operator/linop/diff.py:1938-2759).  x and y hold S stacked problems of N pixels:
+ *   adjoint = 0: y[s][g][p] = sum_{j<J} w[g][j][p] * x[s][j % K][p]              x: (S, K, N) -> y: (S, G, N)
+ *   adjoint = 1: y[s][k][p] = sum_{g<G} sum_{j<J, j%K==k} w[g][j][p] * x[s][g][p]  x: (S, G, N) -> y: (S, K, N)
+ * w: (G, J, N) when wp = 1, or (G, J) applied at every pixel when wp = 0; J a multiple of K.  Products are
+ * rounded, then added in (j, g) order (the reference's DiagonalOp then numpy.sum). */
+int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int64_t N, const void* w, int64_t wp,
+                     const void* x, void* y, int adjoint, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Fused solver steps (the whole m_step of a recognised problem in one launch).
  *
@@ -361,20 +373,32 @@ int pxa_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* 
  * alias x or x_prev.  If `partials` is not NULL, each workgroup writes (sum (x_new-x)^2, sum x^2)
  * for RelError into partials[2*blk..] (double) — pxa_pgd_tv2d_partials_count() gives the number of
  * workgroups.  prox codes: 0 none, 1 positive orthant, 2 l1 with weight prox_w.
- * Two kernels compute the same bits: the march kernel (fp32, blur radius <= 6, n1 % 4 == 0, 16-B
- * aligned arrays, no partials; 64-column strips marched in 16-row bands with the next band's rows in
- * flight) and the tile kernel (everything else).  pxa_pgd_tv2d_last_kernel() names the one the
- * calling thread's last successful pxa_pgd_tv2d_step launched: 1 tile, 2 march (0 before any).
+ * pxa_pgd_tv2d_last_kernel() names the mode of the calling thread's last successful launch:
+ * 1 classic (x, x_prev -> x_new), 2 seed (x, x_prev -> x_new, y_next), 3 y-state (y, x -> x_new,
+ * y_next); 0 before any.
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
 int pxa_pgd_tv2d_last_kernel(void);
-/* Diagnostics: s_memtime stamps of the march kernel's last launch under PXA_TUNE_PGD_DIAG bit 5
- * (workgroups 0 and grid/2, waves 0..3, bands 0..15, 8 points per band; n <= 1024 words). */
-int pxa_pgd_march_trace(uint64_t* host_out, int n);
+/* Diagnostics: s_memtime stamps of the tile kernel's last launch under PXA_TUNE_PGD_DIAG bit 5
+ * (workgroups 0, 1, grid/2, grid-1; waves 0..3; 8 phase points; n <= 128 words). */
+int pxa_pgd_tile_trace(uint64_t* host_out, int n);
 int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
                       const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
                       const void* x_prev, const void* hty, void* x_new, double* partials, void* stream);
+/* The same step with the momentum point carried as solver state (replaces the same reference lines,
+ * pgd.py:173-191; the arithmetic is pxa_pgd_tv2d_step's, bit for bit):
+ *   y == NULL (seed):  yk from (x, x_prev, a) as above;
+ *   y != NULL:         yk = y (x_prev is ignored and may be NULL);
+ * and besides x_new the epilogue writes y_next = (x_new - x) * a_next + x_new, i.e. the next
+ * iteration's yk with its momentum a_next (the same fma the window load would evaluate).  Every stencil
+ * of the step reads yk over a 2R halo, x only at the tile pixels: the steady-state launch reads one
+ * haloed array instead of two.  y_next must not alias x, x_prev, y or x_new. */
+int pxa_pgd_tv2d_step_y(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0,
+                        const int32_t* off0, const double* coef0, int nt1, const int32_t* off1, const double* coef1,
+                        double h0, double h1, double lam, double mu, double a, double a_next, double tau, int prox,
+                        double prox_w, const void* x, const void* x_prev, const void* y, const void* hty, void* x_new,
+                        void* y_next, double* partials, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * FFT LinOp (operator/linop/fft/fft.py:257-379).  `stack` arrays of complex values (interleaved
@@ -403,6 +427,11 @@ int pxa_real_to_complex(int dtype, int64_t n, const void* x, void* z, void* stre
 /* x[i] = Re z[i] (FFT(real=True).adjoint output, fft.py:370-379); n complex elements. */
 int pxa_complex_real_part(int dtype, int64_t n, const void* z, void* x, void* stream);
 
+/* Measurement hook: with pxa_tuning(PXA_TUNE_PDS_EVENTS, 1), pxa_pds_step records HIP events around its
+ * three kernels (at most 64 steps).  This call waits for the last of them and writes into ms_abc[3] the
+ * summed durations of kernels A (axis-0 march), B (in-plane G + update) and C (dual update) over the
+ * recorded steps, then (reset != 0) forgets them.  Returns the number of steps (>= 0) or an error. */
+int pxa_pds_kernel_ms(double* ms_abc, int reset);
 /* ---------------------------------------------------------------------------------------------
  * Fused primal-dual splitting iteration (replaces PD3O.m_step, opt/solver/pds.py:747-761, algo 0, and
  * CondatVu.m_step, pds.py:429-442, algo 1) for f = 1/2 ||S . - y||^2, K = Gradient over the D trailing

@@ -28,6 +28,17 @@ __all__ = [
     "hessian_components",
     "hessian_apply",
     "hessian_adjoint",
+    "gaussian_kernel1d",
+    "gd_kernels",
+    "stack_apply",
+    "stack_adjoint",
+    "gd_gradient_comps",
+    "gd_hessian_comps",
+    "fd_hessian_comps",
+    "unit_direction",
+    "outer_triu",
+    "contract_apply",
+    "contract_adjoint",
     "laplacian_apply",
     "l1_prox",
     "l21_apply",
@@ -431,6 +442,126 @@ def laplacian_apply(x, arg_shape):
     return out
 
 
+# ----------------------------------------------------------------------------- Gaussian derivatives, stacks
+def gaussian_kernel1d(sigma, order, radius):
+    """scipy.ndimage._filters._gaussian_kernel1d (scipy>=1.11,<2, called at diff.py:343 and filter.py:305):
+    the float64 Gaussian on [-radius, radius] normalised by its sum; order n via the polynomial recursion."""
+    x = np.arange(-radius, radius + 1)
+    phi = np.exp(-0.5 / (sigma * sigma) * x**2)
+    phi = phi / phi.sum()
+    if order == 0:
+        return phi
+    rng = np.arange(order + 1)
+    q = np.zeros(order + 1)
+    q[0] = 1
+    Q = np.diag(rng[1:], 1) + np.diag(np.ones(order) / -(sigma * sigma), -1)
+    for _ in range(order):
+        q = Q.dot(q)
+    return (x[:, None] ** rng).dot(q) * phi
+
+
+def gd_kernels(arg_shape, order, sigma=1.0, truncate=3.0, sampling=1.0, dtype=np.float64):
+    """``PartialDerivative.gaussian_derivative`` kernels (diff.py:885-919 -> _GaussianDerivative
+    :264-350): on EVERY axis the flipped order-``order[a]`` Gaussian derivative of sigma / sampling pixels,
+    radius int(truncate * sigma_pix + 0.5), divided by sampling**order[a]."""
+    D = len(arg_shape)
+    t = lambda v: tuple(v) if isinstance(v, (list, tuple)) else (v,) * D  # noqa: E731
+    sigma, truncate, sampling = t(sigma), t(truncate), t(sampling)
+    kernels, centers = [], []
+    for a in range(D):
+        s_pix = sigma[a] / sampling[a]
+        r = int(truncate[a] * float(s_pix) + 0.5)
+        k = np.flip(gaussian_kernel1d(s_pix, order[a], r)) / sampling[a] ** order[a]
+        kernels.append(k.astype(dtype))
+        centers.append(r)
+    return kernels, centers
+
+
+def stack_apply(x, arg_shape, comps):
+    """vstack of stencils (blocks.py:660-679): comps = [(kernels, centers)], direction-major output."""
+    return np.concatenate([stencil_apply(x, arg_shape, k, c) for k, c in comps], axis=-1)
+
+
+def stack_adjoint(z, arg_shape, comps):
+    """vstack adjoint: sum_j S_j^T z_j, left to right (blocks.py:838-860)."""
+    N = int(np.prod(arg_shape))
+    out = 0
+    for j, (k, c) in enumerate(comps):
+        out = out + stencil_adjoint(z[..., j * N:(j + 1) * N], arg_shape, k, c)
+    return out
+
+
+def gd_gradient_comps(arg_shape, dtype, directions=None, **gd):
+    directions = tuple(range(len(arg_shape))) if directions is None else tuple(directions)
+    comps = []
+    for d in directions:
+        order = [0] * len(arg_shape)
+        order[d] = 1
+        comps.append(gd_kernels(arg_shape, order, dtype=dtype, **gd))
+    return comps
+
+
+def gd_hessian_comps(arg_shape, dtype, directions="all", **gd):
+    """Hessian(diff_method="gd") (diff.py:1591-1797): components of hessian_components(), Gaussian derivatives."""
+    return [gd_kernels(arg_shape, order, dtype=dtype, **gd) for order, _ in hessian_components(arg_shape, directions)]
+
+
+def fd_hessian_comps(arg_shape, dtype, directions="all"):
+    return [diff_kernels(arg_shape, order, scheme, dtype=dtype) for order, scheme in hessian_components(arg_shape, directions)]
+
+
+def unit_direction(d, dtype):
+    """direction / ||direction||_2 over axis 0, in the direction dtype (diff.py:2012)."""
+    d = np.asarray(d)
+    return (d / np.linalg.norm(d, axis=0, keepdims=True)).astype(dtype)
+
+
+def outer_triu(n1, n2):
+    """Upper-triangular outer product, off-diagonal terms doubled, Hessian component order
+    (diff.py:2020-2033)."""
+    ndim = n1.shape[0]
+    o = n1[:, None, ...] * n2[None, ...]
+    if ndim == 1:
+        return o.reshape(1, *o.shape[2:])
+    o = o.reshape(ndim**2, *o.shape[2:])
+    dummy = np.arange(ndim**2).reshape(ndim, ndim)
+    o[dummy[np.triu_indices(ndim, k=1)].ravel()] *= 2
+    return o[dummy[np.triu_indices(ndim, k=0)].ravel()]
+
+
+def contract_apply(w, d, N):
+    """Sum o DiagonalOp of the directional operators (diff.py:2049-2060): y_g = sum_j w[g, j] * d_{j mod K},
+    each product rounded, summed left to right.  w: (G, J) or (G, J, N); d: (..., K*N)."""
+    G, J = w.shape[:2]
+    K = d.shape[-1] // N
+    dd = d.reshape(*d.shape[:-1], K, N)
+    out = []
+    for g in range(G):
+        acc = None
+        for j in range(J):
+            wj = w[g, j] if w.ndim == 2 else w[g, j].reshape(-1)
+            t = wj * dd[..., j % K, :]
+            acc = t if acc is None else acc + t
+        out.append(acc)
+    return np.concatenate(out, axis=-1)
+
+
+def contract_adjoint(w, z, N, K):
+    """Adjoint of contract_apply: t_k = sum_g sum_{j mod K = k} w[g, j] * z_g."""
+    G, J = w.shape[:2]
+    zz = z.reshape(*z.shape[:-1], G, N)
+    out = []
+    for k in range(K):
+        acc = None
+        for g in range(G):
+            for j in range(k, J, K):
+                wj = w[g, j] if w.ndim == 2 else w[g, j].reshape(-1)
+                t = wj * zz[..., g, :]
+                acc = t if acc is None else acc + t
+        out.append(acc)
+    return np.concatenate(out, axis=-1)
+
+
 # ----------------------------------------------------------------------------- proxes
 def l1_prox(x, tau):
     """``L1Norm.prox`` (operator/func/norm.py:47-52): ``fmax(0, |x| - tau) * sign(x)``."""
@@ -528,10 +659,11 @@ def deblur_tv_grad(x, blur, y, lam, mu, grad_kw, tv="l21"):
 
 
 # ----------------------------------------------------------------------------- solvers
-def pgd(x0, grad, prox, tau, n_iter, d=75, acceleration=True, history=False):
+def pgd(x0, grad, prox, tau, n_iter, d=75, acceleration=True, history=False, snap=None):
     """``PGD.m_init``/``m_step`` (opt/solver/pgd.py:129-191); returns ``(x, x_prev[, hist])``.
 
     ``grad(y)`` and ``prox(z, tau)`` are the composite callables; ``tau`` the (fp-coerced) step.
+    ``snap``: optional dict whose keys are iteration counts k; snap[k] receives a copy of x after k steps.
     """
     dt = x0.dtype.type
     tau = dt(tau)
@@ -548,6 +680,8 @@ def pgd(x0, grad, prox, tau, n_iter, d=75, acceleration=True, history=False):
         x_prev, x = x, prox(z, tau)
         if history:
             hist.append(relerror(x, x_prev))
+        if snap is not None and (k + 1) in snap:
+            snap[k + 1] = x.copy()
     return (x, x_prev, hist) if history else (x, x_prev)
 
 
@@ -584,8 +718,9 @@ def condat_vu_step_sizes(beta, K_lipschitz, dtype, quadratic_f=True):
     return dt(tau), dt(sigma), dt(delta), dt(1.0)
 
 
-def pd3o(x0, grad_f, prox_g, K, KT, fprox_h, tau, sigma, rho, n_iter, z0=None, u0=None, history=False):
-    """``PD3O.m_init``/``m_step`` (pds.py:722-761).  ``prox_g=None`` means NullFunc (identity prox)."""
+def pd3o(x0, grad_f, prox_g, K, KT, fprox_h, tau, sigma, rho, n_iter, z0=None, u0=None, history=False, snap=None):
+    """``PD3O.m_init``/``m_step`` (pds.py:722-761).  ``prox_g=None`` means NullFunc (identity prox).
+    ``snap``: optional dict of iteration counts k -> (x, z) copies after k steps."""
     dt = x0.dtype.type
     tau, sigma, rho = dt(tau), dt(sigma), dt(rho)
     x = x0
@@ -602,11 +737,13 @@ def pd3o(x0, grad_f, prox_g, K, KT, fprox_h, tau, sigma, rho, n_iter, z0=None, u
         u = (1 - rho) * u + rho * u_temp
         if history:
             hist.append((relerror(x, x_prev), relerror(z, z_prev)))
+        if snap is not None and (_ + 1) in snap:
+            snap[_ + 1] = (x.copy(), z.copy())
     return (x, z, u, hist) if history else (x, z, u)
 
 
-def condat_vu(x0, grad_f, prox_g, K, KT, fprox_h, tau, sigma, rho, n_iter, z0=None, history=False):
-    """``CondatVu.m_step`` (pds.py:429-442)."""
+def condat_vu(x0, grad_f, prox_g, K, KT, fprox_h, tau, sigma, rho, n_iter, z0=None, history=False, snap=None):
+    """``CondatVu.m_step`` (pds.py:429-442).  ``snap``: as in pd3o()."""
     dt = x0.dtype.type
     tau, sigma, rho = dt(tau), dt(sigma), dt(rho)
     x = x0
@@ -622,6 +759,8 @@ def condat_vu(x0, grad_f, prox_g, K, KT, fprox_h, tau, sigma, rho, n_iter, z0=No
         x = rho * x_temp + (1 - rho) * x
         if history:
             hist.append((relerror(x, x_prev), relerror(z, z_prev)))
+        if snap is not None and (_ + 1) in snap:
+            snap[_ + 1] = (x.copy(), z.copy())
     return (x, z, hist) if history else (x, z)
 
 

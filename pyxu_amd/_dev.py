@@ -23,11 +23,18 @@ def _torch():
     return torch
 
 
-def wait_event(ev):
-    """Wait for a recorded HIP event by polling it: a stop check waits a few tens of microseconds, and
-    a blocking hipEventSynchronize wakes the host up later than a poll notices the event."""
+def wait_event(ev, spin_s=1e-4):
+    """Wait for a recorded HIP event: poll it for up to `spin_s` seconds (a stop check usually waits a few
+    tens of microseconds, and a blocking hipEventSynchronize wakes the host up later than a poll notices
+    the event), then yield the GIL between polls so that a long wait does not starve other threads."""
+    import time
+
+    if ev.query():
+        return
+    t_end = time.perf_counter() + spin_s
     while not ev.query():
-        pass
+        if time.perf_counter() > t_end:
+            time.sleep(0)
 
 
 def dtcode(t) -> int:
@@ -157,8 +164,9 @@ def storage_exclusive(t) -> bool:
 
 
 TUNE_NORMAL_DIAG = 1  # PXA_TUNE_NORMAL_DIAG: pxa_dense_normal timing probes (wrong results)
-TUNE_PGD_KERNEL = 0  # PXA_TUNE_PGD_KERNEL: 0 auto, 1 tile kernel, 4 item-order epilogue, 5 march kernel
-TUNE_MARCH_BANDS = 4  # PXA_TUNE_MARCH_BANDS: march kernel bands per workgroup (0 auto)
+TUNE_PGD_DIAG = 3  # PXA_TUNE_PGD_DIAG: bit 5 = s_memtime phase trace of the PGD tile kernel
+TUNE_PGD_STAGGER = 6  # PXA_TUNE_PGD_STAGGER: (sel << 8) | n, delayed first-round workgroups (A/B probe)
+TUNE_PDS_EVENTS = 5  # PXA_TUNE_PDS_EVENTS: per-kernel HIP events inside pxa_pds_step (pds_kernel_ms)
 
 
 def tuning(key, value=-1):
@@ -176,6 +184,11 @@ def empty(shape, like):
 
 def empty_f64(shape, like):
     return _torch().empty(shape, dtype=_torch().float64, device=like.device)
+
+
+def to_device_like(a, like):
+    """Host numpy array -> device tensor of `like`'s dtype (an upload, no compute)."""
+    return _torch().as_tensor(np.ascontiguousarray(a), device=like.device).to(like.dtype)
 
 
 def empty_like(t):
@@ -456,6 +469,15 @@ def set_diag(out, rows, ld, off, value):
     return out
 
 
+def dir_contract(w, wp, x, S, G, J, K, N, adjoint=False):
+    """pxa_dir_contract: y = sum_j w[g, j] * x[j % K] (apply, (S, K, N) -> (S, G, N)) or its adjoint."""
+    x, w = require(x, "x"), require(w, "w")
+    y = empty((S, K if adjoint else G, N), x)
+    check(lib.pxa_dir_contract(dtcode(x), int(S), int(G), int(J), int(K), int(N), ptr(w), int(wp), ptr(x), ptr(y),
+                               int(bool(adjoint)), stream()), "pxa_dir_contract")
+    return y
+
+
 def transpose(x):
     """(rows, cols) -> contiguous (cols, rows)."""
     x = require(x)
@@ -484,6 +506,15 @@ def relerr_stats(x, x_prev, out, copy=True):
     check(lib.pxa_relerr_stats(dtcode(x), rows, n, ptr(x), ptr(x_prev), ptr(xc) if copy else None, out.data_ptr(),
                                ptr(work), stream()), "pxa_relerr_stats")
     return xc
+
+
+def tile_partials_fold(parts, rows, per_row, out):
+    """RelError statistics from the fused PGD step's per-tile partials (pxa_tile_partials_fold):
+    out (contiguous float64 (2, rows), device or pinned host) = per-row sum (x_new - x)^2, sum x^2."""
+    assert out.is_contiguous() and out.numel() == 2 * rows
+    check(lib.pxa_tile_partials_fold(int(rows), int(per_row), parts.data_ptr(), out.data_ptr(), stream()),
+          "pxa_tile_partials_fold")
+    return out
 
 
 def row_reduce(op, x, y=None, out=None):
@@ -739,6 +770,24 @@ def pgd_tv2d_step(x, x_prev, hty, x_new, stack, y_images, n0, n1, taps0, taps1, 
     return x_new
 
 
+def pgd_tv2d_step_y(x, x_prev, y, hty, x_new, y_next, a, a_next, tau, prox, prox_w, pre, partials=None):
+    """One fused PGD iteration with the momentum point carried as state (pxa_pgd_tv2d_step_y): with
+    y = None the window is formed from (x, x_prev, a) (seed), else it is y; writes x_new and
+    y_next = (x_new - x) * a_next + x_new.  `pre`: pgd_tv2d_args(...)."""
+    ev = _TIMER.begin() if _TIMER is not None else None  # measurement hook (bench.py), normally None
+    check(
+        lib.pxa_pgd_tv2d_step_y(
+            dtcode(x), *pre, float(a), float(a_next), float(tau), int(prox), float(prox_w), x.data_ptr(),
+            x_prev.data_ptr() if y is None else None, y.data_ptr() if y is not None else None, hty.data_ptr(),
+            x_new.data_ptr(), y_next.data_ptr(), ptr(partials) if partials is not None else None, stream(),
+        ),
+        "pxa_pgd_tv2d_step_y",
+    )
+    if ev is not None:
+        _TIMER.end(ev)
+    return x_new
+
+
 _PDS_W = 17  # per-axis tap slots of pxa_pds_step (2 * 8 + 1)
 
 
@@ -761,6 +810,15 @@ def pds_step(algo, pre, x, u, z, hty, x_out, u_out, z_out, work_q, work_w, nseg=
                            p(work_q), p(work_w), int(nseg), stream()), "pxa_pds_step")
     if ev is not None:
         _TIMER.end(ev)
+
+
+def pds_kernel_ms(reset=True):
+    """(steps, [ms A, ms B, ms C] summed) of the pxa_pds_step calls recorded under TUNE_PDS_EVENTS."""
+    buf = (ct.c_double * 3)()
+    n = int(lib.pxa_pds_kernel_ms(ct.cast(buf, ct.c_void_p), int(bool(reset))))
+    if n < 0:
+        check(n, "pxa_pds_kernel_ms")
+    return n, [buf[0], buf[1], buf[2]]
 
 
 # ------------------------------------------------------------------ FFT

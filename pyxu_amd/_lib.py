@@ -47,6 +47,7 @@ EXPORTS = {
     "pxa_row_reduce_pow": (i32, [i32, i64, i64, f64, vp, vp, vp, vp, vp]),
     "pxa_relerr_stats_workspace_bytes": (sz, [i64, i64]),
     "pxa_relerr_stats": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp]),
+    "pxa_tile_partials_fold": (i32, [i64, i64, vp, vp, vp]),
     "pxa_stencil_axis": (i32, [i32, i64, i32, P_i64, i32, i32, P_i32, P_f64, i32, vp, i64, vp, i64, f64, vp]),
     "pxa_stencil_sep_workspace_bytes": (sz, [i32, i64, i32, P_i64, P_int]),
     "pxa_stencil_sep": (i32, [i32, i64, i32, P_i64, P_int, P_i32, P_f64, vp, i64, vp, i64, f64, vp, vp]),
@@ -71,13 +72,19 @@ EXPORTS = {
     "pxa_bool_reduce": (i32, [i64, i32, vp, vp, vp]),
     "pxa_set_diag": (i32, [i32, i64, i64, i64, f64, vp, vp]),
     "pxa_transpose": (i32, [i32, i64, i64, vp, vp, vp]),
+    "pxa_dir_contract": (i32, [i32, i64, i64, i64, i64, i64, vp, i64, vp, vp, i32, vp]),
     "pxa_pgd_tv2d_partials_count": (i32, [i64, i64, i64]),
     "pxa_pgd_tv2d_last_kernel": (i32, []),
-    "pxa_pgd_march_trace": (i32, [vp, i32]),
+    "pxa_pgd_tile_trace": (i32, [vp, i32]),
     "pxa_pgd_tv2d_step": (
         i32,
         [i32, i64, i64, i64, i64, i32, P_i32, P_f64, i32, P_i32, P_f64, f64, f64, f64, f64, f64, f64, i32, f64,
          vp, vp, vp, vp, vp, vp],
+    ),
+    "pxa_pgd_tv2d_step_y": (
+        i32,
+        [i32, i64, i64, i64, i64, i32, P_i32, P_f64, i32, P_i32, P_f64, f64, f64, f64, f64, f64, f64, f64, i32, f64,
+         vp, vp, vp, vp, vp, vp, vp, vp],
     ),
     "pxa_fft": (i32, [i32, i32, P_i64, i32, P_int, i64, i32, vp, vp, vp]),
     "pxa_fft_workspace_bytes": (sz, [i32, i32, P_i64, i32, P_int, i64]),
@@ -85,6 +92,7 @@ EXPORTS = {
     "pxa_complex_mul": (i32, [i32, i64, i64, vp, vp, i32, vp, vp]),
     "pxa_real_to_complex": (i32, [i32, i64, vp, vp, vp]),
     "pxa_complex_real_part": (i32, [i32, i64, vp, vp, vp]),
+    "pxa_pds_kernel_ms": (i32, [vp, i32]),
     "pxa_pds_step": (
         i32,
         [i32, i32, P_i64, P_i32, P_i32, P_f64, P_f64, P_f64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp],

@@ -522,17 +522,32 @@ class LinOp(DiffMap):
         return arithmetic.TransposeRule(op=self).op()
 
     def estimate_lipschitz(self, **kwargs):
-        """Spectral norm estimate (operator.py:1392-1466).
+        """A Lipschitz constant of the operator (operator.py:1440-1498).
 
-        method="svd" (default here) runs a device power iteration on A^T A (``n_iter``, ``tol``);
-        it converges to the optimal constant the reference's "svd" method returns.  The reference's
-        default ("trace", Hutch++) is an upper bound; the power iteration is used for both.
+        method="trace" (the default, as in the reference): sqrt of the Hutch++ estimate of
+        tr(A^T A) (or tr(A A^T) when codim < dim) = ||A||_F, an upper bound of ||A||_2, with m = 126
+        queries (pyxu_amd.math.linalg.hutchpp; `m`, `seed` forwarded).
+        method="svd": the optimal constant ||A||_2 by a device power iteration on A^T A (``n_iter``,
+        ``tol``, ``seed``), which converges to what the reference's svdvals(k=1) returns.
         """
-        import torch
+        method = str(kwargs.get("method", "trace")).lower().strip()
+        if method == "trace":
+            if self.shape == (1, 1):
+                return self._power_lipschitz(**kwargs)
+            from pyxu_amd.math.linalg import hutchpp
 
+            op = self.gram() if (self.codim >= self.dim) else self.cogram()
+            tr = hutchpp(op, m=int(kwargs.get("m", 126)), seed=kwargs.get("seed"))
+            return float(np.sqrt(max(tr, 0.0)))
+        if method == "svd":
+            return self._power_lipschitz(**kwargs)
+        raise NotImplementedError(f"method={method!r}")
+
+    def _power_lipschitz(self, **kwargs):
+        """||A||_2 by power iteration on A^T A, every product on the device."""
         n_iter = int(kwargs.get("n_iter", 200))
         tol = float(kwargs.get("tol", 1e-6))
-        seed = int(kwargs.get("seed", 0))
+        seed = int(kwargs.get("seed", 0) or 0)
         from pyxu_amd.util import to_device
 
         x = np.random.default_rng(seed).standard_normal(self.dim).astype(pxrt.getPrecision().value)
@@ -554,7 +569,7 @@ class LinOp(DiffMap):
     def svdvals(self, k=1, which="LM", **kwargs):
         if k != 1 or which.upper() != "LM":
             raise NotImplementedError("pyxu_amd: only the largest singular value (k=1, 'LM') is available on device.")
-        return np.array([self.estimate_lipschitz(**kwargs)], dtype=pxrt.getPrecision().value)
+        return np.array([self._power_lipschitz(**kwargs)], dtype=pxrt.getPrecision().value)
 
     def asarray(self, xp=None, dtype=None):
         """Matrix representation (device tensor unless xp is numpy), built column-block-wise."""

@@ -28,13 +28,26 @@ def _on_device(v):
     return getattr(getattr(v, "device", None), "type", "cpu") != "cpu"
 
 
+_SAVE_LOCK = threading.Lock()
+
+
 def _atomic_savez(path, arrays):
-    """np.savez into a sibling temporary file, then rename over `path`."""
+    """np.savez into a temporary file of its own in the same folder, then rename over `path`.  Writers
+    (the caller's writeback() and the asynchronous checkpoint thread) are serialised, and each writes
+    its own temporary file, so a rename never moves a half-written file over `path`."""
     path = plib.Path(path)
-    tmp = path.with_name(path.name + ".tmp")
-    with open(tmp, "wb") as f:
-        np.savez(f, **arrays)
-    os.replace(tmp, path)
+    with _SAVE_LOCK:
+        fd, tmp = tempfile.mkstemp(dir=path.parent, prefix=path.name + ".", suffix=".tmp")
+        try:
+            with os.fdopen(fd, "wb") as f:
+                np.savez(f, **arrays)
+            os.replace(tmp, path)
+        except BaseException:
+            try:
+                os.unlink(tmp)
+            except OSError:
+                pass
+            raise
 
 
 @enum.unique
@@ -168,6 +181,7 @@ class Solver:
                 i += 1
             else:
                 self._astate["mode"] = None
+                self._wb_drain()  # checkpoints of this run are on disk when steps() returns
                 self._cleanup_logger()
                 return
 
@@ -365,11 +379,13 @@ class Solver:
         resolve = ast["stop_crit"].stop_async(self._mstate)
         token = self._spec_begin()
         err = None
+        ast["idx"] += 1  # as on the synchronous path: m_step sees the index of the step after it
         try:
             self.m_step()
         except Exception as e:  # raised only if the check says continue (then the reference calls m_step)
             err = e
         if resolve():
+            ast["idx"] -= 1
             self._spec_rollback(token)
             with ast["lock"]:
                 self._record(idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, log_on)
@@ -377,7 +393,6 @@ class Solver:
                 ast["logger"].info(f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
             self.writeback()
             return False
-        ast["idx"] += 1
         rec = (idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, _ml and log_on)
         with ast["lock"]:
             ast["pending"].append(rec)

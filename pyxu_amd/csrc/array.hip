@@ -183,6 +183,50 @@ __global__ void __launch_bounds__(kBlock) scatter_cols_kernel(int64_t rows, int6
 
 inline unsigned gy(int64_t rows) { return (unsigned)(rows < 1 ? 1 : (rows > 65535 ? 65535 : rows)); }
 
+// Directional contraction of a stacked derivative output (Sum o DiagonalOp o {Gradient, Hessian},
+// diff.py:1938-2759).  apply:   y[s][g][p] = sum_{j < J} w[g][j][p] * x[s][j % K][p]
+//                    adjoint: y[s][k][p] = sum_{g < G} sum_{j % K == k} w[g][j][p] * x[s][g][p]
+// w is (G, J, N) (wp = 1) or (G, J) broadcast over the pixels (wp = 0).  Each product is rounded, then
+// the terms are added in order (j, then g), like the reference's DiagonalOp followed by numpy.sum over
+// the leading axes (no fma contraction).  One thread per (s, p), grid-stride.
+template <typename T, bool ADJ>
+__global__ void __launch_bounds__(kBlock) dir_contract_kernel(int64_t S, int64_t G, int64_t J, int64_t K, int64_t N,
+                                                              const T* __restrict__ w, int64_t wp,
+                                                              const T* __restrict__ x, T* __restrict__ y) {
+#pragma clang fp contract(off)
+  const int64_t total = S * N;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t sidx = q / N, p = q - sidx * N;
+    const int64_t pw = wp ? p : 0, ldw = wp ? N : 1;
+    if constexpr (!ADJ) {
+      const T* xs = x + sidx * K * N + p;
+      T* ys = y + sidx * G * N + p;
+      for (int64_t g = 0; g < G; ++g) {
+        T acc = T(0);
+        for (int64_t j = 0; j < J; ++j) {
+          const T t = w[(g * J + j) * ldw + pw] * xs[(j % K) * N];
+          acc = j == 0 ? t : acc + t;
+        }
+        ys[g * N] = acc;
+      }
+    } else {
+      const T* xs = x + sidx * G * N + p;
+      T* ys = y + sidx * K * N + p;
+      for (int64_t k = 0; k < K; ++k) {
+        T acc = T(0);
+        bool first = true;
+        for (int64_t g = 0; g < G; ++g)
+          for (int64_t j = k; j < J; j += K) {
+            const T t = w[(g * J + j) * ldw + pw] * xs[g * N];
+            acc = first ? t : acc + t;
+            first = false;
+          }
+        ys[k * N] = acc;
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace pxa
 
@@ -339,6 +383,24 @@ int pxa_scatter_cols(int dtype, int64_t rows, int64_t m, const void* y, int64_t 
     gx = gx > cap ? cap : gx;
     hipLaunchKernelGGL((scatter_cols_kernel<T>), dim3((unsigned)gx, gyv), dim3(kBlock), 0, as_stream(stream), rows, m,
                        (const T*)y, n, idx_dev, (T*)out);
+    return last_launch_status();
+  });
+}
+
+int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int64_t N, const void* w, int64_t wp,
+                     const void* x, void* y, int adjoint, void* stream) {
+  PXA_CHECK_ARG(S >= 0 && G >= 1 && K >= 1 && J >= K && J % K == 0 && N >= 0 && (wp == 0 || wp == 1));
+  PXA_CHECK_ARG(w && x && y && x != y);
+  if (S == 0 || N == 0) return PXA_OK;
+  const int grid = grid_for(S * N);
+  hipStream_t st = as_stream(stream);
+  PXA_DISPATCH(dtype, T, {
+    if (adjoint)
+      hipLaunchKernelGGL((dir_contract_kernel<T, true>), dim3(grid), dim3(kBlock), 0, st, S, G, J, K, N, (const T*)w, wp,
+                         (const T*)x, (T*)y);
+    else
+      hipLaunchKernelGGL((dir_contract_kernel<T, false>), dim3(grid), dim3(kBlock), 0, st, S, G, J, K, N, (const T*)w, wp,
+                         (const T*)x, (T*)y);
     return last_launch_status();
   });
 }

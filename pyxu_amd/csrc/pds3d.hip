@@ -199,6 +199,28 @@ inline int tap_window(int nt, const int32_t* off, const double* coef, double (&k
   return R;
 }
 
+// Measurement hook (PXA_TUNE_PDS_EVENTS > 0, bench.py's c3 record): HIP events recorded on the launch stream
+// before kernel A and after kernels A, B and C of every step, so that the per-kernel times of the timed
+// steps are read afterwards (pxa_pds_kernel_ms) without synchronising inside the timed region.
+constexpr int kPdsEventSteps = 64;
+struct PdsEvents {
+  hipEvent_t ev[kPdsEventSteps][4];
+  int created = 0;  // steps whose events exist
+  int used = 0;     // steps recorded since the last read
+};
+static PdsEvents g_pds_ev;
+
+static void pds_event(int k, hipStream_t st) {
+  PdsEvents& E = g_pds_ev;
+  if (E.used >= kPdsEventSteps) return;
+  if (E.used == E.created) {
+    for (int j = 0; j < 4; ++j) (void)hipEventCreate(&E.ev[E.created][j]);
+    ++E.created;
+  }
+  (void)hipEventRecord(E.ev[E.used][k], st);
+  if (k == 3) ++E.used;
+}
+
 template <typename T>
 int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs, const double* coefs,
               const double* diff, const double* scal, int prox, int h_kind, const void* x, const void* u,
@@ -245,6 +267,8 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
   const int64_t M = n1 * n2;
   constexpr int V = kVecN<T>;
 
+  const bool evs = tuning(PXA_TUNE_PDS_EVENTS) > 0;
+  if (evs) pds_event(0, st);
   // ---- kernel A
   const void* q_src = pd3o ? (const void*)x_out : x;  // kernel B's input plane stack
   if (pd3o || !id0) {
@@ -275,6 +299,7 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
     if (e) return e;
     if (!id0) q_src = work_q;
   }
+  if (evs) pds_event(1, st);
 
   // ---- kernel B
   {
@@ -314,6 +339,7 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
     const int e = run_b(pb, pd3o, R, P, st);
     if (e) return e;
   }
+  if (evs) pds_event(2, st);
 
   // ---- kernel C
   {
@@ -342,6 +368,7 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
                : launch_c<T, 1, false>(pc, iso, M, cseg, work_w, z, z_out, st);
     if (e) return e;
   }
+  if (evs) pds_event(3, st);
   return PXA_OK;
 }
 
@@ -353,6 +380,22 @@ using namespace pxa::pds;
 using namespace pxa;
 
 extern "C" {
+
+int pxa_pds_kernel_ms(double* ms_abc, int reset) {
+  PdsEvents& E = g_pds_ev;
+  if (!ms_abc) return PXA_ERR_ARG;
+  ms_abc[0] = ms_abc[1] = ms_abc[2] = 0.0;
+  const int n = E.used;
+  if (n > 0 && hipEventSynchronize(E.ev[n - 1][3]) != hipSuccess) return PXA_ERR_UNSUPPORTED;
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, E.ev[i][k], E.ev[i][k + 1]) != hipSuccess) return PXA_ERR_UNSUPPORTED;
+      ms_abc[k] += ms;
+    }
+  if (reset) E.used = 0;
+  return n;
+}
 
 int pxa_pds_step(int dtype, int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs,
                  const double* coefs, const double* diff, const double* scal, int prox, int h_kind, const void* x,

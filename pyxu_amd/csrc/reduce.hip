@@ -164,6 +164,24 @@ int launch_relerr(int64_t rows, int64_t n, const void* x, const void* p, void* x
   return last_launch_status();
 }
 
+// Fold of the fused PGD kernel's per-tile RelError partials (pgd_tv2d.hip: tile t wrote
+// part[2 t] = sum (x_new - x)^2 and part[2 t + 1] = sum x^2) into out[0][r] / out[1][r] for each stack row
+// r owning tiles [r per_row, (r + 1) per_row): one wavefront per (statistic, row), lane-strided sums in
+// a fixed order + the wave fold, so the result is deterministic run to run.
+__global__ void __launch_bounds__(kBlock) tile_partials_fold_kernel(int64_t rows, int64_t per_row,
+                                                                    const double* __restrict__ part,
+                                                                    double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // q = stat * rows + row
+  if (q >= 2 * rows) return;
+  const int64_t stat = q / rows, r = q - stat * rows;
+  const double* pr = part + 2 * r * per_row + stat;
+  double acc = 0.0;
+  for (int64_t k = lane; k < per_row; k += 64) acc += pr[2 * k];
+  acc = wave_reduce<PXA_RED_SUMSQ>(acc);
+  if (lane == 0) out[q] = acc;
+}
+
 // General Ln row statistic for the stop criteria (stop.py:222-297 -> pxlg.norm(ord=p)):
 // sum |x - y|^p (p > 0), or the count of non-zero entries (p == 0, NumPy's ord=0).  Same partition
 // and fold as row_partial_kernel (deterministic).
@@ -255,6 +273,15 @@ int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, co
       return PXA_ERR_ARG;
   }
 #undef PXA_RED_CASE
+}
+
+int pxa_tile_partials_fold(int64_t rows, int64_t per_row, const double* partials, double* out, void* stream) {
+  PXA_CHECK_ARG(rows >= 1 && per_row >= 1 && partials != nullptr && out != nullptr);
+  const int64_t waves = 2 * rows, per_block = kBlock / kWave;
+  PXA_CHECK_ARG((waves + per_block - 1) / per_block <= 0x7fffffff);
+  hipLaunchKernelGGL(tile_partials_fold_kernel, dim3((unsigned)((waves + per_block - 1) / per_block)), dim3(kBlock), 0,
+                     as_stream(stream), rows, per_row, partials, out);
+  return last_launch_status();
 }
 
 size_t pxa_relerr_stats_workspace_bytes(int64_t rows, int64_t n) { return 2 * pxa_row_reduce_workspace_bytes(rows, n); }

@@ -89,9 +89,9 @@ def allreduce(t, op="sum", group=None):
     dist = _dist()
     ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
     if t.is_cuda and _host_backend(group):
-        h = t.cpu()  # gloo (CPU tests / several ranks sharing one card): stage through the host
+        h = t.cpu()  # gloo host staging (CPU tests / several ranks sharing one card)
         dist.all_reduce(h, op=ops[op], group=group)
-        t.copy_(h)
+        t.copy_(h)  # gloo host staging
         return t
     dist.all_reduce(t, op=ops[op], group=group)
     return t
@@ -115,19 +115,20 @@ def gather_slabs(x_local, n_global, group=None):
         raise ValueError(f"rank {rank} holds {x_local.shape[0]} rows, expected {sizes[rank]}")
     m = max(sizes)
     buf = x_local
-    if x_local.shape[0] != m:
-        buf = torch.zeros((m, *x_local.shape[1:]), dtype=x_local.dtype, device=x_local.device)
-        buf[: x_local.shape[0]] = x_local
+    if x_local.shape[0] != m:  # pad the slab to the largest one (pxa_fill + pxa_copy2d on the device)
+        n_row = int(np.prod(x_local.shape[1:]))
+        buf = _dev_zeros((m, *x_local.shape[1:]), x_local)
+        _dev_copy_rows(x_local, buf, 1, x_local.shape[0] * n_row, 0, 0, 0, 0)
     dev = buf.device
     if buf.is_cuda and _host_backend(group):
-        buf = buf.cpu()
+        buf = buf.cpu()  # gloo host staging
     parts = [torch.empty_like(buf) for _ in range(w)]
-    _dist().all_gather(parts, buf.contiguous(), group=group)
+    _dist().all_gather(parts, buf, group=group)
     if parts[0].is_cuda:  # RCCL: assemble the slabs on the device (pxa_copy2d)
         from pyxu_amd import xp
 
         return xp.concatenate([p[:s] for p, s in zip(parts, sizes)], axis=0)
-    return torch.cat([p[:s] for p, s in zip(parts, sizes)], dim=0).to(dev)  # gloo: host staging
+    return torch.cat([p[:s] for p, s in zip(parts, sizes)], dim=0).to(dev)  # gloo host staging
 
 
 class _ShardedMixin:
@@ -194,22 +195,22 @@ def RowShardedLinOp(mat_local, M, group=None, enable_warnings=True):
 
 # ------------------------------------------------------------------ halo-exchanged slabs
 def _p2p(sends, recvs, group=None):
-    """Point-to-point exchange: sends = [(tensor, peer)], recvs = [(buffer, peer)].  Device tensors
-    go through RCCL directly; with gloo they are staged through the host."""
+    """Point-to-point exchange: sends = [(tensor, peer)], recvs = [(buffer, peer)], all contiguous.
+    Device tensors go through RCCL directly; with gloo they are staged through the host."""
     dist = _dist()
     if not sends and not recvs:
         return
     host = _host_backend(group)
-    stage = lambda t: t.cpu().contiguous() if (host and t.is_cuda) else t.contiguous()  # noqa: E731
+    stage = lambda t: t.cpu() if (host and t.is_cuda) else t  # noqa: E731  (gloo host staging)
     s_bufs = [(stage(t), peer) for t, peer in sends]
-    r_bufs = [(stage(b) if (host and b.is_cuda) else b, b, peer) for b, peer in recvs]
+    r_bufs = [(stage(b), b, peer) for b, peer in recvs]
     ops = [dist.P2POp(dist.isend, t, _global_rank(peer, group), group) for t, peer in s_bufs]
-    ops += [dist.P2POp(dist.irecv, h, _global_rank(peer, group), group) for h, _, peer in r_bufs]
+    ops.extend(dist.P2POp(dist.irecv, h, _global_rank(peer, group), group) for h, _, peer in r_bufs)
     for req in dist.batch_isend_irecv(ops):
         req.wait()
     for h, b, _ in r_bufs:
         if h is not b:
-            b.copy_(h)
+            b.copy_(h)  # gloo host staging
 
 
 def _global_rank(r, group):
@@ -218,75 +219,109 @@ def _global_rank(r, group):
     return _dist().get_global_rank(group, r)
 
 
-def _accumulate(dst, src):
-    """dst += src (contiguous views).  Device tensors: the HIP element-wise kernel; host tensors only
-    occur in the gloo CPU tests of this exchange logic."""
-    if dst.is_cuda:
+# Device-path array movement: every copy, zero fill and accumulation of the exchange runs on the HIP
+# kernels (pxa_copy2d / pxa_fill); torch tensors only arise as buffers (and as host tensors in the gloo
+# CPU tests, handled by the torch fallbacks below).
+def _dev_zeros(shape, like):
+    import torch
+
+    if like.is_cuda:
         from pyxu_amd import _dev
 
-        _dev.axpby(1.0, dst, 1.0, src, out=dst)
+        return _dev.zeros(shape, like)
+    return torch.zeros(shape, dtype=like.dtype)  # gloo CPU tests
+
+
+def _dev_copy_rows(src, dst, rows, n, lds, ldd, src_off, dst_off, accumulate=0):
+    """dst[dst_off + r ldd + i] (+)= src[src_off + r lds + i], r < rows, i < n (element offsets)."""
+    if rows == 0 or n == 0:
+        return dst
+    if src.is_cuda:
+        from pyxu_amd import _dev
+
+        return _dev.copy2d(src, dst, rows, n, lds, ldd, src_off=src_off, dst_off=dst_off, accumulate=accumulate)
+    s2 = src.reshape(-1).as_strided((rows, n), (lds, 1), src_off)  # gloo CPU tests
+    d2 = dst.reshape(-1).as_strided((rows, n), (ldd, 1), dst_off)
+    if accumulate:
+        d2 += s2
     else:
-        dst.add_(src)
+        d2.copy_(s2)
+    return dst
+
+
+def _planes(x, p0, p1):
+    """Contiguous copy of planes [p0, p1) of every stack row of x (S, P, M)."""
+    S, P, M = x.shape
+    out = _dev_zeros((S, p1 - p0, M), x) if not x.is_cuda else _empty(x, (S, p1 - p0, M))
+    return _dev_copy_rows(x, out, S, (p1 - p0) * M, P * M, (p1 - p0) * M, p0 * M, 0)
+
+
+def _empty(like, shape):
+    import torch
+
+    return torch.empty(shape, dtype=like.dtype, device=like.device)
 
 
 def halo_pad(x, lo, hi, group=None):
     """x: (S, nl, M) slab of axis-0 planes owned by this rank -> (S, lo + nl + hi, M) with the last
-    `lo` planes of rank-1 in front, the first `hi` planes of rank+1 behind (zeros beyond the volume)."""
-    import torch
-
+    `lo` planes of rank-1 in front, the first `hi` planes of rank+1 behind (zeros beyond the volume).
+    The received halos land directly in the padded output (one pxa_copy2d places the slab)."""
     rank, w = world(group)
     S, nl, M = x.shape
     if nl < max(lo, hi) and w > 1:
         raise ValueError(f"slab of {nl} planes is thinner than the halo ({lo}, {hi})")
-    left = torch.zeros((S, lo, M), dtype=x.dtype, device=x.device)
-    right = torch.zeros((S, hi, M), dtype=x.dtype, device=x.device)
-    sends, recvs = [], []
+    x = x if x.is_contiguous() else x.contiguous()
+    P = lo + nl + hi
+    out = _dev_zeros((S, P, M), x)
+    _dev_copy_rows(x, out, S, nl * M, nl * M, P * M, 0, lo * M)
+    sends, recvs, land = [], [], []
     if rank > 0:
         if hi:
-            sends.append((x[:, :hi], rank - 1))
+            sends.append((_planes(x, 0, hi), rank - 1))
         if lo:
+            left = _empty(x, (S, lo, M))
             recvs.append((left, rank - 1))
+            land.append((left, 0, lo))
     if rank < w - 1:
         if lo:
-            sends.append((x[:, nl - lo:], rank + 1))
+            sends.append((_planes(x, nl - lo, nl), rank + 1))
         if hi:
+            right = _empty(x, (S, hi, M))
             recvs.append((right, rank + 1))
+            land.append((right, lo + nl, hi))
     _p2p(sends, recvs, group)
-    if x.is_cuda:
-        from pyxu_amd import xp
-
-        return xp.concatenate([left, x.contiguous(), right], axis=1)
-    return torch.cat([left, x, right], dim=1)  # gloo CPU tests
+    for buf, p0, n in land:
+        _dev_copy_rows(buf, out, S, n * M, n * M, P * M, 0, p0 * M)
+    return out
 
 
 def halo_reduce(xp, lo, hi, group=None):
     """Adjoint of halo_pad: xp (S, lo + nl + hi, M) -> (S, nl, M), the halo planes sent back to the
-    neighbours that own them and added to their edge planes (dropped beyond the volume)."""
-    import torch
-
+    neighbours that own them and added to their edge planes (dropped beyond the volume).  Each
+    received halo is added to all S stack rows by ONE pxa_copy2d accumulate launch."""
     rank, w = world(group)
-    S, pl, M = xp.shape
-    nl = pl - lo - hi
-    out = xp[:, lo:lo + nl].contiguous()
-    from_left = torch.empty((S, hi, M), dtype=xp.dtype, device=xp.device) if (rank > 0 and hi) else None
-    from_right = torch.empty((S, lo, M), dtype=xp.dtype, device=xp.device) if (rank < w - 1 and lo) else None
-    sends, recvs = [], []
+    S, P, M = xp.shape
+    nl = P - lo - hi
+    xp = xp if xp.is_contiguous() else xp.contiguous()
+    out = _planes(xp, lo, lo + nl)
+    sends, recvs, land = [], [], []
     if rank > 0:
         if lo:
-            sends.append((xp[:, :lo], rank - 1))  # my left halo = rank-1's last lo planes
+            sends.append((_planes(xp, 0, lo), rank - 1))  # my left halo = rank-1's last lo planes
         if hi:
+            from_left = _empty(xp, (S, hi, M))
             recvs.append((from_left, rank - 1))  # rank-1's right halo = my first hi planes
+            land.append((from_left, 0, hi))
     if rank < w - 1:
         if hi:
-            sends.append((xp[:, lo + nl:], rank + 1))
+            sends.append((_planes(xp, lo + nl, P), rank + 1))
         if lo:
+            from_right = _empty(xp, (S, lo, M))
             recvs.append((from_right, rank + 1))
+            land.append((from_right, nl - lo, lo))
     _p2p(sends, recvs, group)
-    for s in range(S):  # per stack row: contiguous plane ranges
-        if from_left is not None:
-            _accumulate(out[s, :hi], from_left[s])
-        if from_right is not None:
-            _accumulate(out[s, nl - lo:], from_right[s])
+    for buf, p0, n in land:
+        _dev_copy_rows(buf, out, S, n * M, n * M, nl * M, 0, p0 * M, accumulate=1)
     return out
 
 
@@ -327,17 +362,22 @@ class SlabLinOp(pxa.LinOp):
     def apply(self, arr):
         (lo, hi), nl, M, K = self._halo, self._nl, self._M, self._K
         sh, S = self._stack(arr)
+        P = lo + nl + hi
         xp = halo_pad(arr.reshape(S, nl, M), lo, hi, self._group)
-        y = self._local.apply(xp.reshape(S, -1)).reshape(S, K, lo + nl + hi, M)
-        return y[:, :, lo:lo + nl].contiguous().reshape(*sh, K * nl * M)
+        y = self._local.apply(xp.reshape(S, -1))
+        y = y if y.is_contiguous() else y.contiguous()
+        out = _empty(y, (S * K, nl * M))  # crop: planes [lo, lo + nl) of every (row, block), one launch
+        _dev_copy_rows(y, out, S * K, nl * M, P * M, nl * M, lo * M, 0)
+        return out.reshape(*sh, K * nl * M)
 
     @pxrt.enforce_precision(i="arr")
     def adjoint(self, arr):
-        import torch
-
         (lo, hi), nl, M, K = self._halo, self._nl, self._M, self._K
         sh, S = self._stack(arr)
-        yp = torch.zeros((S, K, lo + nl + hi, M), dtype=arr.dtype, device=arr.device)
-        yp[:, :, lo:lo + nl] = arr.reshape(S, K, nl, M)
-        xp = self._local.adjoint(yp.reshape(S, -1)).reshape(S, lo + nl + hi, M)
+        P = lo + nl + hi
+        a = arr.reshape(S * K, nl * M)
+        a = a if a.is_contiguous() else a.contiguous()
+        yp = _dev_zeros((S * K, P * M), a)  # embed into the zero-padded slab, one launch
+        _dev_copy_rows(a, yp, S * K, nl * M, nl * M, P * M, 0, lo * M)
+        xp = self._local.adjoint(yp.reshape(S, -1)).reshape(S, P, M)
         return halo_reduce(xp, lo, hi, self._group).reshape(*sh, nl * M)

@@ -1,6 +1,7 @@
 """
-Finite-difference operators (mirrors reference operator/linop/diff.py): PartialDerivative,
-Gradient.
+Differential operators (mirrors reference operator/linop/diff.py): PartialDerivative (finite and
+Gaussian-derivative differences), Gradient, Jacobian, Divergence, Hessian, Laplacian and the directional
+family (DirectionalDerivative / Gradient / Laplacian / Hessian).
 
 ``Gradient`` (diff.py:1113-1265) is a vstack of per-direction separable Stencils, output
 direction-major ``(..., D*N)`` (diff.py:923-935, blocks.py:674-679).  When every direction is a
@@ -17,7 +18,8 @@ import pyxu_amd.runtime as pxrt
 from pyxu_amd import _dev
 from pyxu_amd.operator.linop.stencil import Stencil
 
-__all__ = ["PartialDerivative", "Gradient", "Hessian", "Laplacian", "Divergence", "fd_coefficients"]
+__all__ = ["PartialDerivative", "Gradient", "Jacobian", "Hessian", "Laplacian", "Divergence", "DirectionalDerivative",
+           "DirectionalGradient", "DirectionalLaplacian", "DirectionalHessian", "fd_coefficients", "gd_coefficients"]
 
 
 def fd_coefficients(order, scheme, accuracy, sampling, dtype):
@@ -39,6 +41,18 @@ def fd_coefficients(order, scheme, accuracy, sampling, dtype):
     coefs = np.linalg.solve(mat, vec)
     coefs /= sampling**order
     return ids, coefs, ids.index(0)
+
+
+def gd_coefficients(order, sigma, truncate, sampling):
+    """_GaussianDerivative._fill_coefs (diff.py:330-349): the order-`order` derivative of a Gaussian of
+    standard deviation sigma / sampling pixels, truncated at `truncate` deviations, flipped for correlation,
+    divided by sampling**order (float64; cast to the runtime precision by Stencil)."""
+    from pyxu_amd.operator.linop.filter import gaussian_kernel1d
+
+    sigma_pix = sigma / sampling
+    radius = int(truncate * float(sigma_pix) + 0.5)
+    coefs = np.flip(gaussian_kernel1d(sigma_pix, order, radius)) / sampling**order
+    return list(range(-radius, radius + 1)), coefs, radius
 
 
 def _tuple(v, n):
@@ -75,6 +89,31 @@ class PartialDerivative:
         op = Stencil(arg_shape=arg_shape, kernel=kernel, center=center, mode=mode)
         op._name = "PartialDerivative"
         op.meta = dict(sampling=sampling, scheme=scheme, accuracy=accuracy)
+        return op
+
+    @staticmethod
+    def gaussian_derivative(arg_shape, order, sigma=1.0, truncate=3.0, mode="constant", gpu=True, dtype=None,
+                            sampling=1):
+        """Gaussian-derivative partial derivative (diff.py:762-919): EVERY axis is filtered by the
+        derivative of a Gaussian of its order (order 0 = Gaussian smoothing), as one separable Stencil."""
+        arg_shape = tuple(arg_shape)
+        D = len(arg_shape)
+        dtype = pxrt.getPrecision().value if dtype is None else dtype
+        order = tuple(order)
+        assert len(order) == D, "`order` must have one entry per axis of `arg_shape`"
+        assert all(o >= 0 for o in order), "Order must be positive"
+        sigma, truncate, sampling = _tuple(sigma, D), _tuple(truncate, D), _tuple(sampling, D)
+        assert all(v >= 0 for v in sigma), "Sigma must be strictly positive"
+        assert all(v > 0 for v in truncate), "Truncate must be strictly positive"
+        assert all(v > 0 for v in sampling), "Sampling must be strictly positive"
+        kernel, center = [], []
+        for ax in range(D):
+            _, coefs, c = gd_coefficients(order[ax], sigma[ax], truncate[ax], sampling[ax])
+            kernel.append(np.asarray(coefs, dtype=dtype))
+            center.append(c)
+        op = Stencil(arg_shape=arg_shape, kernel=kernel, center=center, mode=mode)
+        op._name = "PartialDerivative"
+        op.meta = dict(sampling=sampling, sigma=sigma, truncate=truncate)
         return op
 
 
@@ -151,11 +190,25 @@ class _DiffStack(pxa.LinOp):
         return "\n".join(f"\nDirection {d} \n" + st.visualize() for d, st in zip(self._directions, self._stencils))
 
 
+def _gd_stencil(arg_shape, order, diff_kwargs, mode, dtype):
+    """PartialDerivative.gaussian_derivative with Gradient / Hessian's `sigma`, `truncate`, `sampling`
+    keywords (diff.py:1148-1157: defaults 1.0, 3.0, 1.0)."""
+    return PartialDerivative.gaussian_derivative(arg_shape=arg_shape, order=tuple(order),
+                                                 sigma=diff_kwargs.get("sigma", 1.0),
+                                                 truncate=diff_kwargs.get("truncate", 3.0), mode=mode, dtype=dtype,
+                                                 sampling=diff_kwargs.get("sampling", 1.0))
+
+
+def _check_method(diff_method):
+    if diff_method not in ("fd", "gd"):
+        raise NotImplementedError(f"diff_method must be 'fd' or 'gd', got {diff_method!r}.")
+
+
 def Gradient(arg_shape, directions=None, diff_method="fd", mode="constant", gpu=True, dtype=None, parallel=False,
              **diff_kwargs):
-    """Gradient operator (diff.py:1113-1265)."""
-    if diff_method != "fd":
-        raise NotImplementedError("pyxu_amd: only diff_method='fd' (finite differences) is on the hot path.")
+    """Gradient operator (diff.py:1113-1265); diff_method "fd" (finite differences) or "gd" (Gaussian
+    derivatives: axis d differentiated, every other axis smoothed)."""
+    _check_method(diff_method)
     arg_shape = tuple(arg_shape)
     D = len(arg_shape)
     directions = tuple(range(D)) if directions is None else tuple(np.atleast_1d(directions).tolist())
@@ -172,13 +225,61 @@ def Gradient(arg_shape, directions=None, diff_method="fd", mode="constant", gpu=
     for d in directions:
         order = [0] * D
         order[d] = 1
-        stencils.append(
-            PartialDerivative.finite_difference(arg_shape=arg_shape, order=tuple(order), scheme=sch, accuracy=acc,
-                                                mode=mode, dtype=dtype, sampling=samp)
-        )
+        if diff_method == "gd":
+            stencils.append(_gd_stencil(arg_shape, order, diff_kwargs, mode, dtype))
+        else:
+            stencils.append(
+                PartialDerivative.finite_difference(arg_shape=arg_shape, order=tuple(order), scheme=sch, accuracy=acc,
+                                                    mode=mode, dtype=dtype, sampling=samp)
+            )
     op = _DiffStack(arg_shape, stencils, directions)
     op._name = "Gradient"
-    op.meta = dict(sampling=samp, scheme=sch, accuracy=acc)
+    op.meta = dict(sampling=samp, scheme=sch, accuracy=acc) if diff_method == "fd" else \
+        dict(sampling=samp, sigma=_tuple(diff_kwargs.get("sigma", 1.0), D), truncate=_tuple(diff_kwargs.get("truncate", 3.0), D))
+    return op
+
+
+class _Jacobian(pxa.LinOp):
+    """block_diag of `n_channels` Gradients (diff.py:1268-1416): (..., C*N) -> (..., C*D*N), channel-major;
+    every channel runs through the one gradient launch as a stack row."""
+
+    def __init__(self, grad, n_channels):
+        N, K, C = grad._N, len(grad._stencils), int(n_channels)
+        super().__init__(shape=(C * K * N, C * N))
+        self._grad, self._C, self._N, self._K = grad, C, N, K
+        self.arg_shape = (K, *grad.arg_shape)
+        self.lipschitz = float(grad.lipschitz)
+
+    @pxrt.enforce_precision(i="arr")
+    def apply(self, arr):
+        x = _dev.require(arr)
+        sh = x.shape[:-1]
+        return self._grad.apply(x.reshape(*sh, self._C, self._N)).reshape(*sh, self._C * self._K * self._N)
+
+    @pxrt.enforce_precision(i="arr")
+    def adjoint(self, arr):
+        z = _dev.require(arr)
+        sh = z.shape[:-1]
+        return self._grad.adjoint(z.reshape(*sh, self._C, self._K * self._N)).reshape(*sh, self._C * self._N)
+
+    def unravel(self, arr):
+        return arr.reshape(*arr.shape[:-1], -1, *self.arg_shape)
+
+    def ravel(self, arr):
+        return arr.reshape(*arr.shape[: -1 - len(self.arg_shape)], -1)
+
+
+def Jacobian(arg_shape, n_channels, directions=None, diff_method="fd", mode="constant", gpu=True, dtype=None,
+             parallel=False, **diff_kwargs):
+    """Jacobian of a multi-channel signal (diff.py:1268-1416): the Gradient of each of the `n_channels`
+    channels, stacked channel-major."""
+    grad = Gradient(arg_shape=arg_shape, directions=directions, diff_method=diff_method, mode=mode, gpu=gpu,
+                    dtype=dtype, parallel=parallel, **diff_kwargs)
+    if n_channels <= 1:
+        grad._name = "Jacobian"
+        return grad
+    op = _Jacobian(grad, n_channels)
+    op._name = "Jacobian"
     return op
 
 
@@ -291,8 +392,7 @@ def Hessian(arg_shape, directions="all", diff_method="fd", mode="constant", gpu=
             **diff_kwargs):
     """Hessian (diff.py:1591-1797): vstack of second-order partial derivatives, upper triangle for "all".
     Diagonal components default to the central scheme, off-diagonal ones to `scheme` (forward)."""
-    if diff_method != "fd":
-        raise NotImplementedError("pyxu_amd: only diff_method='fd' (finite differences) is on the hot path.")
+    _check_method(diff_method)
     arg_shape = tuple(arg_shape)
     D = len(arg_shape)
     axes, order = _hessian_directions(arg_shape, directions)
@@ -304,6 +404,9 @@ def Hessian(arg_shape, directions="all", diff_method="fd", mode="constant", gpu=
         full = [0] * D
         for a in ax:
             full[a] = o
+        if diff_method == "gd":
+            stencils.append(_gd_stencil(arg_shape, full, diff_kwargs, mode, dtype))
+            continue
         scheme = user_scheme if user_scheme is not None else ("central" if o == 2 else "forward")
         stencils.append(_fd_stencil(arg_shape, full, _tuple(scheme, D) if isinstance(scheme, str) else scheme,
                                     _tuple(accuracy, D), mode, dtype, _tuple(sampling, D)))
@@ -329,8 +432,7 @@ def Divergence(arg_shape, directions=None, diff_method="fd", mode="constant", gp
                **diff_kwargs):
     """Divergence (diff.py:1418-1589): Sum(axis=0) o block_diag of per-direction first derivatives,
     with the finite-difference scheme reversed (forward <-> backward; central stays, the default)."""
-    if diff_method != "fd":
-        raise NotImplementedError("pyxu_amd: only diff_method='fd' (finite differences) is on the hot path.")
+    _check_method(diff_method)
     arg_shape = tuple(arg_shape)
     D = len(arg_shape)
     change = {"central": "central", "forward": "backward", "backward": "forward"}
@@ -343,8 +445,162 @@ def Divergence(arg_shape, directions=None, diff_method="fd", mode="constant", gp
     for d in directions:
         order = [0] * D
         order[d] = 1
+        if diff_method == "gd":
+            stencils.append(_gd_stencil(arg_shape, order, diff_kwargs, mode, dtype))
+            continue
         stencils.append(_fd_stencil(arg_shape, order, _tuple(scheme, D) if isinstance(scheme, str) else tuple(scheme),
                                     _tuple(accuracy, D), mode, dtype, _tuple(sampling, D)))
     op = _Divergence(arg_shape, stencils)
     op._name = "Divergence"
     return op
+
+
+# ------------------------------------------------------------------ directional family (diff.py:1938-2759)
+def _unit(direction, xp_dtype):
+    """direction / ||direction||_2 over axis 0, in the direction's dtype (diff.py:2012, 2121, 2268, 2433)."""
+    d = np.asarray(direction)
+    return (d / np.linalg.norm(d, axis=0, keepdims=True)).astype(xp_dtype)
+
+
+def _outer_triu(n1, n2):
+    """Upper-triangular outer product of two unit directions with the off-diagonal terms doubled, in the
+    Hessian's component order (diff.py:2020-2033)."""
+    ndim = n1.shape[0]
+    o = n1[:, None, ...] * n2[None, ...]
+    if ndim == 1:
+        return o.reshape(1, *o.shape[2:])
+    o = o.reshape(ndim**2, *o.shape[2:])
+    dummy = np.arange(ndim**2).reshape(ndim, ndim)
+    o[dummy[np.triu_indices(ndim, k=1)].ravel()] *= 2
+    return o[dummy[np.triu_indices(ndim, k=0)].ravel()]
+
+
+class _Directional(pxa.LinOp):
+    """Sum o DiagonalOp o diff (the directional operators of diff.py:1938-2759) as the derivative stack
+    `diff` (Gradient or Hessian: K components) followed by ONE contraction launch (pxa_dir_contract):
+    output group g = sum_j w[g, j] * diff_{j mod K}.  w: host (G, J) or (G, J, *arg_shape) weights."""
+
+    def __init__(self, diff, w, name):
+        w = np.asarray(w)
+        G, J = w.shape[0], w.shape[1]
+        N, K = diff._N, len(diff._stencils)
+        assert J % K == 0
+        per_pixel = w.ndim > 2
+        super().__init__(shape=(G * N, N))
+        self._diff, self._G, self._J, self._K, self._N = diff, G, J, K, N
+        self.arg_shape = diff.arg_shape
+        self._wp = 1 if per_pixel else 0
+        from pyxu_amd.util import to_device
+
+        self._w_host = np.ascontiguousarray(w.reshape(G, J, N) if per_pixel else w)
+        self._w = to_device(self._w_host.reshape(-1))
+        self._name = name
+        # sqrt(#groups) * max|w| * sqrt(J) * L(diff): the product bound of the reference's chain
+        self.lipschitz = float(np.sqrt(G) * np.max(np.abs(self._w_host)) * np.sqrt(J // K) * float(diff.lipschitz))
+
+    def _weights(self, x):
+        w = self._w
+        return w if w.dtype == x.dtype else _dev.cast(w, x)
+
+    @pxrt.enforce_precision(i="arr")
+    def apply(self, arr):
+        x = _dev.require(arr)
+        sh = x.shape[:-1]
+        S = int(np.prod(sh)) if len(sh) else 1
+        d = self._diff.apply(x.reshape(S, self._N))
+        y = _dev.dir_contract(self._weights(x), self._wp, d, S, self._G, self._J, self._K, self._N)
+        return y.reshape(*sh, self._G * self._N)
+
+    @pxrt.enforce_precision(i="arr")
+    def adjoint(self, arr):
+        z = _dev.require(arr)
+        sh = z.shape[:-1]
+        S = int(np.prod(sh)) if len(sh) else 1
+        t = _dev.dir_contract(self._weights(z), self._wp, z.reshape(S, self._G * self._N), S, self._G, self._J, self._K,
+                              self._N, adjoint=True)
+        return self._diff.adjoint(t.reshape(S, self._K * self._N)).reshape(*sh, self._N)
+
+    def unravel(self, arr):
+        return arr.reshape(*arr.shape[:-1], *self.arg_shape) if self._G == 1 else \
+            arr.reshape(*arr.shape[:-1], self._G, *self.arg_shape)
+
+    def ravel(self, arr):
+        n = len(self.arg_shape) + (0 if self._G == 1 else 1)
+        return arr.reshape(*arr.shape[:-n], -1)
+
+
+def _dir_dtype(d):
+    d = d[0] if isinstance(d, (list, tuple)) else d
+    return np.asarray(d.cpu() if hasattr(d, "cpu") else d).dtype
+
+
+def _host(d):
+    return np.asarray(d.cpu() if hasattr(d, "cpu") else d)
+
+
+def DirectionalDerivative(arg_shape, order, directions, diff_method="fd", mode="constant", parallel=False,
+                          **diff_kwargs):
+    """First / second directional derivative (diff.py:1938-2073): sum_i v_i d_i f, or
+    sum_{i<=j} (2 - delta_ij) v_i u_j d_ij f with unit directions v (and u), constant or per pixel."""
+    arg_shape = tuple(arg_shape)
+    ndim = len(arg_shape)
+    assert order in [1, 2], "`order` should be either 1 or 2"
+    if order == 1:
+        assert not isinstance(directions, (list, tuple)), "`directions` for first directional derivative should be an NDArray"
+        d1 = d2 = _host(directions)
+    else:
+        if isinstance(directions, (list, tuple)):
+            assert len(directions) == 2, "`directions` for second directional derivative should be an NDArray or a tuple/list with two NDArrays of the same shape"
+            d1, d2 = _host(directions[0]), _host(directions[1])
+            assert d1.shape == d2.shape
+        else:
+            d1 = d2 = _host(directions)
+    assert d1.shape[0] == ndim, "The length of `directions` should match `len(arg_shape)`"
+    dt = d1.dtype
+    if order == 1:
+        diff = Gradient(arg_shape=arg_shape, diff_method=diff_method, mode=mode, dtype=dt, **diff_kwargs)
+        w = _unit(d1, dt)
+    else:
+        diff = Hessian(arg_shape=arg_shape, diff_method=diff_method, mode=mode, dtype=dt, **diff_kwargs)
+        w = _outer_triu(_unit(d1, dt), _unit(d2, dt))
+    return _Directional(diff, w[None], "FirstDirectionalDerivative" if order == 1 else "SecondDirectionalDerivative")
+
+
+def DirectionalGradient(arg_shape, directions, diff_method="fd", mode="constant", parallel=False, **diff_kwargs):
+    """Stack of first directional derivatives along each of `directions` (diff.py:2076-2197)."""
+    arg_shape = tuple(arg_shape)
+    assert isinstance(directions, (list, tuple))
+    dt = _dir_dtype(directions)
+    diff = Gradient(arg_shape=arg_shape, diff_method=diff_method, mode=mode, dtype=dt, **diff_kwargs)
+    w = np.stack([_unit(_host(d), dt) for d in directions])
+    return _Directional(diff, w, "DirectionalGradient")
+
+
+def DirectionalLaplacian(arg_shape, directions, weights=None, diff_method="fd", mode="constant", parallel=False,
+                         **diff_kwargs):
+    """Weighted sum of second directional derivatives (diff.py:2200-2364)."""
+    arg_shape = tuple(arg_shape)
+    assert isinstance(directions, (list, tuple))
+    if weights is None:
+        weights = [1.0] * len(directions)
+    elif len(weights) != len(directions):
+        raise ValueError("The number of weights and directions provided differ.")
+    dt = _dir_dtype(directions)
+    diff = Hessian(arg_shape=arg_shape, diff_method=diff_method, mode=mode, dtype=dt, **diff_kwargs)
+    parts = []
+    for wt, d in zip(weights, directions):
+        n = _unit(_host(d), dt)
+        parts.append(wt * _outer_triu(n, n))
+    w = np.concatenate(parts, axis=0)[None]  # one output group, L * K terms (term j reads component j % K)
+    return _Directional(diff, w, "DirectionalLaplacian")
+
+
+def DirectionalHessian(arg_shape, directions, diff_method="gd", mode="constant", parallel=False, **diff_kwargs):
+    """Second directional derivatives along every pair (i <= j) of `directions` (diff.py:2367-2542)."""
+    arg_shape = tuple(arg_shape)
+    assert isinstance(directions, (list, tuple))
+    dt = _dir_dtype(directions)
+    diff = Hessian(arg_shape=arg_shape, diff_method=diff_method, mode=mode, dtype=dt, **diff_kwargs)
+    units = [_unit(_host(d), dt) for d in directions]
+    w = np.stack([_outer_triu(units[i], units[j]) for i in range(len(units)) for j in range(i, len(units))])
+    return _Directional(diff, w, "DirectionalHessian")

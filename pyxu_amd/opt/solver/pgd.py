@@ -21,6 +21,30 @@ class AutoInferenceWarning(UserWarning):
     pass
 
 
+class _Momentum:
+    """The momentum sequence a_k (pgd.py:164-171) with a one-value look-ahead: the fused y-state step
+    writes the next iteration's momentum point, so it needs a_{k+1} while consuming a_k.  `push`
+    returns a consumed value (speculative-step rollback)."""
+
+    def __init__(self, it):
+        self._it = iter(it)
+        self._buf = []
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        return self._buf.pop() if self._buf else next(self._it)
+
+    def peek(self):
+        if not self._buf:
+            self._buf.append(next(self._it))
+        return self._buf[-1]
+
+    def push(self, v):
+        self._buf.append(v)
+
+
 class PGD(pxa.Solver):
     r"""Accelerated proximal gradient descent (Chambolle--Dossal momentum).
 
@@ -63,11 +87,11 @@ class PGD(pxa.Solver):
         if acceleration:
             try:
                 assert d > 2
-                mst["a"] = (pxrt.coerce(k / (k + 1 + d)) for k in itertools.count(start=0))
+                mst["a"] = _Momentum(pxrt.coerce(k / (k + 1 + d)) for k in itertools.count(start=0))
             except Exception:
                 raise ValueError(f"Expected d > 2, got {d}.")
         else:
-            mst["a"] = itertools.repeat(pxrt.coerce(0))
+            mst["a"] = _Momentum(itertools.repeat(pxrt.coerce(0)))
         self._plan = match_pgd_deblur(self._f, self._g, x0) if fused else None
         if self._plan is not None:
             p = self._plan
@@ -77,7 +101,20 @@ class PGD(pxa.Solver):
             p["stack"] = p["rows"] * p["B"]
             p["pre"] = _dev.pgd_tv2d_args(p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"], p["h1"],
                                           p["lam"], p["mu"], p["prox"], p["prox_scale"])
+            # per-tile RelError partials of the launch that precedes a stop check (pxa_tile_partials_fold)
+            ntiles = int(_dev.lib.pxa_pgd_tv2d_partials_count(p["stack"], p["n0"], p["n1"]))
+            p["parts"] = _dev.empty_f64((2 * ntiles,), x0)
+            p["tiles_per_row"] = ntiles // max(p["rows"], 1)
             self._spare = None
+            # the momentum point yk = (x - x_prev) * a + x is carried as state (pxa_pgd_tv2d_step_y): the
+            # solver owns both y buffers (never exposed), None = derive it from (x, x_prev) in the next step
+            self._y = self._y_spare = None
+            # the solver never writes a tensor it has published as x (outputs go to fresh or recycled
+            # buffers nobody else references), so stop criteria may keep references instead of copies
+            mst["__immutable__"] = frozenset({"x"})
+
+    # publish the fused step's per-tile RelError partials to the stop criteria (False: A/B and parity tests)
+    _fused_relerr = True
 
     # speculative stop checks (abc/solver.py _step_speculative): the fused step writes a buffer that is
     # neither x nor x_prev, so undoing it is restoring (x, x_prev) and the momentum value it consumed
@@ -92,8 +129,10 @@ class PGD(pxa.Solver):
     def _spec_rollback(self, token):
         mst = self._mstate
         mst["x"], mst["x_prev"] = token
-        mst["a"] = itertools.chain([self._last_a], mst["a"])
+        mst["a"].push(self._last_a)
+        mst.pop("__relerr__", None)
         self._spare = None
+        self._y = None  # the carried momentum point belonged to the undone step
         self._spec_refs = 0
 
     def m_step(self):
@@ -102,13 +141,26 @@ class PGD(pxa.Solver):
         self._last_a = a
         if self._plan is not None:
             p = self._plan
+            mst.pop("__relerr__", None)  # (holds x_prev: drop it before the buffer-recycling refcount below)
             x, xp = mst["x"], mst["x_prev"]
             out = self._spare
             if out is None or out is x or out is xp:
                 out = _dev.empty_like(x)
+            y_next = self._y_spare if self._y_spare is not None else _dev.empty_like(x)
             tau = mst["tau"]
-            _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
-                               p["h0"], p["h1"], p["lam"], p["mu"], a, tau, p["prox"], tau * p["prox_scale"], pre=p["pre"])
+            # RelError partials only for the launch right before a stop check (the engine advances idx
+            # before m_step: the next check runs at idx when idx % stop_rate == 0)
+            ast = self._astate
+            want = (self._fused_relerr and ast.get("stop_rate") is not None
+                    and ast["idx"] % ast["stop_rate"] == 0)
+            parts = p["parts"] if want else None
+            _dev.pgd_tv2d_step_y(x, xp, self._y, p["hty"], out, y_next, a, mst["a"].peek(), tau, p["prox"],
+                                 tau * p["prox_scale"], p["pre"], partials=parts)
+            self._y_spare, self._y = self._y, y_next
+            if want:  # (var, x_new, the x the statistics are relative to, partials, rows, tiles per row)
+                mst["__relerr__"] = ("x", out, x, parts, p["rows"], p["tiles_per_row"])
+            else:
+                mst.pop("__relerr__", None)
             mst["x_prev"], mst["x"] = x, out
             # recycle the old x_prev as the next output buffer iff nobody else holds it (the reference
             # allocates fresh arrays, so user-held results must never be overwritten)

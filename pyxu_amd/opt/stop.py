@@ -238,14 +238,51 @@ class RelError(pxa.StoppingCriterion):
         self._val = np.r_[0]
         self._x_prev = None
 
+    def _keep(self, state, x):
+        """What the criterion keeps of x for its next check: a reference when the solver promises never
+        to write a tensor it has published under this name (state["__immutable__"]), else a copy."""
+        if hasattr(state, "get") and self._var in state.get("__immutable__", ()):
+            return x
+        return _dev.copy(x)
+
+    def _fused(self, state, x):
+        """The solver step's own statistics for this check, or None: the fused PGD step publishes
+        (var, x_new, x, per-tile partials, rows, tiles per row) when its launch computed
+        sum (x_new - x)^2 and sum x^2 per tile; they are this check's statistics iff x_new is the state
+        x and x is the very tensor this criterion kept at its previous check (stop_rate 1, or any rate
+        whose previous check saw the launch's input)."""
+        h = state.get("__relerr__") if hasattr(state, "get") else None
+        if (h is None or h[0] != self._var or h[1] is not x or self._x_prev is not h[2] or self._f is not _identity
+                or self._norm != 2):
+            return None
+        return h
+
+    def _decide(self, st, shape):
+        num = st[0].reshape(*shape, 1)
+        den = st[1].reshape(*shape, 1)
+        rule = np.all if self._satisfy_all else np.any
+        decision = bool(rule(num <= self._eps * den))
+        with np.errstate(divide="ignore", invalid="ignore"):  # 0/0 -> nan -> 0 below (stop.py:375-379)
+            self._val = num / den
+            self._val[np.isnan(self._val)] = 0
+        return decision
+
     def stop(self, state) -> bool:
         x = state[self._var]
         if isinstance(x, numbers.Real):
             raise NotImplementedError("pyxu_amd: RelError on scalar state variables is not supported.")
         if self._x_prev is None:
-            self._x_prev = _dev.copy(x)
+            self._x_prev = self._keep(state, x)
             self._val = np.zeros(shape=(1,) if (x.ndim == 1) else tuple(x.shape[:-1]))
             return False
+        h = self._fused(state, x)
+        if h is not None:
+            st = _dev.empty_f64((2, max(h[4], 1)), x)
+            _dev.tile_partials_fold(h[3], h[4], h[5], st)
+            if self._reduce is not None:
+                st = self._reduce(st, "sum")
+            self._x_prev = x
+            return self._decide(_finish(st.cpu().numpy(), 2), x.shape[:-1])
         fx_prev = self._f(self._x_prev)
         fx = self._f(x)
         # numerator and denominator row statistics in one device tensor -> one host sync
@@ -254,23 +291,17 @@ class RelError(pxa.StoppingCriterion):
         # the reference copies x after the decision (stop.py:381); the copy is decision-independent, so it
         # is made here, before the host sync.  Identity f and the 2-norm (the default): both statistics
         # and the copy in one pass over x and x_prev (pxa_relerr_stats).
+        borrow = hasattr(state, "get") and self._var in state.get("__immutable__", ())
         if self._f is _identity and self._norm == 2 and 0 < rows <= 65535 and fx.dtype == fx_prev.dtype:
-            x_copy = _dev.relerr_stats(fx, fx_prev, st)
+            x_copy = _dev.relerr_stats(fx, fx_prev, st, copy=not borrow)
         else:
             _rowstat(fx, self._norm, fx_prev, out=st[0])
             _rowstat(fx_prev, self._norm, out=st[1])
-            x_copy = _dev.copy(x)
+            x_copy = None if borrow else _dev.copy(x)
         if self._reduce is not None:
             st = self._reduce(st, "max" if self._norm == np.inf else "sum")
-        st = _finish(st.cpu().numpy(), self._norm)
-        num = st[0].reshape(*fx.shape[:-1], 1)
-        den = st[1].reshape(*fx.shape[:-1], 1)
-        rule = np.all if self._satisfy_all else np.any
-        decision = bool(rule(num <= self._eps * den))
-        with np.errstate(divide="ignore", invalid="ignore"):  # 0/0 -> nan -> 0 below (stop.py:375-379)
-            self._val = num / den
-            self._val[np.isnan(self._val)] = 0
-        self._x_prev = x_copy
+        decision = self._decide(_finish(st.cpu().numpy(), self._norm), fx.shape[:-1])
+        self._x_prev = x if borrow else x_copy
         return decision
 
     # hook: combine a device row statistic across shards (identity on one process)
@@ -296,22 +327,28 @@ class RelError(pxa.StoppingCriterion):
             buf = (torch.empty((2, rows), dtype=torch.float64, pin_memory=True), torch.cuda.Event())
             self._async_buf = buf
         host, ev = buf
-        # the final fold writes the statistics straight into the pinned host buffer (device-mapped):
-        # no device -> host copy launch between the statistics and the event
-        x_copy = _dev.relerr_stats(x, self._x_prev, host)
+        h = self._fused(state, x)
+        if h is not None:
+            # the step's own per-tile partials, folded straight into the pinned host buffer: no pass over
+            # x / x_prev, no copy.  x is kept (a reference) now, so that the solver's next step, enqueued
+            # before the decision is read, may recycle the previous iterate's buffer
+            _dev.tile_partials_fold(h[3], h[4], h[5], host)
+            x_copy = x
+        else:
+            # the final fold writes the statistics straight into the pinned host buffer (device-mapped):
+            # no device -> host copy launch between the statistics and the event
+            borrow = self._var in state.get("__immutable__", ()) if hasattr(state, "get") else False
+            x_copy = _dev.relerr_stats(x, self._x_prev, host, copy=not borrow)
+            if borrow:
+                x_copy = x
         ev.record()
+        if h is not None:
+            self._x_prev = x_copy
         shape = x.shape[:-1]
 
         def resolve():
             _dev.wait_event(ev)
-            fin = _finish(host.numpy().copy(), self._norm)
-            num = fin[0].reshape(*shape, 1)
-            den = fin[1].reshape(*shape, 1)
-            rule = np.all if self._satisfy_all else np.any
-            decision = bool(rule(num <= self._eps * den))
-            with np.errstate(divide="ignore", invalid="ignore"):  # 0/0 -> nan -> 0 (stop.py:375-379)
-                self._val = num / den
-                self._val[np.isnan(self._val)] = 0
+            decision = self._decide(_finish(host.numpy().copy(), self._norm), shape)
             self._x_prev = x_copy
             return decision
 

@@ -190,11 +190,9 @@ def pad(x, pad_width, mode="constant"):
     """numpy.pad over every axis of x (modes of operator/linop/pad.py: constant (0), wrap, reflect,
     symmetric, edge) through pxa_pad."""
     x = _dev.require(x)
-    if np.isscalar(pad_width):
-        pad_width = [(int(pad_width), int(pad_width))] * x.ndim
-    pad_width = [(int(p), int(p)) if np.isscalar(p) else (int(p[0]), int(p[1])) for p in pad_width]
-    if len(pad_width) == 1 and x.ndim > 1:
-        pad_width = pad_width * x.ndim
+    # numpy's pad_width forms: int, (n,), (before, after) for every axis, or ((before, after), ...) per axis
+    pw = np.broadcast_to(np.asarray(pad_width, dtype=np.int64), (x.ndim, 2))
+    pad_width = [(int(a), int(b)) for a, b in pw]
     lo = [p[0] for p in pad_width]
     hi = [p[1] for p in pad_width]
     y = _dev.pad(x, 1, tuple(x.shape), lo, hi, [mode] * x.ndim)

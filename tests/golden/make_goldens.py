@@ -201,6 +201,95 @@ def gen_diffops():
             )
 
 
+DIR_CASES = [
+    # (kind, constructor kwargs); "dirs" entries: list of direction vectors, "varying" broadcasts them per pixel
+    ("jacobian", dict(arg_shape=(9, 11), n_channels=2)),
+    ("jacobian", dict(arg_shape=(5, 6, 7), n_channels=3, directions=(0, 2))),
+    ("gradient_gd", dict(arg_shape=(9, 11), sigma=1.0)),
+    ("gradient_gd", dict(arg_shape=(6, 7, 8), sigma=(0.8, 1.0, 1.2), truncate=2.5, sampling=2.0)),
+    ("hessian_gd", dict(arg_shape=(9, 11), sigma=1.0)),
+    ("hessian_gd", dict(arg_shape=(6, 7, 8), sigma=0.7)),
+    ("laplacian_gd", dict(arg_shape=(9, 11), sigma=1.3)),
+    ("divergence_gd", dict(arg_shape=(9, 11), sigma=1.0)),
+    ("dirderiv", dict(arg_shape=(5,), order=1, dirs=[(1.0,)], varying=False)),
+    ("dirderiv", dict(arg_shape=(7, 9), order=1, dirs=[(0.3, -1.2)], varying=False)),
+    ("dirderiv", dict(arg_shape=(5, 5, 5), order=1, dirs=[(0.1, 2.0, 1.0)], varying=True)),
+    ("dirderiv", dict(arg_shape=(7, 9), order=2, dirs=[(0.3, -1.2)], varying=False)),
+    ("dirderiv", dict(arg_shape=(7, 9), order=2, dirs=[(0.3, -1.2), (1.0, 0.5)], varying=True)),
+    ("dirderiv", dict(arg_shape=(5, 5, 5), order=2, dirs=[(0.1, 2.0, 1.0)], varying=False, diff_method="gd")),
+    ("dirgrad", dict(arg_shape=(5, 5, 5), dirs=[(0.1, 2.0, 1.0), (0.1, 1.0, 2.0), (2.0, 0.1, 1.0), (2.0, 1.0, 0.1)],
+                     varying=False)),
+    ("dirgrad", dict(arg_shape=(7, 9), dirs=[(0.3, -1.2), (1.0, 0.5)], varying=True)),
+    ("dirlap", dict(arg_shape=(7, 9), dirs=[(0.3, -1.2), (1.0, 0.5)], weights=(0.1, 0.7), varying=False)),
+    ("dirlap", dict(arg_shape=(5, 5, 5), dirs=[(0.1, 2.0, 1.0), (2.0, 1.0, 0.1)], weights=(0.1, 0.2), varying=True,
+                    diff_method="gd")),
+    ("dirhess", dict(arg_shape=(7, 9), dirs=[(0.3, -1.2), (1.0, 0.5)], varying=False)),
+    ("dirhess", dict(arg_shape=(5, 5, 5), dirs=[(0.1, 2.0, 1.0), (2.0, 1.0, 0.1)], varying=True, sigma=0.8)),
+]
+
+
+def _dir_arrays(kw, dt):
+    sh = kw["arg_shape"]
+    out = []
+    for d in kw["dirs"]:
+        v = np.array(d, dtype=dt)
+        if kw["varying"]:  # per-pixel directions: the same vector at every pixel, scaled per pixel
+            scale = np.linspace(0.5, 2.0, int(np.prod(sh))).reshape(sh).astype(dt)
+            v = (v.reshape((-1,) + (1,) * len(sh)) * scale[None]).astype(dt)
+        out.append(v)
+    return out
+
+
+def make_dir_op(mod, kind, kw, dt):
+    """The operator of a DIR_CASES entry from module `mod` (the reference pyxu.operator or pyxu_amd.operator)."""
+    kw = dict(kw)
+    sh = kw.pop("arg_shape")
+    gd = {k: kw.pop(k) for k in ("sigma", "truncate", "sampling") if k in kw}
+    if kind == "jacobian":
+        return mod.Jacobian(arg_shape=sh, n_channels=kw["n_channels"], directions=kw.get("directions"))
+    if kind == "gradient_gd":
+        return mod.Gradient(arg_shape=sh, diff_method="gd", **gd)
+    if kind == "hessian_gd":
+        return mod.Hessian(arg_shape=sh, diff_method="gd", **gd)
+    if kind == "laplacian_gd":
+        return mod.Laplacian(arg_shape=sh, diff_method="gd", **gd)
+    if kind == "divergence_gd":
+        return mod.Divergence(arg_shape=sh, diff_method="gd", **gd)
+    dirs = _dir_arrays(dict(kw, arg_shape=sh), dt)
+    method = kw.get("diff_method", "gd" if kind == "dirhess" else "fd")
+    if kind == "dirderiv":
+        d = dirs[0] if len(dirs) == 1 else tuple(dirs)
+        return mod.DirectionalDerivative(arg_shape=sh, order=kw["order"], directions=d, diff_method=method, **gd)
+    if kind == "dirgrad":
+        return mod.DirectionalGradient(arg_shape=sh, directions=dirs, diff_method=method, **gd)
+    if kind == "dirlap":
+        return mod.DirectionalLaplacian(arg_shape=sh, directions=dirs, weights=kw["weights"], diff_method=method, **gd)
+    return mod.DirectionalHessian(arg_shape=sh, directions=dirs, diff_method=method, **gd)
+
+
+def gen_directional():
+    """Jacobian (diff.py:1268), Gaussian-derivative Gradient / Hessian / Laplacian / Divergence
+    (diff_method="gd", diff.py:264-350) and DirectionalDerivative / Gradient / Laplacian / Hessian
+    (diff.py:1938-2759): apply and adjoint on stacked inputs.  A case the reference itself rejects (its
+    3-D second-order finite differences, see gen_diffops) is recorded with `raises`."""
+    import json
+
+    rng = np.random.default_rng(11)
+    for w, width in WIDTHS.items():
+        dt = width.value
+        for ci, (kind, kw) in enumerate(DIR_CASES):
+            rec = dict(kind=kind, kwargs=json.dumps(kw))
+            with pxrt.Precision(width):
+                try:
+                    op = make_dir_op(pxo, kind, kw, dt)
+                    x = rng.standard_normal((2, op.dim)).astype(dt)
+                    z = rng.standard_normal((2, op.codim)).astype(dt)
+                    rec.update(x=x, y=op.apply(x), z=z, adj=op.adjoint(z), shape=np.array(op.shape), raises="")
+                except Exception as e:  # noqa: BLE001
+                    rec.update(raises=f"{type(e).__name__}: {e}")
+            save(f"directional_{w}_c{ci}", **rec)
+
+
 def gen_norms():
     rng = np.random.default_rng(3)
     for w, width in WIDTHS.items():
@@ -541,3 +630,4 @@ if __name__ == "__main__":
     gen_filters()
     gen_aliases()
     gen_padselect()
+    gen_directional()

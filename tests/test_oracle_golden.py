@@ -202,3 +202,18 @@ def test_diffops(name):
         y, a = orc.hessian_apply(g["x"], sh, dirs), orc.hessian_adjoint(g["z"], sh, dirs)
     assert rel_err(y, g["y"]) <= _tol(y)
     assert rel_err(a, g["adj"]) <= _tol(a)
+
+
+@pytest.mark.parametrize("name", golden_names("directional_"))
+def test_directional(name):
+    """Jacobian, Gaussian-derivative Gradient / Hessian / Laplacian / Divergence and the directional
+    family restated on the oracle vs the reference's own outputs (diff.py:264-350, 1268-1416, 1938-2759)."""
+    from _directional import case, oracle_fns
+
+    g = load_golden(name)
+    assert str(g["raises"]) == "", str(g["raises"])
+    kind, kw = case(g)
+    ap, ad = oracle_fns(kind, kw, g["x"].dtype)
+    y, a = ap(g["x"]), ad(g["z"])
+    assert rel_err(y, g["y"]) <= _tol(y), (kind, rel_err(y, g["y"]))
+    assert rel_err(a, g["adj"]) <= _tol(a), (kind, rel_err(a, g["adj"]))
