@@ -169,6 +169,15 @@ int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, co
 int pxa_row_reduce_pow(int dtype, int64_t rows, int64_t n, double p, const void* x, const void* y, double* out,
                        void* work, void* stream);
 
+/* CG iteration tail after A p (opt/solver/cg.py:125-153), for `rows` stacked problems of n entries, in
+ * three launches: alpha = (T)(rr / <p, A p>), x += alpha p, r -= alpha A p, rr' = ||r||^2,
+ * beta = (T)(rr' / rr), p = r + beta p.  rr: this step's ||r||^2 per row (device double); rr_out (device,
+ * != rr) and rr_host (pinned / device-mapped host memory, may be NULL) receive rr'.  All sums in double
+ * with a fixed partition and order.  `work`: pxa_cg_update_workspace_bytes(rows) bytes. */
+size_t pxa_cg_update_workspace_bytes(int64_t rows);
+int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
+                  double* rr_out, double* rr_host, void* work, void* stream);
+
 /* RelError statistics from the fused PGD step's per-tile partials (pxa_pgd_tv2d_step[_y] with
  * `partials`): out[0 * rows + r] = sum (x_new - x)^2 and out[1 * rows + r] = sum x^2 over the per_row
  * consecutive tiles of stack row r, fixed summation order.  At stop_rate 1 the criterion's stored x_prev
@@ -373,9 +382,7 @@ int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int6
  * alias x or x_prev.  If `partials` is not NULL, each workgroup writes (sum (x_new-x)^2, sum x^2)
  * for RelError into partials[2*blk..] (double) — pxa_pgd_tv2d_partials_count() gives the number of
  * workgroups.  prox codes: 0 none, 1 positive orthant, 2 l1 with weight prox_w.
- * pxa_pgd_tv2d_last_kernel() names the mode of the calling thread's last successful launch:
- * 1 classic (x, x_prev -> x_new), 2 seed (x, x_prev -> x_new, y_next), 3 y-state (y, x -> x_new,
- * y_next); 0 before any.
+ * pxa_pgd_tv2d_last_kernel() is 1 once the calling thread has launched the tile kernel (0 before).
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
 int pxa_pgd_tv2d_last_kernel(void);
@@ -386,19 +393,7 @@ int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, in
                       const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
                       const void* x_prev, const void* hty, void* x_new, double* partials, void* stream);
-/* The same step with the momentum point carried as solver state (replaces the same reference lines,
- * pgd.py:173-191; the arithmetic is pxa_pgd_tv2d_step's, bit for bit):
- *   y == NULL (seed):  yk from (x, x_prev, a) as above;
- *   y != NULL:         yk = y (x_prev is ignored and may be NULL);
- * and besides x_new the epilogue writes y_next = (x_new - x) * a_next + x_new, i.e. the next
- * iteration's yk with its momentum a_next (the same fma the window load would evaluate).  Every stencil
- * of the step reads yk over a 2R halo, x only at the tile pixels: the steady-state launch reads one
- * haloed array instead of two.  y_next must not alias x, x_prev, y or x_new. */
-int pxa_pgd_tv2d_step_y(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0,
-                        const int32_t* off0, const double* coef0, int nt1, const int32_t* off1, const double* coef1,
-                        double h0, double h1, double lam, double mu, double a, double a_next, double tau, int prox,
-                        double prox_w, const void* x, const void* x_prev, const void* y, const void* hty, void* x_new,
-                        void* y_next, double* partials, void* stream);
+
 
 /* ---------------------------------------------------------------------------------------------
  * FFT LinOp (operator/linop/fft/fft.py:257-379).  `stack` arrays of complex values (interleaved

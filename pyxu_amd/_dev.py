@@ -508,6 +508,15 @@ def relerr_stats(x, x_prev, out, copy=True):
     return xc
 
 
+def cg_update(x, r, p, ap, rr, rr_out, rr_host, work):
+    """pxa_cg_update: the CG iteration tail after A p on (rows, n) x / r / p / A p (in place), from this
+    step's ||r||^2 `rr` (device float64 (rows,)); ||r'||^2 lands in rr_out (device) and rr_host (pinned)."""
+    rows, n = x.shape
+    check(lib.pxa_cg_update(dtcode(x), rows, n, ptr(x), ptr(r), ptr(p), ptr(ap), rr.data_ptr(), rr_out.data_ptr(),
+                            rr_host.data_ptr() if rr_host is not None else None, work.data_ptr(), stream()),
+          "pxa_cg_update")
+
+
 def tile_partials_fold(parts, rows, per_row, out):
     """RelError statistics from the fused PGD step's per-tile partials (pxa_tile_partials_fold):
     out (contiguous float64 (2, rows), device or pinned host) = per-row sum (x_new - x)^2, sum x^2."""
@@ -764,24 +773,6 @@ def pgd_tv2d_step(x, x_prev, hty, x_new, stack, y_images, n0, n1, taps0, taps1, 
             stream(),
         ),
         "pxa_pgd_tv2d_step",
-    )
-    if ev is not None:
-        _TIMER.end(ev)
-    return x_new
-
-
-def pgd_tv2d_step_y(x, x_prev, y, hty, x_new, y_next, a, a_next, tau, prox, prox_w, pre, partials=None):
-    """One fused PGD iteration with the momentum point carried as state (pxa_pgd_tv2d_step_y): with
-    y = None the window is formed from (x, x_prev, a) (seed), else it is y; writes x_new and
-    y_next = (x_new - x) * a_next + x_new.  `pre`: pgd_tv2d_args(...)."""
-    ev = _TIMER.begin() if _TIMER is not None else None  # measurement hook (bench.py), normally None
-    check(
-        lib.pxa_pgd_tv2d_step_y(
-            dtcode(x), *pre, float(a), float(a_next), float(tau), int(prox), float(prox_w), x.data_ptr(),
-            x_prev.data_ptr() if y is None else None, y.data_ptr() if y is not None else None, hty.data_ptr(),
-            x_new.data_ptr(), y_next.data_ptr(), ptr(partials) if partials is not None else None, stream(),
-        ),
-        "pxa_pgd_tv2d_step_y",
     )
     if ev is not None:
         _TIMER.end(ev)

@@ -48,6 +48,8 @@ EXPORTS = {
     "pxa_relerr_stats_workspace_bytes": (sz, [i64, i64]),
     "pxa_relerr_stats": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp]),
     "pxa_tile_partials_fold": (i32, [i64, i64, vp, vp, vp]),
+    "pxa_cg_update_workspace_bytes": (sz, [i64]),
+    "pxa_cg_update": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "pxa_stencil_axis": (i32, [i32, i64, i32, P_i64, i32, i32, P_i32, P_f64, i32, vp, i64, vp, i64, f64, vp]),
     "pxa_stencil_sep_workspace_bytes": (sz, [i32, i64, i32, P_i64, P_int]),
     "pxa_stencil_sep": (i32, [i32, i64, i32, P_i64, P_int, P_i32, P_f64, vp, i64, vp, i64, f64, vp, vp]),
@@ -80,11 +82,6 @@ EXPORTS = {
         i32,
         [i32, i64, i64, i64, i64, i32, P_i32, P_f64, i32, P_i32, P_f64, f64, f64, f64, f64, f64, f64, i32, f64,
          vp, vp, vp, vp, vp, vp],
-    ),
-    "pxa_pgd_tv2d_step_y": (
-        i32,
-        [i32, i64, i64, i64, i64, i32, P_i32, P_f64, i32, P_i32, P_f64, f64, f64, f64, f64, f64, f64, f64, i32, f64,
-         vp, vp, vp, vp, vp, vp, vp, vp],
     ),
     "pxa_fft": (i32, [i32, i32, P_i64, i32, P_int, i64, i32, vp, vp, vp]),
     "pxa_fft_workspace_bytes": (sz, [i32, i32, P_i64, i32, P_int, i64]),

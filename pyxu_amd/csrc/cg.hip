@@ -1,0 +1,131 @@
+// CG iteration tail (opt/solver/cg.py:125-153) after A p, in three launches instead of the row-op chain
+// (<p, A p> partial + fold, alpha, x update, r update, ||r'||^2 partial + fold, beta, p update, D2H copy):
+//   cg_dot    per-block partials of <p, A p> (double)
+//   cg_xr     every block folds the <p, A p> partials in the same fixed order, alpha = (T)(rr / pAp) (the
+//             float64 division then the cast of the host / row_ratio path), x += alpha p, r -= alpha A p,
+//             per-block partials of ||r'||^2
+//   cg_p      every block folds the ||r'||^2 partials, beta = (T)(rr' / rr), p = r + beta p; block 0 stores
+//             rr' for the next step (device) and into pinned host memory (the stop check's value)
+// One row of the stacked problem per grid.y.  All sums in double with a fixed partition and order, so the
+// results are deterministic run to run.  HBM-bound streaming (p, A p read twice; x, r, p written once).
+#include "common.hpp"
+
+namespace pxa {
+namespace {
+
+constexpr int kCgBlocks = 64;  // partial-sum blocks per row
+
+__device__ inline double block_sum(double v, double* sh) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0) {
+    r = sh[0];
+    for (int k = 1; k < kBlock / 64; ++k) r += sh[k];
+  }
+  return r;  // valid in thread 0
+}
+
+// fixed-order fold of the nb partials of row `row` (every thread gets the same bits)
+__device__ inline double fold(const double* __restrict__ part, int64_t row, int nb) {
+  double s = 0.0;
+  for (int k = 0; k < nb; ++k) s += part[row * nb + k];
+  return s;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) cg_dot_kernel(int64_t n, const T* __restrict__ p, const T* __restrict__ ap,
+                                                        double* __restrict__ part) {
+  __shared__ double sh[kBlock / 64];
+  const int64_t row = blockIdx.y;
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  const T* pr = p + row * n;
+  const T* ar = ap + row * n;
+  double acc = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += (double)pr[i] * (double)ar[i];
+  const double s = block_sum(acc, sh);
+  if (threadIdx.x == 0) part[row * gridDim.x + blockIdx.x] = s;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) cg_xr_kernel(int64_t n, const double* __restrict__ rr,
+                                                       const double* __restrict__ part_pap, const T* __restrict__ p,
+                                                       const T* __restrict__ ap, T* __restrict__ x, T* __restrict__ r,
+                                                       double* __restrict__ part_rr) {
+  __shared__ double sh[kBlock / 64];
+  const int64_t row = blockIdx.y;
+  const T alpha = (T)(rr[row] / fold(part_pap, row, gridDim.x));
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  const T* pr = p + row * n;
+  const T* ar = ap + row * n;
+  T* xr = x + row * n;
+  T* rw = r + row * n;
+  double acc = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    xr[i] = fma(alpha, pr[i], xr[i]);            // x += alpha p
+    const T rn = fma(-alpha, ar[i], rw[i]);      // r -= alpha A p
+    rw[i] = rn;
+    acc += (double)rn * (double)rn;
+  }
+  const double s = block_sum(acc, sh);
+  if (threadIdx.x == 0) part_rr[row * gridDim.x + blockIdx.x] = s;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) cg_p_kernel(int64_t n, const double* __restrict__ rr,
+                                                      const double* __restrict__ part_rr, const T* __restrict__ r,
+                                                      T* __restrict__ p, double* __restrict__ rr_out,
+                                                      double* __restrict__ rr_host) {
+  const int64_t row = blockIdx.y;
+  const double rn = fold(part_rr, row, gridDim.x);
+  const T beta = (T)(rn / rr[row]);
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  const T* rw = r + row * n;
+  T* pw = p + row * n;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) pw[i] = fma(beta, pw[i], rw[i]);  // p = r + beta p
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rr_out[row] = rn;
+    if (rr_host) rr_host[row] = rn;
+  }
+}
+
+}  // namespace
+}  // namespace pxa
+
+using namespace pxa;
+
+extern "C" {
+
+size_t pxa_cg_update_workspace_bytes(int64_t rows) { return rows > 0 ? (size_t)rows * 2 * kCgBlocks * sizeof(double) : 0; }
+
+int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
+                  double* rr_out, double* rr_host, void* work, void* stream) {
+  PXA_CHECK_ARG(rows >= 1 && rows <= 65535 && n >= 1);
+  PXA_CHECK_ARG(x && r && p && ap && rr && rr_out && work && rr_out != rr);
+  hipStream_t st = as_stream(stream);
+  const int nb = (int)(n < (int64_t)kCgBlocks * kBlock ? (n + kBlock - 1) / kBlock : kCgBlocks);
+  double* part_pap = (double*)work;
+  double* part_rr = part_pap + rows * kCgBlocks;
+  const dim3 grid((unsigned)nb, (unsigned)rows);
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((cg_dot_kernel<T>), grid, dim3(kBlock), 0, st, n, (const T*)p, (const T*)ap, part_pap);
+    int e = last_launch_status();
+    if (e) return e;
+    hipLaunchKernelGGL((cg_xr_kernel<T>), grid, dim3(kBlock), 0, st, n, rr, part_pap, (const T*)p, (const T*)ap,
+                       (T*)x, (T*)r, part_rr);
+    e = last_launch_status();
+    if (e) return e;
+    hipLaunchKernelGGL((cg_p_kernel<T>), grid, dim3(kBlock), 0, st, n, rr, part_rr, (const T*)r, (T*)p, rr_out,
+                       rr_host);
+    return last_launch_status();
+  });
+}
+
+}  // extern "C"

@@ -50,7 +50,6 @@ struct PgdParams {
   T g0[kMaxG], g1[kMaxG];                  // interior G taps, d = -2R..2R (index d + 2R)
   T g0a, g0b, g1a, g1b;                    // forward-difference taps per axis (-1/h, 1/h)
   T lam, mu, inv_mu, a, tau, pw;
-  T a_next;  // momentum of the NEXT iteration (modes 1, 2: y_next = (x_new - x) * a_next + x_new)
   int prox;  // 0 none, 1 positive orthant, 2 l1 (uniform branch)
   bool tv;   // lam != 0 (uniform branch)
   bool vec_ok;
@@ -59,15 +58,10 @@ struct PgdParams {
   unsigned round1;  // workgroups resident at once (4 per CU)
 };
 
-// Kernel modes (template parameter MODE).  The momentum point yk = (x - x_prev) * a + x is what every
-// stencil of the step reads (over the tile plus a 2R halo); x itself is only needed at the tile's own
-// pixels.  Mode 2 therefore carries yk as solver state: the epilogue that writes x_new also writes the
-// next iteration's y_next = (x_new - x) * a_next + x_new (the same fma, the same bits), and the next
-// launch reads ONE haloed window (y) instead of two (x, x_prev).
-//   0 classic:  window from (x, x_prev, a)                 -> x_new
-//   1 seed:     window from (x, x_prev, a)                 -> x_new, y_next      (first step of a run)
-//   2 y-state:  window from y; x at the tile pixels only   -> x_new, y_next      (steady state)
-enum : int { kModeClassic = 0, kModeSeed = 1, kModeY = 2 };
+// Round 3 also measured a variant that carried yk as solver state (the epilogue writing the next
+// iteration's yk, the window reading one array instead of two): equal at 2048^2 (25.4 vs 24.9 us) and
+// slower at 4096^2 (79.6 vs 66.2 us), where the fifth compulsory stream costs more than the halved window
+// saves; it was removed.
 
 // Timing trace (PXA_TUNE_PGD_DIAG bit 5, read by pxa_pgd_tile_trace): s_memtime stamps of waves 0-3 of
 // workgroups 0, 1, grid/2 and grid-1, 8 points of their tile.  Staged in LDS beyond the kernel's own
@@ -91,20 +85,18 @@ __device__ inline float tv_weight<float>(float n2, float lam, float mu, float in
   return lam * (r < inv_mu ? r : inv_mu);
 }
 
-// ---- phase 0 of the tile kernel: the yk window A, zero outside the image.  Modes 0 / 1 form
-// yk = (x - x_prev) * a + x from two loads per vector; mode 2 copies the carried y.  All K0 vectors of a
-// thread are loaded before the first LDS store, so their latencies overlap.
-template <typename T, int R, bool EDGE, int MODE>
+// ---- phase 0 of the tile kernel: yk = (x - x_prev) * a + x on the A window, zero outside the image.
+// All K0 vector pairs of a thread are loaded before the first LDS store, so their latencies overlap.
+template <typename T, int R, bool EDGE>
 __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0, const T* __restrict__ xs,
                                    const T* __restrict__ xps) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
-  constexpr bool TWO = MODE != kModeY;  // two source arrays (x, x_prev) or one (y, passed as xs)
   const int n0 = p.n0, n1 = p.n1;
   const int tid = threadIdx.x;
   constexpr int K0 = cdiv(L::N0, kThreads);
-  T xv[K0][V], pv[TWO ? K0 : 1][V];
+  T xv[K0][V], pv[K0][V];
 #pragma unroll
   for (int k = 0; k < K0; ++k) {
     const int it = tid + k * kThreads;
@@ -114,16 +106,16 @@ __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0
       if (!EDGE) {
         const unsigned off = (unsigned)(gr * n1 + gc);
         ld_vec<T, V>(xs + off, xv[k]);
-        if constexpr (TWO) ld_vec<T, V>(xps + off, pv[k]);
+        ld_vec<T, V>(xps + off, pv[k]);
       } else if (gr >= 0 && gr < n0 && p.vec_ok && gc >= 0 && gc + V <= n1) {
         ld_vec<T, V>(xs + (int64_t)gr * n1 + gc, xv[k]);
-        if constexpr (TWO) ld_vec<T, V>(xps + (int64_t)gr * n1 + gc, pv[k]);
+        ld_vec<T, V>(xps + (int64_t)gr * n1 + gc, pv[k]);
       } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           const bool in = gr >= 0 && gr < n0 && gc + v >= 0 && gc + v < n1;
           xv[k][v] = in ? xs[(int64_t)gr * n1 + gc + v] : T(0);
-          if constexpr (TWO) pv[k][v] = in ? xps[(int64_t)gr * n1 + gc + v] : T(0);
+          pv[k][v] = in ? xps[(int64_t)gr * n1 + gc + v] : T(0);
         }
       }
     }
@@ -133,17 +125,10 @@ __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0
     const int it = tid + k * kThreads;
     if (it < L::N0) {
       const int r = it / L::NGA, g = it - r * L::NGA;
-      if constexpr (TWO) {
-        T out[V];
+      T out[V];
 #pragma unroll
-        for (int v = 0; v < V; ++v) out[v] = fma(xv[k][v] - pv[k][v], p.a, xv[k][v]);  // one rounding site
-        st_vec<T, V>(A + r * L::AP + V * g, out);
-      } else {
-        T out[V];
-#pragma unroll
-        for (int v = 0; v < V; ++v) out[v] = xv[k][v];
-        st_vec<T, V>(A + r * L::AP + V * g, out);
-      }
+      for (int v = 0; v < V; ++v) out[v] = fma(xv[k][v] - pv[k][v], p.a, xv[k][v]);  // one rounding site
+      st_vec<T, V>(A + r * L::AP + V * g, out);
     }
   }
 }
@@ -284,17 +269,23 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
 
 // ---- staged epilogue: every thread parks g = G yk + Grad^T q of its pass-B pixels in O (the PT
 // region, free once all G1 sweeps are done), then the workgroup finishes the tile in row-major order:
-// each 16-B vector of a row is one lane (16 lanes per fp32 row), so the H^T y / x loads and the
-// x_new / y_next stores are full 128-B lines instead of the pass-B item order's 64-B row pieces
-// (measured on MI355X: a 2048^2 fp32 store in the item order 7.2 us, row-major 5.2 us).  yk comes from A.
-// StagedB: H^T y (and x, when the mode or the RelError partials need it) of this thread's epilogue
-// vectors, zero outside the image; issued before the O staging so that the latency overlaps it.
+// each 16-B vector of a row is one lane (16 lanes per fp32 row), so the H^T y / x loads and the x_new
+// stores are full 128-B lines instead of the pass-B item order's 64-B row pieces (measured on MI355X: a
+// 2048^2 fp32 store in the item order 7.2 us, row-major 5.2 us).  yk comes from A.
+// StagedB: H^T y (and x, when the RelError partials need it) of this thread's epilogue vectors, zero
+// outside the image; H^T y is issued before the O staging so that its latency overlaps it.
 template <typename T, int R>
 struct StagedB {
   static constexpr int NS = TY / Stage<T, R>::RPS;
   T v[NS][kVecN<T>];
   T x[NS][kVecN<T>];
 };
+
+// a whole 16-B vector of row gr at column gc lies inside the image and can be moved as one access
+template <typename T>
+__device__ inline bool vec_inside(const PgdParams<T>& p, int gr, int gc) {
+  return p.vec_ok && gr < p.n0 && gc + kVecN<T> <= p.n1;
+}
 
 template <typename T, int R, bool EDGE>
 __device__ inline void load_staged(const PgdParams<T>& p, int ty0, int tx0, const T* __restrict__ src, T (&v)[StagedB<T, R>::NS][kVecN<T>]) {
@@ -308,6 +299,8 @@ __device__ inline void load_staged(const PgdParams<T>& p, int ty0, int tx0, cons
     const int gr = ty0 + r0 + s * S::RPS, gc = tx0 + V * cq;
     if (!EDGE) {
       ld_vec<T, V>(src + (unsigned)(gr * n1 + gc), v[s]);
+    } else if (vec_inside(p, gr, gc)) {  // edge tile, but this vector is inside: one 16-B load
+      ld_vec<T, V>(src + (int64_t)gr * n1 + gc, v[s]);
     } else {
 #pragma unroll
       for (int w = 0; w < V; ++w) v[s][w] = (gr < n0 && gc + w < n1) ? src[(int64_t)gr * n1 + gc + w] : T(0);
@@ -315,26 +308,24 @@ __device__ inline void load_staged(const PgdParams<T>& p, int ty0, int tx0, cons
   }
 }
 
-// z = ((G yk + Grad^T q) - H^T y) * (-tau) + yk; x_new = prox(z); y_next = (x_new - x) * a_next + x_new;
-// RelError partials sum (x_new - x)^2, sum x^2 in double.  One 16-B vector of one tile row.
-template <typename T, bool EDGE, bool OUTY>
+// z = ((G yk + Grad^T q) - H^T y) * (-tau) + yk; x_new = prox(z); RelError partials sum (x_new - x)^2,
+// sum x^2 in double.  One 16-B vector of one tile row.
+template <typename T, bool EDGE>
 __device__ inline void finish_vec(const PgdParams<T>& p, int gr, int gc, const T (&g)[kVecN<T>], const T (&bv)[kVecN<T>],
                                   const T (&yc)[kVecN<T>], const T (&xv)[kVecN<T>], T* __restrict__ xns,
-                                  T* __restrict__ yns, bool want_part, double& part_d, double& part_x) {
+                                  bool want_part, double& part_d, double& part_x) {
   constexpr int V = kVecN<T>;
   const int n0 = p.n0, n1 = p.n1;
-  T xo[V], yo[V];
+  T xo[V];
 #pragma unroll
   for (int w = 0; w < V; ++w) {
     const T gsum = g[w] - bv[w];  // (G yk + Grad^T q) - H^T y
     const T z = fma(gsum, -p.tau, yc[w]);
     xo[w] = apply_prox<T>(p.prox, z, p.pw);
-    if constexpr (OUTY) yo[w] = fma(xo[w] - xv[w], p.a_next, xo[w]);  // the next launch's yk, same fma
   }
-  if (!EDGE) {
-    const unsigned off = (unsigned)(gr * n1 + gc);
-    st_vec<T, V>(xns + off, xo);
-    if constexpr (OUTY) st_vec<T, V>(yns + off, yo);
+  const bool whole = !EDGE || vec_inside(p, gr, gc);
+  if (whole) {
+    st_vec<T, V>(xns + (EDGE ? (int64_t)gr * n1 + gc : (int64_t)(unsigned)(gr * n1 + gc)), xo);
     if (want_part) {
 #pragma unroll
       for (int w = 0; w < V; ++w) {
@@ -348,7 +339,6 @@ __device__ inline void finish_vec(const PgdParams<T>& p, int gr, int gc, const T
     for (int w = 0; w < V; ++w) {
       if (gc + w < n1) {
         xns[(int64_t)gr * n1 + gc + w] = xo[w];
-        if constexpr (OUTY) yns[(int64_t)gr * n1 + gc + w] = yo[w];
         if (want_part) {
           const double dd = (double)xo[w] - (double)xv[w];
           part_d += dd * dd;
@@ -389,16 +379,15 @@ __device__ inline void fold_partials(double part_d, double part_x, double* red, 
 
 // One output tile: phase 0 (window), pass A, [ghost columns], pass B (parked in registers), the H^T y / x
 // loads, O staging, row-major epilogue, [RelError partials].
-template <typename T, int R, bool EDGE, int MODE>
+template <typename T, int R, bool EDGE>
 __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
-                                const T* __restrict__ xs, const T* __restrict__ ws, const T* __restrict__ bs,
-                                T* __restrict__ xns, T* __restrict__ yns, double* __restrict__ partials) {
+                                const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
+                                T* __restrict__ xns, double* __restrict__ partials) {
   using L = Layout<T, R>;
   using S = Stage<T, R>;
   constexpr int CW = L::CW;
   constexpr int V = L::V;
   constexpr int KB = cdiv(L::NPB, kThreads);
-  constexpr bool OUTY = MODE != kModeClassic;
   T* A = reinterpret_cast<T*>(smem);
   T* PT = A + L::AR * L::AP;
   T* KT = PT + L::AC * L::PTP;  // H taps for runtime-indexed reads (boundary corrections)
@@ -412,16 +401,13 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   }
   double part_d = 0.0, part_x = 0.0;
   const bool want_part = partials != nullptr;
-  const bool need_x = OUTY || want_part;
   const bool tracing = (p.diag & 32) != 0;
   unsigned long long* ts = reinterpret_cast<unsigned long long*>(smem + kGhOff<T, R> + kGhBytes<T, R>);
   auto tmark = [&](int pt) {
     if (tracing && (tid & 63) == 0) ts[(tid >> 6) * 8 + pt] = clock64();
   };
   tmark(0);
-  // window source: (x, x_prev) in modes 0 / 1, the carried y in mode 2 (ws = x_prev or y)
-  if constexpr (MODE == kModeY) load_window<T, R, EDGE, MODE>(p, A, ty0, tx0, ws, nullptr);
-  else load_window<T, R, EDGE, MODE>(p, A, ty0, tx0, xs, ws);
+  load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
   tmark(1);
   __syncthreads();
   tmark(2);
@@ -462,9 +448,8 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       }
     }
   }
-  // x is loaded only now, once pass B's parked results are out of the registers (holding it across the
-  // O staging as well costs the y-state launch 96 B/lane of scratch at 128 VGPRs)
-  if (need_x) load_staged<T, R, EDGE>(p, ty0, tx0, xs, hb.x);
+  // x (RelError partials only) is loaded once pass B's parked results are out of the registers
+  if (want_part) load_staged<T, R, EDGE>(p, ty0, tx0, xs, hb.x);
   __syncthreads();
   tmark(6);
   {
@@ -476,7 +461,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
       T g[V], y[V];
       ld_vec<T, V>(O + S::idx(r, V * cq), g);
       ld_vec<T, V>(A + (r + 2 * R) * L::AP + L::CA + V * cq, y);
-      finish_vec<T, EDGE, OUTY>(p, ty0 + r, tx0 + V * cq, g, hb.v[s], y, hb.x[s], xns, yns, want_part, part_d, part_x);
+      finish_vec<T, EDGE>(p, ty0 + r, tx0 + V * cq, g, hb.v[s], y, hb.x[s], xns, want_part, part_d, part_x);
     }
   }
   tmark(7);
@@ -489,12 +474,10 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   }
 }
 
-// xs: x; ws: x_prev (modes 0, 1) or the carried y (mode 2); yn: y_next (modes 1, 2)
-template <typename T, int R, int MODE>
+template <typename T, int R>
 __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
-                                                            const T* __restrict__ w, const T* __restrict__ b,
-                                                            T* __restrict__ xn, T* __restrict__ yn,
-                                                            double* __restrict__ partials) {
+                                                            const T* __restrict__ xp, const T* __restrict__ b,
+                                                            T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   if (p.stagger && blockIdx.x < p.round1) {
@@ -519,58 +502,47 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
   const int ty0 = (int)trow * TY, tx0 = (int)(tr - trow * (unsigned)p.tiles1) * TX;
   const int64_t img = (int64_t)p.n0 * p.n1;
   const T* xs = x + (int64_t)s * img;
-  const T* ws = w + (int64_t)s * img;
+  const T* xps = xp + (int64_t)s * img;
   const T* bs = b + (int64_t)(s % (unsigned)p.y_images) * img;
   T* xns = xn + (int64_t)s * img;
-  T* yns = MODE != kModeClassic ? yn + (int64_t)s * img : nullptr;
   // interior: the whole A window lies inside the image (so no boundary rows / columns of G either),
   // rows are 16-B aligned and 32-bit offsets suffice -> no bounds tests
   const bool interior = p.vec_ok && img <= 0x7fffffff && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0 &&
                         tx0 - L::CA >= 0 && tx0 + TX + L::CA <= p.n1;
   if (interior)
-    pgd_tile<T, R, false, MODE>(p, smem_raw, tile, ty0, tx0, xs, ws, bs, xns, yns, partials);
+    pgd_tile<T, R, false>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
   else
-    pgd_tile<T, R, true, MODE>(p, smem_raw, tile, ty0, tx0, xs, ws, bs, xns, yns, partials);
+    pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
 }
 
-template <typename T, int R, int MODE>
-int launch_pgd_m(const PgdParams<T>& p, const void* x, const void* w, const void* b, void* xn, void* yn,
-                 double* partials, hipStream_t s) {
+template <typename T, int R>
+int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
+               hipStream_t s) {
   // Layout + the ghost terms (+ the timing trace under PXA_TUNE_PGD_DIAG bit 5)
   const size_t smem = kGhOff<T, R> + kGhBytes<T, R> + ((p.diag & 32) ? 256 : 0);
-  auto kern = pgd_tv2d_kernel<T, R, MODE>;
+  auto kern = pgd_tv2d_kernel<T, R>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(kGhOff<T, R> + kGhBytes<T, R> + 256));
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)w, (const T*)b,
-                     (T*)xn, (T*)yn, partials);
+  hipLaunchKernelGGL(kern, dim3(p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp, (const T*)b,
+                     (T*)xn, partials);
   return last_launch_status();
 }
 
-template <typename T, int R>
-int launch_pgd(int mode, const PgdParams<T>& p, const void* x, const void* w, const void* b, void* xn, void* yn,
-               double* partials, hipStream_t s) {
-  if (mode == kModeY) return launch_pgd_m<T, R, kModeY>(p, x, w, b, xn, yn, partials, s);
-  if (mode == kModeSeed) return launch_pgd_m<T, R, kModeSeed>(p, x, w, b, xn, yn, partials, s);
-  return launch_pgd_m<T, R, kModeClassic>(p, x, w, b, xn, yn, partials, s);
-}
-
-thread_local int g_last_pgd_kernel = 0;  // pxa_pgd_tv2d_last_kernel: 1 + mode of the last launch
+thread_local int g_last_pgd_kernel = 0;  // pxa_pgd_tv2d_last_kernel
 
 template <typename T>
-int pgd_entry(int mode, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
+int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
               const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1, double lam,
-              double mu, double a, double a_next, double tau, int prox, double prox_w, const void* x, const void* w,
-              const void* hty, void* x_new, void* y_next, double* partials, hipStream_t s) {
-  PXA_CHECK_ARG(mode >= kModeClassic && mode <= kModeY);
+              double mu, double a, double tau, int prox, double prox_w, const void* x, const void* x_prev,
+              const void* hty, void* x_new, double* partials, hipStream_t s) {
   PXA_CHECK_ARG(stack >= 1 && n0 >= 1 && n1 >= 1 && y_images >= 1 && stack % y_images == 0);
   PXA_CHECK_ARG(n0 <= 0x7fffffff && n1 <= 0x7fffffff);
-  PXA_CHECK_ARG(x && w && hty && x_new);
-  PXA_CHECK_ARG(x_new != x && x_new != w);
-  PXA_CHECK_ARG(mode == kModeClassic || (y_next && y_next != x && y_next != w && y_next != x_new));
+  PXA_CHECK_ARG(x && x_prev && hty && x_new);
+  PXA_CHECK_ARG(x_new != x && x_new != x_prev);
   PXA_CHECK_ARG(prox >= 0 && prox <= 2);
   PXA_CHECK_ARG(nt0 >= 1 && nt1 >= 1 && off0 && off1 && coef0 && coef1);
   int R = 1;  // TV needs a 1-pixel halo even for a 1-tap blur
@@ -614,12 +586,10 @@ int pgd_entry(int mode, int64_t stack, int64_t y_images, int64_t n0, int64_t n1,
   p.mu = (T)mu;
   p.inv_mu = (T)(1.0 / mu);
   p.a = (T)a;
-  p.a_next = (T)a_next;
   p.tau = (T)tau;
   p.pw = (T)prox_w;
   constexpr int V = kVecN<T>;
-  p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(w) && aligned16(hty) && aligned16(x_new) &&
-             (mode == kModeClassic || aligned16(y_next));
+  p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new);
   p.tv = lam != 0.0;
   p.prox = prox;
   p.diag = tuning(PXA_TUNE_PGD_DIAG);
@@ -627,16 +597,16 @@ int pgd_entry(int mode, int64_t stack, int64_t y_images, int64_t n0, int64_t n1,
   p.round1 = 4u * 256u;
   int st;
   switch (R) {
-    case 1: st = launch_pgd<T, 1>(mode, p, x, w, hty, x_new, y_next, partials, s); break;
-    case 2: st = launch_pgd<T, 2>(mode, p, x, w, hty, x_new, y_next, partials, s); break;
-    case 3: st = launch_pgd<T, 3>(mode, p, x, w, hty, x_new, y_next, partials, s); break;
-    case 4: st = launch_pgd<T, 4>(mode, p, x, w, hty, x_new, y_next, partials, s); break;
-    case 5: st = launch_pgd<T, 5>(mode, p, x, w, hty, x_new, y_next, partials, s); break;
-    case 6: st = launch_pgd<T, 6>(mode, p, x, w, hty, x_new, y_next, partials, s); break;
-    case 7: st = launch_pgd<T, 7>(mode, p, x, w, hty, x_new, y_next, partials, s); break;
-    default: st = launch_pgd<T, 8>(mode, p, x, w, hty, x_new, y_next, partials, s); break;
+    case 1: st = launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 2: st = launch_pgd<T, 2>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 3: st = launch_pgd<T, 3>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 4: st = launch_pgd<T, 4>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 5: st = launch_pgd<T, 5>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 6: st = launch_pgd<T, 6>(p, x, x_prev, hty, x_new, partials, s); break;
+    case 7: st = launch_pgd<T, 7>(p, x, x_prev, hty, x_new, partials, s); break;
+    default: st = launch_pgd<T, 8>(p, x, x_prev, hty, x_new, partials, s); break;
   }
-  if (st == PXA_OK) g_last_pgd_kernel = 1 + mode;
+  if (st == PXA_OK) g_last_pgd_kernel = 1;
   return st;
 }
 
@@ -666,21 +636,8 @@ int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, in
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
                       const void* x_prev, const void* hty, void* x_new, double* partials, void* stream) {
   PXA_DISPATCH(dtype, T,
-               return pgd_entry<T>(kModeClassic, stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1,
-                                   lam, mu, a, 0.0, tau, prox, prox_w, x, x_prev, hty, x_new, nullptr, partials,
-                                   as_stream(stream)));
-}
-
-int pxa_pgd_tv2d_step_y(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0,
-                        const int32_t* off0, const double* coef0, int nt1, const int32_t* off1, const double* coef1,
-                        double h0, double h1, double lam, double mu, double a, double a_next, double tau, int prox,
-                        double prox_w, const void* x, const void* x_prev, const void* y, const void* hty, void* x_new,
-                        void* y_next, double* partials, void* stream) {
-  const int mode = y ? kModeY : kModeSeed;
-  PXA_DISPATCH(dtype, T,
-               return pgd_entry<T>(mode, stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu,
-                                   a, a_next, tau, prox, prox_w, x, y ? y : x_prev, hty, x_new, y_next, partials,
-                                   as_stream(stream)));
+               return pgd_entry<T>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, a,
+                                   tau, prox, prox_w, x, x_prev, hty, x_new, partials, as_stream(stream)));
 }
 
 }  // extern "C"

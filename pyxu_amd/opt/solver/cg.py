@@ -36,6 +36,18 @@ class _HostRows:
         return self._h.numpy()
 
 
+class _KernelRows(_HostRows):
+    """A row statistic that a kernel writes into a device buffer AND straight into pinned host memory
+    (pxa_cg_update): no copy launch, one event."""
+
+    def __init__(self, dev, host):
+        import torch
+
+        self.dev, self._h = dev, host
+        self._ev = torch.cuda.Event()
+        self._ev.record()
+
+
 class CG(pxa.Solver):
     """Solve ``A x = b`` for positive-definite ``A`` (cg.py:14-187)."""
 
@@ -76,10 +88,17 @@ class CG(pxa.Solver):
 
             mst["b"], mst["x"] = bcast(b), bcast(x0)
         self._apply = self._make_apply(mst["x"])
-        mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._apply(mst["x"]))
+        if x0 is None:
+            # x = 0: A x = 0 exactly, so r = b - A x = b bit for bit -- skip the product (one full pass over
+            # the operator per solve; QuadraticFunc.prox, i.e. every ADMM x-update, starts from zero)
+            mst["residual"] = _dev.copy(mst["b"])
+        else:
+            mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._apply(mst["x"]))
         mst["conjugate_dir"] = _dev.copy(mst["residual"])
         self._rr = None  # ||r||^2 of the current residual, carried from the previous step's beta
         self._Ap_next = None  # A p of the current p, launched ahead by the previous step (see m_step)
+        self._rr_hist = []  # host ||r||^2 (max over rows) of the last steps: convergence-rate estimate
+        self._abs_eps = self._stop_eps()
         mst[_ROWSTAT] = {}
 
     def _make_apply(self, like):
@@ -131,16 +150,32 @@ class CG(pxa.Solver):
         Ap, self._Ap_next = self._Ap_next, None
         if Ap is None:
             Ap = self._apply(p)
-        pAp = _dev.row_reduce(_dev.RED_DOT, _rows2d(p), _rows2d(Ap))
         if self._rr is not None and self._rr[1] is r:
             rr = self._rr[0]  # ||r||^2 of this r: the previous step's beta numerator (identical bits)
         else:
             rr = _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)))
         self._rr = None
+        eps = pxrt.Width(np.dtype(str(x.dtype).replace("torch.", ""))).eps()
+        rr_host = rr.host()  # already waited for by the stop check of this iteration (same value)
+        fast = (not np.any(rr_host <= eps) and self._astate["idx"] % mst["restart_rate"] != 0
+                and 0 < _rows2d(x).shape[0] <= 65535)
+        if fast:
+            # the whole tail in three launches (pxa_cg_update): alpha, x, r, ||r'||^2, beta, p; ||r'||^2 is
+            # written straight into pinned host memory for the next stop check
+            hr = self._rows_buffers(_rows2d(x).shape[0])
+            _dev.cg_update(_rows2d(x), _rows2d(r), _rows2d(p), _rows2d(Ap), rr.dev, hr[0], hr[1], self._cg_work)
+            hr = _KernelRows(hr[0], hr[1])
+            self._rr = (hr, r)
+            if self._astate.get("internal"):
+                mst[_ROWSTAT] = {"residual": (r, 2, hr)}
+                if not self._predict_stop(rr_host):
+                    self._Ap_next = self._apply(p)
+            mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
+            return
+        pAp = _dev.row_reduce(_dev.RED_DOT, _rows2d(p), _rows2d(Ap))
         alpha = _dev.row_ratio(rr.dev, pAp, x)
         _dev.axpy_rows(alpha, 1.0, _rows2d(p), _rows2d(x), out=_rows2d(x))  # x += alpha p
-        eps = pxrt.Width(np.dtype(str(x.dtype).replace("torch.", ""))).eps()
-        if np.any(rr.host() <= eps):
+        if np.any(rr_host <= eps):
             _dev.axpby(1.0, mst["b"], -1.0, self._apply(x), out=r)
         else:
             _dev.axpy_rows(alpha, -1.0, _rows2d(Ap), _rows2d(r), out=_rows2d(r))  # r -= alpha A p
@@ -155,8 +190,50 @@ class CG(pxa.Solver):
             self._rr = (hr, r)
             if self._astate.get("internal"):
                 mst[_ROWSTAT] = {"residual": (r, 2, hr)}
-                self._Ap_next = self._apply(p)
+                if not self._predict_stop(rr_host):
+                    self._Ap_next = self._apply(p)
         mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
+
+    def _rows_buffers(self, rows):
+        """(device, pinned host) float64 (rows,) buffers for ||r'||^2, two sets used alternately (a step reads
+        the previous step's device value while its kernel writes the other), plus the update workspace."""
+        import torch
+
+        bufs = getattr(self, "_rr_bufs", None)
+        if bufs is None or bufs[0][0].numel() != rows:
+            dev = self._mstate["x"].device
+            bufs = [(torch.empty((rows,), dtype=torch.float64, device=dev),
+                     torch.empty((rows,), dtype=torch.float64, pin_memory=True)) for _ in range(2)]
+            self._rr_bufs, self._rr_flip = bufs, 0
+            self._cg_work = torch.empty((max(int(_dev.lib.pxa_cg_update_workspace_bytes(rows)) // 8, 1),),
+                                        dtype=torch.float64, device=dev)
+        self._rr_flip ^= 1
+        return bufs[self._rr_flip]
+
+    def _stop_eps(self):
+        """eps of the AbsError(var="residual", norm=2) in this run's stop criterion (None if absent)."""
+        from pyxu_amd.abc.solver import _StoppingCriteriaComposition
+        from pyxu_amd.opt.stop import AbsError
+
+        todo, found = [self._astate.get("stop_crit")], None
+        while todo:
+            c = todo.pop()
+            if isinstance(c, _StoppingCriteriaComposition):
+                todo += [c._lhs, c._rhs]
+            elif isinstance(c, AbsError) and c._var == "residual" and c._norm == 2 and c._reduce is None:
+                found = float(c._eps)
+        return found
+
+    def _predict_stop(self, rr_host):
+        """Whether the NEXT stop check will probably end the solve, from the geometric rate of the last two
+        ||r||^2: then A p' is not launched ahead (it would be dropped).  A wrong guess either way only
+        moves where A p' is computed; the iterates are the same."""
+        self._rr_hist = (self._rr_hist + [float(np.max(rr_host))])[-2:]
+        if self._abs_eps is None or len(self._rr_hist) < 2 or self._rr_hist[0] <= 0:
+            return False
+        r0, r1 = self._rr_hist
+        pred = r1 * (r1 / r0)  # ||r_next||^2 at the current contraction rate
+        return pred <= self._abs_eps**2
 
     def default_stop_crit(self):
         from pyxu_amd.opt.stop import AbsError

@@ -22,9 +22,8 @@ class AutoInferenceWarning(UserWarning):
 
 
 class _Momentum:
-    """The momentum sequence a_k (pgd.py:164-171) with a one-value look-ahead: the fused y-state step
-    writes the next iteration's momentum point, so it needs a_{k+1} while consuming a_k.  `push`
-    returns a consumed value (speculative-step rollback)."""
+    """The momentum sequence a_k (pgd.py:164-171) with `push`, which returns a consumed value (rollback of a
+    speculative step) without nesting one more itertools.chain per rollback."""
 
     def __init__(self, it):
         self._it = iter(it)
@@ -35,11 +34,6 @@ class _Momentum:
 
     def __next__(self):
         return self._buf.pop() if self._buf else next(self._it)
-
-    def peek(self):
-        if not self._buf:
-            self._buf.append(next(self._it))
-        return self._buf[-1]
 
     def push(self, v):
         self._buf.append(v)
@@ -106,9 +100,6 @@ class PGD(pxa.Solver):
             p["parts"] = _dev.empty_f64((2 * ntiles,), x0)
             p["tiles_per_row"] = ntiles // max(p["rows"], 1)
             self._spare = None
-            # the momentum point yk = (x - x_prev) * a + x is carried as state (pxa_pgd_tv2d_step_y): the
-            # solver owns both y buffers (never exposed), None = derive it from (x, x_prev) in the next step
-            self._y = self._y_spare = None
             # the solver never writes a tensor it has published as x (outputs go to fresh or recycled
             # buffers nobody else references), so stop criteria may keep references instead of copies
             mst["__immutable__"] = frozenset({"x"})
@@ -132,7 +123,6 @@ class PGD(pxa.Solver):
         mst["a"].push(self._last_a)
         mst.pop("__relerr__", None)
         self._spare = None
-        self._y = None  # the carried momentum point belonged to the undone step
         self._spec_refs = 0
 
     def m_step(self):
@@ -146,7 +136,6 @@ class PGD(pxa.Solver):
             out = self._spare
             if out is None or out is x or out is xp:
                 out = _dev.empty_like(x)
-            y_next = self._y_spare if self._y_spare is not None else _dev.empty_like(x)
             tau = mst["tau"]
             # RelError partials only for the launch right before a stop check (the engine advances idx
             # before m_step: the next check runs at idx when idx % stop_rate == 0)
@@ -154,9 +143,9 @@ class PGD(pxa.Solver):
             want = (self._fused_relerr and ast.get("stop_rate") is not None
                     and ast["idx"] % ast["stop_rate"] == 0)
             parts = p["parts"] if want else None
-            _dev.pgd_tv2d_step_y(x, xp, self._y, p["hty"], out, y_next, a, mst["a"].peek(), tau, p["prox"],
-                                 tau * p["prox_scale"], p["pre"], partials=parts)
-            self._y_spare, self._y = self._y, y_next
+            _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
+                               p["h0"], p["h1"], p["lam"], p["mu"], a, tau, p["prox"], tau * p["prox_scale"],
+                               partials=parts, pre=p["pre"])
             if want:  # (var, x_new, the x the statistics are relative to, partials, rows, tiles per row)
                 mst["__relerr__"] = ("x", out, x, parts, p["rows"], p["tiles_per_row"])
             else:

@@ -1,5 +1,4 @@
-"""A/B probe of the fused PGD launch: classic (x, x_prev window) vs y-state (carried y window) modes and
-the PXA_TUNE_PGD_STAGGER start-delay settings, at 2048^2 / 4096^2 fp32 (Gaussian sigma=2, TV, PositiveOrthant).
+"""A/B probe of the fused PGD launch (pxa_pgd_tv2d_step) under PXA_TUNE_PGD_STAGGER start-delay settings, at 2048^2 / 4096^2 fp32 (Gaussian sigma=2, TV, PositiveOrthant).
 Each configuration is timed as windows of 50 back-to-back launches between two HIP events (the bench's
 LaunchTimer convention), the configurations interleaved over 5 rounds; prints the median per launch.
 usage: python scripts/pgd_modes_probe.py [n ...]"""
@@ -24,12 +23,8 @@ def setup(n):
 
 
 def launch(a, pre, mode):
-    if mode == "classic":
-        _dev.pgd_tv2d_step(a["x"], a["xp"], a["b"], a["out"], *([None] * 14), pre=pre) if False else \
-            _dev.lib.pxa_pgd_tv2d_step(0, *pre, 0.3, 0.5, 1, 0.0, a["x"].data_ptr(), a["xp"].data_ptr(), a["b"].data_ptr(),
-                                       a["out"].data_ptr(), None, _dev.stream())
-    else:
-        _dev.pgd_tv2d_step_y(a["x"], a["xp"], a["y"], a["b"], a["out"], a["yn"], 0.3, 0.4, 0.5, 1, 0.0, pre)
+    _dev.lib.pxa_pgd_tv2d_step(0, *pre, 0.3, 0.5, 1, 0.0, a["x"].data_ptr(), a["xp"].data_ptr(), a["b"].data_ptr(),
+                               a["out"].data_ptr(), None, _dev.stream())
 
 
 def window(a, pre, mode, stagger, n_launch=50):
@@ -46,7 +41,7 @@ def window(a, pre, mode, stagger, n_launch=50):
 
 def main():
     sizes = [int(v) for v in sys.argv[1:]] or [2048, 4096]
-    confs = [("classic", 0), ("y", 0)] + [("classic", (sel << 8) | nn) for sel in (1, 2, 4) for nn in (2, 4, 8)]
+    confs = [("classic", 0)] + [("classic", (sel << 8) | nn) for sel in (4,) for nn in (4,)]
     for n in sizes:
         a, pre = setup(n)
         for m, s in confs:

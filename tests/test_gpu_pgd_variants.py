@@ -1,13 +1,16 @@
 """
-Fused PGD step modes (csrc/pgd_tv2d.hip) against each other, bit for bit.
+The fused PGD tile kernel (csrc/pgd_tv2d.hip) against itself on its different code paths, bit for bit:
 
-The classic launch (pxa_pgd_tv2d_step) forms the momentum point yk = (x - x_prev) * a + x inside its
-window load.  The y-state launches (pxa_pgd_tv2d_step_y) carry yk as solver state: the seed launch
-forms it like the classic one and also writes y_next = (x_new - x) * a_next + x_new, the steady-state
-launch reads y instead of (x, x_prev).  Every per-pixel fp32 operation is the same, so x_new must agree
-BIT FOR BIT on every shape class: interior and edge tiles, ragged tile grids, fewer tiles than
-resident workgroups, stacks with shared and per-image data, every blur radius 1..8, every prox kind.
-The classic kernel itself is pinned to the oracle by test_gpu_parity.py and test_gpu_bench_shapes.py.
+* the 16-B vector path of the edge tiles (a vector that lies inside the image is moved as one access)
+  against the all-scalar path the kernel takes when the arrays are not 16-B aligned;
+* launches with and without the RelError partials;
+* the partials themselves against the separate RelError pass (pxa_relerr_stats) and the solver's
+  stop_rate = 1 path that consumes them (pxa_tile_partials_fold).
+
+Every per-pixel fp32 operation is the same on every path, so x_new must agree BIT FOR BIT on every shape
+class: interior and edge tiles, ragged tile grids, fewer tiles than resident workgroups, stacks with shared
+and per-image data, every blur radius 1..8, every prox kind.  The kernel itself is pinned to the oracle by
+test_gpu_parity.py and test_gpu_bench_shapes.py.
 """
 import numpy as np
 import pytest
@@ -60,23 +63,23 @@ def _plan(sh, stack, y_images, sigma, g_kind, fused=True, **kw):
         return s
 
 
-def _classic(s, x, xp, a, parts=None):
+def _launch(s, x, xp, hty, a, parts=None):
     p, m = s._plan, s._mstate
     out = _dev.empty_like(x)
-    _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
+    _dev.pgd_tv2d_step(x, xp, hty, out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
                        p["h1"], p["lam"], p["mu"], a, m["tau"], p["prox"], m["tau"] * p["prox_scale"], partials=parts,
                        pre=p["pre"])
     assert int(lib.pxa_pgd_tv2d_last_kernel()) == 1
     return out
 
 
-def _ystep(s, x, xp, y, a, a_next, parts=None):
-    p, m = s._plan, s._mstate
-    out, yn = _dev.empty_like(x), _dev.empty_like(x)
-    _dev.pgd_tv2d_step_y(x, xp, y, p["hty"], out, yn, a, a_next, m["tau"], p["prox"], m["tau"] * p["prox_scale"],
-                         p["pre"], partials=parts)
-    assert int(lib.pxa_pgd_tv2d_last_kernel()) == (3 if y is not None else 2)
-    return out, yn
+def _misaligned(t):
+    """A copy of t whose data pointer is 4 B past a 16-B boundary (the kernel's scalar path)."""
+    buf = torch.empty(t.numel() + 4, dtype=t.dtype, device=t.device)
+    v = buf[1: 1 + t.numel()].view(t.shape)
+    v.copy_(t)
+    assert v.data_ptr() % 16 != 0
+    return v
 
 
 def _parts(s):
@@ -94,61 +97,34 @@ CASES = [
     ((257, 516), 1, 1, 1.0, "l1"),      # R = 3, odd row count
     ((128, 192), 3, 1, 2.0, "pos"),     # stacked initial points, one y
     ((64, 320), 4, 4, 1.5, "pos"),      # batch-as-axis: per-image data
-    ((517, 1003), 1, 1, 2.0, "l1"),     # R = 6, odd row length (no 16-B vector path)
     ((40, 36), 2, 2, 1.0, "none"),      # tiles larger than the image
 ]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}-sig{c[3]}-{c[4]}")
-def test_y_state_modes_bit_exact_vs_classic(case):
-    """Two iterations k, k+1 with momenta a = 0.37, a' = 0.61: the seed launch and then the y-state launch
-    reproduce the classic launch's x_new bit for bit, and the RelError partials of every mode are the same
-    bits (same per-tile order)."""
+def test_vector_and_scalar_paths_bit_exact(case):
+    """Aligned arrays (16-B vector loads / stores, also on the edge tiles' inside vectors) against
+    misaligned copies (every access scalar): x_new and the RelError partials bit for bit; a launch
+    without partials gives the same x_new."""
     sh, stack, y_images, sigma, g_kind = case
     s = _plan(sh, stack, y_images, sigma, g_kind)
-    m = s._mstate
-    x, xp = m["x"], m["x_prev"]
-    a, a2 = 0.37, 0.61
-    pc, ps, py = _parts(s), _parts(s), _parts(s)
-    c1 = _classic(s, x, xp, a, pc)
-    s1, y1 = _ystep(s, x, xp, None, a, a2, ps)
-    assert np.array_equal(to_NUMPY(c1), to_NUMPY(s1))
-    assert np.array_equal(to_NUMPY(pc), to_NUMPY(ps)) and np.all(to_NUMPY(pc) >= 0)
-    # y_next is the classic window's yk of the next iteration: (x1 - x) * a2 + x1 in one fma
-    x1, x0 = to_NUMPY(s1).astype(np.float64), to_NUMPY(x).astype(np.float64)
-    d = (to_NUMPY(s1) - to_NUMPY(x)).astype(np.float64)
-    ref = (d * np.float64(np.float32(a2)) + x1).astype(np.float32)
-    assert np.max(np.abs(to_NUMPY(y1) - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1.2e-7
-    c2 = _classic(s, c1, x, a2, pc)
-    s2, _ = _ystep(s, s1, None, y1, a2, 0.7, py)
-    assert np.array_equal(to_NUMPY(c2), to_NUMPY(s2))
-    assert np.array_equal(to_NUMPY(pc), to_NUMPY(py))
+    m, p = s._mstate, s._plan
+    x, xp, hty = m["x"], m["x_prev"], p["hty"]
+    pa, pb = _parts(s), _parts(s)
+    a = _launch(s, x, xp, hty, 0.37, pa)
+    b = _launch(s, _misaligned(x), _misaligned(xp), _misaligned(hty), 0.37, pb)
+    c = _launch(s, x, xp, hty, 0.37)
     torch.cuda.synchronize()
-
-
-def test_solver_y_state_trajectory_equals_classic_loop():
-    """30 iterations of the fused solver (seed launch, then y-state launches with the look-ahead momentum
-    a_{k+1} = (k+1)/(k+2+d)) against a loop of classic launches fed the reference's a_k: identical x."""
-    s = _plan((256, 320), 1, 1, 2.0, "pos")
-    f, g = s._f, s._g
-    rng = np.random.default_rng(3)
-    x0 = to_device(rng.uniform(0, 1, 256 * 320).astype(np.float32))
-    with pxrt.Precision(pxrt.Width.SINGLE):
-        sol = pxs.PGD(f=f, g=g, show_progress=False)
-        sol.fit(x0=x0, stop_crit=pxst.MaxIter(30))
-        got = to_NUMPY(sol.solution())
-        x, xp = x0, x0
-        for k in range(30):
-            a = float(np.float32(k / (k + 1 + 75)))
-            x, xp = _classic(s, x, xp, a), x
-    assert np.array_equal(got, to_NUMPY(x))
+    assert np.array_equal(to_NUMPY(a), to_NUMPY(b))
+    assert np.array_equal(to_NUMPY(a), to_NUMPY(c))
+    assert np.array_equal(to_NUMPY(pa), to_NUMPY(pb)) and np.all(to_NUMPY(pa) >= 0)
 
 
 @pytest.mark.parametrize("stack,rows", [(1, 1), (6, 3)])
 def test_fused_relerr_matches_separate_pass(stack, rows):
     """stop_rate 1 RelError from the kernel's per-tile partials (pxa_tile_partials_fold) against the
-    separate relerr_stats pass: the same stop iteration, values within 1e-6 relative, and the fused
-    path launches no relerr pass (no x copy)."""
+    separate relerr_stats pass: the same stop iteration, the same iterates, RelError values within 1e-6
+    relative; the fused path launches the separate pass at most once (the first comparison)."""
     y_images = stack // rows
     outs = {}
     for fused_rel in (True, False):
@@ -175,11 +151,10 @@ def test_fused_relerr_matches_separate_pass(stack, rows):
     (n1, h1, x1, c1), (n2, h2, x2, c2) = outs[True], outs[False]
     assert n1 == n2 and 1 < n1 < 500
     assert np.array_equal(x1, x2)
-    key = [k for k in h1.dtype.names if k.startswith("RelError")]
-    for k in key:
+    for k in [k for k in h1.dtype.names if k.startswith("RelError")]:
         v1, v2 = h1[k].astype(np.float64), h2[k].astype(np.float64)
         assert np.allclose(v1, v2, rtol=1e-6, atol=0), k
-    assert c1 <= 1 and c2 >= n2 - 2  # fused: at most the first comparison falls back to the separate pass
+    assert c1 <= 1 and c2 >= n2 - 2
 
 
 def test_wide_blur_warns_and_runs_generic_path():
