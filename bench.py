@@ -28,8 +28,7 @@ Sub-records on the same line (north_star):
         per-kernel times of the fused three-launch step (single GPU: replicas only at N > 1).
 
 Roofline convention.  `frac` is the dominant kernel's time against ITS OWN compulsory bytes (every array
-it must read or write, once): the y-state PGD launch reads y, x, H^T y and writes x_new, y_next =
-20 B/pixel.  `frac_survey` keeps SURVEY §8(d)'s 48 B/pixel figure for the same time; that model is not a
+it must read or write, once): the fused PGD launch reads x, x_prev, H^T y and writes x_new = 16 B/pixel.  `frac_survey` keeps SURVEY §8(d)'s 48 B/pixel figure for the same time; that model is not a
 bound on a one-launch kernel (it charges intermediates this kernel never materialises).
 """
 import argparse
@@ -50,8 +49,7 @@ KERNEL = "pgd_tv2d_kernel"
 SURVEY_BYTES_PER_PIXEL = 48  # 8 reads + 4 writes of fp32 per pixel per PGD iteration
 CPU_THREADS_MAX = 16  # the GPU box's CPU share per GPU (gpurun: 16)
 # pxa_pgd_tv2d_last_kernel() -> (mode name, own compulsory bytes per pixel): the arrays the launch reads / writes
-PGD_MODES = {1: ("classic: x, x_prev, H^T y -> x_new", 16), 2: ("seed: x, x_prev, H^T y -> x_new, y_next", 20),
-             3: ("y-state: y, x, H^T y -> x_new, y_next", 20)}
+PGD_MODES = {1: ("x, x_prev, H^T y -> x_new", 16)}
 
 
 # ----------------------------------------------------------------------------- launcher (no GPU here)

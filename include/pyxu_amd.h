@@ -48,7 +48,8 @@ extern "C" {
 #define PXA_MODE_EDGE 4
 
 /* Kernel-selection knobs (pxa_tuning). */
-#define PXA_TUNE_PGD_KERNEL 0 /* reserved (round 2's kernel variants were removed; 0 = the tile kernel) */
+#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 default, 1 the tile kernel, 2 the pipelined producer /
+                                 consumer kernel (fp32, blur radius <= 6; else the tile kernel) */
 #define PXA_TUNE_NORMAL_DIAG 1 /* pxa_dense_normal timing probes (WRONG results, measurement only): 0 off,
                                   1 no x loads, 2 no cross-wave reduction, 3 no LDS accumulator */
 #define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel: bit 5 s_memtime phase trace (pxa_pgd_tile_trace) */
@@ -379,10 +380,11 @@ int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int6
  * computed once by the caller (e.g. pxa_stencil_sep with the flipped taps).  `stack` independent
  * images, each (n0, n1), contiguous; image s uses data image (s % y_images) of hty (1 = one y shared
  * by a stack of initial points, stack = batch-as-axis images with their own data).  x_new must not
- * alias x or x_prev.  If `partials` is not NULL, each workgroup writes (sum (x_new-x)^2, sum x^2)
- * for RelError into partials[2*blk..] (double) — pxa_pgd_tv2d_partials_count() gives the number of
- * workgroups.  prox codes: 0 none, 1 positive orthant, 2 l1 with weight prox_w.
- * pxa_pgd_tv2d_last_kernel() is 1 once the calling thread has launched the tile kernel (0 before).
+ * alias x or x_prev.  If `partials` is not NULL, each (tile, wavefront) slot writes (sum (x_new-x)^2,
+ * sum x^2) for RelError into partials[2*slot..] (double) — pxa_pgd_tv2d_partials_count() gives the
+ * number of slots (tiles x 4; the slots of one image are contiguous).  prox codes: 0 none, 1 positive
+ * orthant, 2 l1 with weight prox_w.  pxa_pgd_tv2d_last_kernel() is the kernel the calling thread
+ * launched last: 1 the tile kernel, 2 the pipelined kernel (0 before any launch).
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
 int pxa_pgd_tv2d_last_kernel(void);

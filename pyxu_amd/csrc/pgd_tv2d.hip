@@ -87,58 +87,76 @@ __device__ inline float tv_weight<float>(float n2, float lam, float mu, float in
 
 // ---- phase 0 of the tile kernel: yk = (x - x_prev) * a + x on the A window, zero outside the image.
 // All K0 vector pairs of a thread are loaded before the first LDS store, so their latencies overlap.
+// `lt`: the thread's index among the kThreads threads that share the window.
+template <typename T, int R>
+struct Window {
+  using L = Layout<T, R>;
+  static constexpr int K0 = cdiv(L::N0, kThreads);
+  T xv[K0][L::V], pv[K0][L::V];
+};
+
 template <typename T, int R, bool EDGE>
-__device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0, const T* __restrict__ xs,
-                                   const T* __restrict__ xps) {
+__device__ inline void win_issue(const PgdParams<T>& p, int ty0, int tx0, const T* __restrict__ xs,
+                                 const T* __restrict__ xps, Window<T, R>& w, int lt) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
   const int n0 = p.n0, n1 = p.n1;
-  const int tid = threadIdx.x;
-  constexpr int K0 = cdiv(L::N0, kThreads);
-  T xv[K0][V], pv[K0][V];
 #pragma unroll
-  for (int k = 0; k < K0; ++k) {
-    const int it = tid + k * kThreads;
+  for (int k = 0; k < Window<T, R>::K0; ++k) {
+    const int it = lt + k * kThreads;
     if (it < L::N0) {
       const int r = it / L::NGA, g = it - r * L::NGA;
       const int gr = ty0 - 2 * R + r, gc = tx0 - CA + V * g;
       if (!EDGE) {
         const unsigned off = (unsigned)(gr * n1 + gc);
-        ld_vec<T, V>(xs + off, xv[k]);
-        ld_vec<T, V>(xps + off, pv[k]);
+        ld_vec<T, V>(xs + off, w.xv[k]);
+        ld_vec<T, V>(xps + off, w.pv[k]);
       } else if (gr >= 0 && gr < n0 && p.vec_ok && gc >= 0 && gc + V <= n1) {
-        ld_vec<T, V>(xs + (int64_t)gr * n1 + gc, xv[k]);
-        ld_vec<T, V>(xps + (int64_t)gr * n1 + gc, pv[k]);
+        ld_vec<T, V>(xs + (int64_t)gr * n1 + gc, w.xv[k]);
+        ld_vec<T, V>(xps + (int64_t)gr * n1 + gc, w.pv[k]);
       } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           const bool in = gr >= 0 && gr < n0 && gc + v >= 0 && gc + v < n1;
-          xv[k][v] = in ? xs[(int64_t)gr * n1 + gc + v] : T(0);
-          pv[k][v] = in ? xps[(int64_t)gr * n1 + gc + v] : T(0);
+          w.xv[k][v] = in ? xs[(int64_t)gr * n1 + gc + v] : T(0);
+          w.pv[k][v] = in ? xps[(int64_t)gr * n1 + gc + v] : T(0);
         }
       }
     }
   }
+}
+
+template <typename T, int R>
+__device__ inline void win_store(const PgdParams<T>& p, T* A, const Window<T, R>& w, int lt) {
+  using L = Layout<T, R>;
+  constexpr int V = L::V;
 #pragma unroll
-  for (int k = 0; k < K0; ++k) {
-    const int it = tid + k * kThreads;
+  for (int k = 0; k < Window<T, R>::K0; ++k) {
+    const int it = lt + k * kThreads;
     if (it < L::N0) {
       const int r = it / L::NGA, g = it - r * L::NGA;
       T out[V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) out[v] = fma(xv[k][v] - pv[k][v], p.a, xv[k][v]);  // one rounding site
+      for (int v = 0; v < V; ++v) out[v] = fma(w.xv[k][v] - w.pv[k][v], p.a, w.xv[k][v]);  // one rounding site
       st_vec<T, V>(A + r * L::AP + V * g, out);
     }
   }
 }
 
+template <typename T, int R, bool EDGE>
+__device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0, const T* __restrict__ xs,
+                                   const T* __restrict__ xps) {
+  Window<T, R> w;
+  win_issue<T, R, EDGE>(p, ty0, tx0, xs, xps, w, threadIdx.x);
+  win_store<T, R>(p, A, w, threadIdx.x);
+}
+
 // ---- pass A: PT[col][row] = (G0 yk)[row][col] for the TY tile rows and all A columns
 template <typename T, int R, bool EDGE>
-__device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T* KT, int ty0) {
+__device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T* KT, int ty0, int tid = threadIdx.x) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
-  const int tid = threadIdx.x;
   constexpr int KA = cdiv(L::NPA, kThreads);
   // one item per thread (fp32): items spread over all 4 waves in chunks of a multiple of NA, so each
   // lane keeps it % NA == lane % NA (the conflict-free lane pattern) -- e.g. 48 / 48 / 48 / 32 for the
@@ -171,13 +189,12 @@ __device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T*
 // coalesced epilogue (epilogue_staged).
 template <typename T, int R, bool EDGE, typename Emit>
 __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, const T* KT, const T* GH, int ty0, int tx0,
-                              Emit&& emit) {
+                              Emit&& emit, int tid = threadIdx.x) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
   constexpr int CW = L::CW;
   const int n0 = p.n0, n1 = p.n1;
-  const int tid = threadIdx.x;
   constexpr int KB = cdiv(L::NPB, kThreads);
   const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n1 - R);
 #pragma unroll
@@ -288,12 +305,13 @@ __device__ inline bool vec_inside(const PgdParams<T>& p, int gr, int gc) {
 }
 
 template <typename T, int R, bool EDGE>
-__device__ inline void load_staged(const PgdParams<T>& p, int ty0, int tx0, const T* __restrict__ src, T (&v)[StagedB<T, R>::NS][kVecN<T>]) {
+__device__ inline void load_staged(const PgdParams<T>& p, int ty0, int tx0, const T* __restrict__ src, T (&v)[StagedB<T, R>::NS][kVecN<T>],
+                                   int lt = threadIdx.x) {
   using S = Stage<T, R>;
   constexpr int V = kVecN<T>;
   const int n0 = p.n0, n1 = p.n1;
   int r0, cq;
-  S::lane(threadIdx.x, r0, cq);
+  S::lane(lt, r0, cq);
 #pragma unroll
   for (int s = 0; s < StagedB<T, R>::NS; ++s) {  // all loads first: one round trip
     const int gr = ty0 + r0 + s * S::RPS, gc = tx0 + V * cq;
@@ -349,31 +367,19 @@ __device__ inline void finish_vec(const PgdParams<T>& p, int gr, int gc, const T
   }
 }
 
-// Workgroup fold of the per-thread RelError partials into partials[2 tile .. 2 tile + 1] (fixed order).
-// `red`: 2 * kThreads / 64 doubles of LDS that no other phase touches between the two barriers.
-template <typename Barrier>
-__device__ inline void fold_partials(double part_d, double part_x, double* red, double* partials, unsigned tile,
-                                     Barrier&& barrier) {
+// RelError partials per wavefront: lane 0 of the wave writes its (sum (x_new - x)^2, sum x^2) to
+// partials[2 slot .. 2 slot + 1], slot = tile * kPartWaves + wave (fixed-order shuffle fold, no barrier).
+constexpr int kPartWaves = kThreads / 64;
+
+__device__ inline void wave_partials(double part_d, double part_x, double* partials, unsigned slot) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     part_d += __shfl_down(part_d, off, 64);
     part_x += __shfl_down(part_x, off, 64);
   }
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  barrier();
-  if (lane == 0) {
-    red[w] = part_d;
-    red[kThreads / 64 + w] = part_x;
-  }
-  barrier();
-  if (tid == 0) {
-    double a0 = 0, a1 = 0;
-    for (int k = 0; k < kThreads / 64; ++k) {
-      a0 += red[k];
-      a1 += red[kThreads / 64 + k];
-    }
-    partials[2 * tile] = a0;
-    partials[2 * tile + 1] = a1;
+  if ((threadIdx.x & 63) == 0) {
+    partials[2 * slot] = part_d;
+    partials[2 * slot + 1] = part_x;
   }
 }
 
@@ -465,7 +471,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     }
   }
   tmark(7);
-  if (want_part) fold_partials(part_d, part_x, reinterpret_cast<double*>(smem), partials, tile, [] { __syncthreads(); });
+  if (want_part) wave_partials(part_d, part_x, partials, tile * kPartWaves + (tid >> 6));
   const unsigned nb = gridDim.x, bid = blockIdx.x;
   if (tracing && (bid == 0 || bid == 1 || bid == nb / 2 || bid == nb - 1)) {
     __syncthreads();
@@ -513,6 +519,222 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
     pgd_tile<T, R, false>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
   else
     pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
+}
+
+// =====================================================================================================
+// Pipelined form (fp32): the same per-tile arithmetic as pgd_tv2d_kernel (bit-identical x_new), with the
+// window traffic of tile i+1 in flight while tile i computes.
+//
+// The tile kernel serialises per workgroup: window load -> pass A -> pass B -> epilogue, and at 2048^2
+// its 2 048 workgroups run as two synchronous rounds of 1 024 (4 per CU): the whole chip loads, then the
+// whole chip computes (phase trace: ~10 k of 23.5 k cycles per tile in the window load; SQ_WAIT_ANY 42 %).
+// Here 2 persistent workgroups of 2 x 256 threads per CU walk a static list of tiles (XCD-banded) with two
+// roles, wave-uniform:
+//   consumers (waves 0-3): pass A (A[i] -> PT) | barrier | pass B (PT, A[i] -> O) | barrier
+//   producers (waves 4-7): epilogue of tile i-1 (O, A[i-1], H^T y -> x_new, RelError partials) and the
+//                          H^T y / x loads of tile i | barrier | yk of tile i+1 from registers loaded one
+//                          tile earlier -> A[i+1], then the loads of tile i+2's window | barrier
+// A is double-buffered and O has its own region, so one tile costs two barriers (three on edge-column
+// tiles: the cooperative ghost terms between pass A and pass B are computed by all 512 threads).  The
+// loads of tile i+2's x / x_prev window are issued at the end of tile i and consumed one whole tile later.
+// LDS: 2 A windows + PT + O + taps + ghost terms = 65 KB at R = 6 (two workgroups per CU); 128 VGPRs.
+constexpr int kPcThreads = 2 * kThreads;
+
+template <typename T, int R>
+struct PcCarve {
+  using L = Layout<T, R>;
+  static constexpr size_t A_BYTES = ((size_t)L::AR * L::AP * sizeof(T) + 15) / 16 * 16;
+  static constexpr size_t PT_OFF = 2 * A_BYTES;
+  static constexpr size_t O_OFF = PT_OFF + ((size_t)L::AC * L::PTP * sizeof(T) + 15) / 16 * 16;
+  static constexpr size_t KT_OFF = O_OFF + (size_t)TY * Stage<T, R>::OP * sizeof(T);
+  static constexpr size_t GH_OFF = KT_OFF + ((size_t)2 * kKT * sizeof(T) + 15) / 16 * 16;
+  static constexpr size_t BYTES = GH_OFF + kGhBytes<T, R>;
+};
+
+// geometry of one tile (the tile kernel's decode)
+struct TileRef {
+  int ty0, tx0;
+  int64_t xoff, boff;  // element offsets of the tile's image in x / x_prev / x_new and in H^T y
+  bool interior, edge_cols;
+};
+
+template <typename T, int R>
+__device__ inline TileRef tile_ref(const PgdParams<T>& p, unsigned tile) {
+  using L = Layout<T, R>;
+  const unsigned tpi = (unsigned)p.tiles0 * (unsigned)p.tiles1;
+  const unsigned s = tile / tpi;
+  const unsigned tr = tile - s * tpi;
+  const unsigned trow = tr / (unsigned)p.tiles1;
+  TileRef t;
+  t.ty0 = (int)trow * TY;
+  t.tx0 = (int)(tr - trow * (unsigned)p.tiles1) * TX;
+  const int64_t img = (int64_t)p.n0 * p.n1;
+  t.xoff = (int64_t)s * img;
+  t.boff = (int64_t)(s % (unsigned)p.y_images) * img;
+  t.interior = p.vec_ok && img <= 0x7fffffff && t.ty0 - 2 * R >= 0 && t.ty0 + TY + 2 * R <= p.n0 &&
+               t.tx0 - L::CA >= 0 && t.tx0 + TX + L::CA <= p.n1;
+  t.edge_cols = !t.interior && (t.tx0 < R || t.tx0 + TX > p.n1 - R);
+  return t;
+}
+
+// This workgroup's tiles: first, first + stride, ... (count of them).  banded: XCD g = blockIdx % 8 walks
+// its own contiguous band of tiles (the tile kernel's xcd_tile partition; needs gridDim % 8 == 0).
+struct TileSeq {
+  unsigned first, stride, count;
+};
+
+__device__ inline TileSeq tile_seq(unsigned ntiles, bool banded) {
+  const unsigned G = gridDim.x, b = blockIdx.x;
+  if (!banded) return {b, G, b < ntiles ? (ntiles - b + G - 1) / G : 0u};
+  const unsigned g = b & 7u, j = b >> 3, nj = (G - g + 7u) >> 3;
+  const unsigned q8 = ntiles >> 3, r8 = ntiles & 7u;
+  const unsigned lo = g * q8 + (g < r8 ? g : r8), len = q8 + (g < r8 ? 1u : 0u);
+  return {lo + j, nj, j < len ? (len - j + nj - 1) / nj : 0u};
+}
+
+template <int R>
+__global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> p, const float* __restrict__ x,
+                                                             const float* __restrict__ xp, const float* __restrict__ b,
+                                                             float* __restrict__ xn, double* __restrict__ partials,
+                                                             int banded) {
+  using T = float;
+  using L = Layout<T, R>;
+  using S = Stage<T, R>;
+  using C = PcCarve<T, R>;
+  constexpr int V = L::V;
+  constexpr int CW = L::CW;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  unsigned char* smem = smem_raw;
+  T* PT = reinterpret_cast<T*>(smem + C::PT_OFF);
+  T* O = reinterpret_cast<T*>(smem + C::O_OFF);
+  T* KT = reinterpret_cast<T*>(smem + C::KT_OFF);
+  T* GH = reinterpret_cast<T*>(smem + C::GH_OFF);
+  const TileSeq seq = tile_seq(p.ntiles, banded != 0);
+  if (seq.count == 0) return;  // (uniform over the workgroup)
+  const int lt = threadIdx.x & (kThreads - 1);
+  const bool want_part = partials != nullptr;
+  auto abuf = [&](unsigned i) { return reinterpret_cast<T*>(smem + (i & 1u) * C::A_BYTES); };
+  auto tile_of = [&](unsigned i) { return seq.first + i * seq.stride; };
+  if (threadIdx.x >= kThreads) {  // ---------------- producers (waves 4-7)
+    Window<T, R> w;
+    StagedB<T, R> hb;
+    auto issue = [&](unsigned i) {
+      const TileRef t = tile_ref<T, R>(p, tile_of(i));
+      if (t.interior) win_issue<T, R, false>(p, t.ty0, t.tx0, x + t.xoff, xp + t.xoff, w, lt);
+      else win_issue<T, R, true>(p, t.ty0, t.tx0, x + t.xoff, xp + t.xoff, w, lt);
+    };
+    auto stage_b = [&](unsigned i) {
+      const TileRef t = tile_ref<T, R>(p, tile_of(i));
+      if (t.interior) {
+        load_staged<T, R, false>(p, t.ty0, t.tx0, b + t.boff, hb.v, lt);
+        if (want_part) load_staged<T, R, false>(p, t.ty0, t.tx0, x + t.xoff, hb.x, lt);
+      } else {
+        load_staged<T, R, true>(p, t.ty0, t.tx0, b + t.boff, hb.v, lt);
+        if (want_part) load_staged<T, R, true>(p, t.ty0, t.tx0, x + t.xoff, hb.x, lt);
+      }
+    };
+    auto epilogue = [&](unsigned i) {
+      const unsigned tile = tile_of(i);
+      const TileRef t = tile_ref<T, R>(p, tile);
+      const T* A = abuf(i);
+      double part_d = 0.0, part_x = 0.0;
+      int r0, cq;
+      S::lane(lt, r0, cq);
+#pragma unroll
+      for (int s = 0; s < StagedB<T, R>::NS; ++s) {
+        const int r = r0 + s * S::RPS;
+        T g[V], y[V];
+        ld_vec<T, V>(O + S::idx(r, V * cq), g);
+        ld_vec<T, V>(A + (r + 2 * R) * L::AP + L::CA + V * cq, y);
+        if (t.interior)
+          finish_vec<T, false>(p, t.ty0 + r, t.tx0 + V * cq, g, hb.v[s], y, hb.x[s], xn + t.xoff, want_part, part_d, part_x);
+        else
+          finish_vec<T, true>(p, t.ty0 + r, t.tx0 + V * cq, g, hb.v[s], y, hb.x[s], xn + t.xoff, want_part, part_d, part_x);
+      }
+      if (want_part) wave_partials(part_d, part_x, partials, tile * kPartWaves + (lt >> 6));
+    };
+    issue(0);
+    win_store<T, R>(p, abuf(0), w, lt);
+    if (seq.count > 1) issue(1);
+    __syncthreads();  // B0: A[0] ready
+    for (unsigned i = 0; i < seq.count; ++i) {
+      if (i >= 1) epilogue(i - 1);
+      stage_b(i);
+      __syncthreads();  // B1
+      if (tile_ref<T, R>(p, tile_of(i)).edge_cols) {
+        ghost_cols_coop<T, R>(p.k1, PT, GH, tile_ref<T, R>(p, tile_of(i)).tx0, p.n1, threadIdx.x, kPcThreads);
+        __syncthreads();  // B1'
+      }
+      if (i + 1 < seq.count) {
+        win_store<T, R>(p, abuf(i + 1), w, lt);
+        if (i + 2 < seq.count) issue(i + 2);
+      }
+      __syncthreads();  // B2
+    }
+    epilogue(seq.count - 1);
+  } else {  // ---------------------------------------- consumers (waves 0-3)
+    if (lt < 2 * R + 1) {
+      KT[lt] = p.k0[lt];
+      KT[kKT + lt] = p.k1[lt];
+    }
+    __syncthreads();  // B0
+    for (unsigned i = 0; i < seq.count; ++i) {
+      const TileRef t = tile_ref<T, R>(p, tile_of(i));
+      const T* A = abuf(i);
+      if (t.interior) pass_a<T, R, false>(p, A, PT, KT, t.ty0, lt);
+      else pass_a<T, R, true>(p, A, PT, KT, t.ty0, lt);
+      __syncthreads();  // B1
+      if (t.edge_cols) {
+        ghost_cols_coop<T, R>(p.k1, PT, GH, t.tx0, p.n1, threadIdx.x, kPcThreads);
+        __syncthreads();  // B1'
+      }
+      auto emit = [&](int, int, int gr, int gc, const T(&g)[CW], const T(&)[CW]) {
+        *reinterpret_cast<float2*>(O + S::idx(gr - t.ty0, gc - t.tx0)) = make_float2(g[0], g[1]);
+      };
+      if (t.interior) pass_b<T, R, false>(p, A, PT, KT, GH, t.ty0, t.tx0, emit, lt);
+      else pass_b<T, R, true>(p, A, PT, KT, GH, t.ty0, t.tx0, emit, lt);
+      __syncthreads();  // B2
+    }
+  }
+}
+
+// CUs of the current device (cached per device ordinal)
+inline int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+template <int R>
+int launch_pgd_pc(const PgdParams<float>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
+                  hipStream_t s) {
+  using C = PcCarve<float, R>;
+  static_assert(C::BYTES <= 80 * 1024, "two pipelined workgroups per CU");
+  auto kern = pgd_pc_kernel<R>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::BYTES);
+    attr_set = true;
+  }
+  unsigned grid;
+  int banded;
+  if (p.ntiles >= 8) {
+    const unsigned g2 = 2u * (unsigned)device_cus();
+    grid = (p.ntiles < g2 ? p.ntiles : g2) & ~7u;
+    banded = 1;
+  } else {
+    grid = p.ntiles;
+    banded = 0;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kPcThreads), C::BYTES, s, p, (const float*)x, (const float*)xp,
+                     (const float*)b, (float*)xn, partials, banded);
+  return last_launch_status();
 }
 
 template <typename T, int R>
@@ -596,6 +818,22 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.stagger = tuning(PXA_TUNE_PGD_STAGGER);
   p.round1 = 4u * 256u;
   int st;
+  // kernel selection (PXA_TUNE_PGD_KERNEL: 0 default, 1 tile kernel, 2 pipelined kernel)
+  const int ksel = tuning(PXA_TUNE_PGD_KERNEL);
+  if constexpr (sizeof(T) == 4) {
+    if (ksel == 2 && R <= 6) {
+      switch (R) {
+        case 1: st = launch_pgd_pc<1>(p, x, x_prev, hty, x_new, partials, s); break;
+        case 2: st = launch_pgd_pc<2>(p, x, x_prev, hty, x_new, partials, s); break;
+        case 3: st = launch_pgd_pc<3>(p, x, x_prev, hty, x_new, partials, s); break;
+        case 4: st = launch_pgd_pc<4>(p, x, x_prev, hty, x_new, partials, s); break;
+        case 5: st = launch_pgd_pc<5>(p, x, x_prev, hty, x_new, partials, s); break;
+        default: st = launch_pgd_pc<6>(p, x, x_prev, hty, x_new, partials, s); break;
+      }
+      if (st == PXA_OK) g_last_pgd_kernel = 2;
+      return st;
+    }
+  }
   switch (R) {
     case 1: st = launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s); break;
     case 2: st = launch_pgd<T, 2>(p, x, x_prev, hty, x_new, partials, s); break;
@@ -627,7 +865,7 @@ int pxa_pgd_tile_trace(uint64_t* host_out, int n) {
 }
 
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1) {
-  int64_t t = stack * ((n0 + TY - 1) / TY) * ((n1 + TX - 1) / TX);
+  int64_t t = stack * ((n0 + TY - 1) / TY) * ((n1 + TX - 1) / TX) * kPartWaves;
   return (int)t;
 }
 

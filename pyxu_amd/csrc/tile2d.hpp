@@ -178,9 +178,10 @@ __device__ inline void ghost_fix(int i0, int n, int q0, const T* __restrict__ sr
 // column and lane: one wave then runs thousands of cycles past the others (measured by the PGD
 // kernels' s_memtime trace).  Followed by a barrier, then ghost_fix_pre() in pass B.
 template <typename T, int R>
-__device__ inline void ghost_cols_coop(const T* __restrict__ k, const T* PT, T* GH, int tx0, int n) {
+__device__ inline void ghost_cols_coop(const T* __restrict__ k, const T* PT, T* GH, int tx0, int n, int lt = threadIdx.x,
+                                       int nthr = kThreads) {
   using L = Layout<T, R>;
-  for (int t = threadIdx.x; t < 2 * R * TY; t += kThreads) {
+  for (int t = lt; t < 2 * R * TY; t += nthr) {
     const int side = t / (R * TY), m = (t / TY) % R, r = t % TY;
     const int row = (side == 0 ? -R : n) + m - (tx0 - L::CA);  // PT row of the ghost column
     T g = T(0);

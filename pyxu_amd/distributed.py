@@ -118,7 +118,8 @@ def gather_slabs(x_local, n_global, group=None):
     if x_local.shape[0] != m:  # pad the slab to the largest one (pxa_fill + pxa_copy2d on the device)
         n_row = int(np.prod(x_local.shape[1:]))
         buf = _dev_zeros((m, *x_local.shape[1:]), x_local)
-        _dev_copy_rows(x_local, buf, 1, x_local.shape[0] * n_row, 0, 0, 0, 0)
+        n_el = x_local.shape[0] * n_row
+        _dev_copy_rows(x_local, buf, 1, n_el, n_el, n_el, 0, 0)
     dev = buf.device
     if buf.is_cuda and _host_backend(group):
         buf = buf.cpu()  # gloo host staging
@@ -236,6 +237,8 @@ def _dev_copy_rows(src, dst, rows, n, lds, ldd, src_off, dst_off, accumulate=0):
     """dst[dst_off + r ldd + i] (+)= src[src_off + r lds + i], r < rows, i < n (element offsets)."""
     if rows == 0 or n == 0:
         return dst
+    if lds < 0 or ldd < n:  # pxa_copy2d's argument contract, checked on the gloo CPU path too
+        raise ValueError(f"copy rows: lds={lds}, ldd={ldd} for rows of {n}")
     if src.is_cuda:
         from pyxu_amd import _dev
 

@@ -1,7 +1,7 @@
 # usage: bash scripts/gpu_r03.sh <tag> [quick|noprof]
 # One GPU call of round 3: the PGD mode parity tests first, then the whole -m gpu suite, smoke, the
 # default bench line (N=1, every sub-record), rocprofv3 kernel trace / stats of the headline, SQ counter
-# passes and FETCH / WRITE traffic of the y-state pgd_tv2d_kernel at 2048^2, 4096^2 and C5.  Test failures
+# passes and FETCH / WRITE traffic of pgd_tv2d_kernel at 2048^2, 4096^2 and C5.  Test failures
 # (rc 1) do not stop the run; any other failure (fault, abort, timeout) ends it there.
 set -o pipefail
 T=${1:-r03}
@@ -37,7 +37,7 @@ step write4k 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/write4k -o run 
 B5="python3 bench.py --only c5 --c5-steps 10 --c5-warmup 2"
 step fetchc5 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetchc5 -o run --output-format csv -- $B5
 step writec5 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writec5 -o run --output-format csv -- $B5
-K="pgd_tv2d_kernel<float, 6, 2>"
+K="pgd_tv2d_kernel<float, 6>"
 python3 scripts/pmc_traffic.py $P/fetch $P/write "$K" pgd_tv2d_kernel@2048x2048 $P/traffic.json $T
 python3 scripts/pmc_traffic.py $P/fetch4k $P/write4k "$K" pgd_tv2d_kernel@4096x4096 $P/traffic.json $T
 python3 scripts/pmc_traffic.py $P/fetchc5 $P/writec5 "$K" pgd_tv2d_kernel@512x512x512 $P/traffic.json $T

@@ -1,7 +1,9 @@
-"""A/B probe of the fused PGD launch (pxa_pgd_tv2d_step) under PXA_TUNE_PGD_STAGGER start-delay settings, at 2048^2 / 4096^2 fp32 (Gaussian sigma=2, TV, PositiveOrthant).
-Each configuration is timed as windows of 50 back-to-back launches between two HIP events (the bench's
+"""A/B probe of the fused PGD launch (pxa_pgd_tv2d_step): the tile kernel (PXA_TUNE_PGD_KERNEL = 1) against
+the pipelined producer / consumer kernel (= 2), fp32, Gaussian sigma=2 (R = 6), TV, PositiveOrthant, at
+n x n images (`stack` images of n x n with per-image data when given as n:stack).
+Each configuration is timed as windows of back-to-back launches between two HIP events (the bench's
 LaunchTimer convention), the configurations interleaved over 5 rounds; prints the median per launch.
-usage: python scripts/pgd_modes_probe.py [n ...]"""
+usage: python scripts/pgd_modes_probe.py [n[:stack] ...]"""
 import sys
 
 import numpy as np
@@ -15,45 +17,51 @@ k = gaussian_kernel1d(2.0, 0, 6)
 T = (list(range(-6, 7)), [float(v) for v in k])
 
 
-def setup(n):
+def setup(n, stack):
     g = torch.Generator(device="cuda").manual_seed(0)
-    a = {name: torch.rand((n, n), device="cuda", generator=g) for name in ("x", "xp", "y", "b")}
-    a.update(out=torch.empty_like(a["x"]), yn=torch.empty_like(a["x"]))
-    return a, _dev.pgd_tv2d_args(1, 1, n, n, T, T, 1.0, 1.0, 0.01, 0.01, 1, 0.0)
+    a = {name: torch.rand((stack, n, n), device="cuda", generator=g) for name in ("x", "xp", "b")}
+    a["out"] = torch.empty_like(a["x"])
+    return a, _dev.pgd_tv2d_args(stack, stack, n, n, T, T, 1.0, 1.0, 0.01, 0.01, 1, 0.0)
 
 
-def launch(a, pre, mode):
+def launch(a, pre):
     _dev.lib.pxa_pgd_tv2d_step(0, *pre, 0.3, 0.5, 1, 0.0, a["x"].data_ptr(), a["xp"].data_ptr(), a["b"].data_ptr(),
                                a["out"].data_ptr(), None, _dev.stream())
 
 
-def window(a, pre, mode, stagger, n_launch=50):
-    _dev.tuning(_dev.TUNE_PGD_STAGGER, stagger)
+def window(a, pre, kern, n_launch):
+    prev = _dev.tuning(_dev.TUNE_PGD_KERNEL, kern)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(n_launch):
-        launch(a, pre, mode)
+        launch(a, pre)
     e1.record()
     e1.synchronize()
-    _dev.tuning(_dev.TUNE_PGD_STAGGER, 0)
+    _dev.tuning(_dev.TUNE_PGD_KERNEL, prev)
     return e0.elapsed_time(e1) * 1000.0 / n_launch
 
 
 def main():
-    sizes = [int(v) for v in sys.argv[1:]] or [2048, 4096]
-    confs = [("classic", 0)] + [("classic", (sel << 8) | nn) for sel in (4,) for nn in (4,)]
-    for n in sizes:
-        a, pre = setup(n)
-        for m, s in confs:
-            for _ in range(3):
-                window(a, pre, m, s)
-        res = {c: [] for c in confs}
+    sizes = sys.argv[1:] or ["2048", "4096", "512:512"]
+    for spec in sizes:
+        n, stack = (int(v) for v in (spec.split(":") + ["1"])[:2])
+        a, pre = setup(n, stack)
+        nl = max(5, int(2e6 / (n * n * stack) * 50) if n * n * stack < 2e7 else 10)
+        ref = None
+        outs = {}
+        for kern in (1, 2):
+            window(a, pre, kern, 3)
+            outs[kern] = a["out"].clone()
+        same = bool(torch.equal(outs[1], outs[2]))
+        res = {1: [], 2: []}
         for _ in range(5):
-            for m, s in confs:
-                res[(m, s)].append(window(a, pre, m, s))
-        for (m, s), v in res.items():
-            print(f"n={n} mode={m:8s} stagger=0x{s:04x}  {np.median(v):8.2f} us  (min {min(v):.2f})", flush=True)
-        del a
+            for kern in (1, 2):
+                res[kern].append(window(a, pre, kern, nl))
+        for kern, v in res.items():
+            name = {1: "tile", 2: "pipelined"}[kern]
+            print(f"n={n} stack={stack} kernel={name:9s} {np.median(v):9.2f} us  (min {min(v):.2f}, max {max(v):.2f})  "
+                  f"bit-identical={same}", flush=True)
+        del a, outs
 
 
 if __name__ == "__main__":
