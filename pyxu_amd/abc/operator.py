@@ -478,7 +478,7 @@ class QuadraticFunc(ProxDiffFunc):
         Q, c, _ = self._quad_spec()
         A = Q + HomothetyOp(cst=1 / tau, dim=Q.dim)
         b = _dev.div(arr, tau)
-        b = _dev.axpby(1.0, b, -1.0, c.grad(arr), out=b)
+        b = _dev.axpby(1.0, b, -1.0, self._c_grad(c, arr), out=b)
         slvr = CG(A=A, show_progress=False, _internal=True)
         sentinel = MaxIter(n=2 * A.dim)
         stop_crit = slvr.default_stop_crit() | sentinel
@@ -493,6 +493,18 @@ class QuadraticFunc(ProxDiffFunc):
     def estimate_diff_lipschitz(self, **kwargs):
         Q, *_ = self._quad_spec()
         return Q.estimate_lipschitz(**kwargs)
+
+    def _c_grad(self, c, arr):
+        """c.grad(arr) of the linear term: a constant vector (a linear functional's gradient does not depend on
+        where it is taken), evaluated once per (stack shape, dtype, device) and reused.  For a loss composed
+        with a dense K (ADMM's x-update, QuadraticFunc.prox -> CG) it costs two adjoint passes over K, which
+        the reference repeats on every prox call (operator.py:1257-1280)."""
+        key = (id(c), tuple(arr.shape[:-1]), arr.dtype, str(arr.device))
+        memo = self.__dict__.setdefault("_c_grad_memo", {})
+        hit = memo.get(key)
+        if hit is None or hit[0] is not c:  # (c is held by the entry, so its id cannot be reused meanwhile)
+            hit = memo[key] = (c, _dev.copy(c.grad(arr)))  # own buffer: callers only read it
+        return hit[1]
 
     def _quad_spec(self):
         return (self._Q, self._c, self._t)

@@ -111,7 +111,12 @@ __device__ inline void win_issue(const PgdParams<T>& p, int ty0, int tx0, const 
       if (!EDGE) {
         const unsigned off = (unsigned)(gr * n1 + gc);
         ld_vec<T, V>(xs + off, w.xv[k]);
-        ld_vec<T, V>(xps + off, w.pv[k]);
+        if (p.diag & 256) {  // timing probe only (WRONG results): one window array instead of two
+#pragma unroll
+          for (int v = 0; v < V; ++v) w.pv[k][v] = w.xv[k][v];
+        } else {
+          ld_vec<T, V>(xps + off, w.pv[k]);
+        }
       } else if (gr >= 0 && gr < n0 && p.vec_ok && gc >= 0 && gc + V <= n1) {
         ld_vec<T, V>(xs + (int64_t)gr * n1 + gc, w.xv[k]);
         ld_vec<T, V>(xps + (int64_t)gr * n1 + gc, w.pv[k]);
@@ -413,11 +418,16 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     if (tracing && (tid & 63) == 0) ts[(tid >> 6) * 8 + pt] = clock64();
   };
   tmark(0);
-  load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+  if (p.diag & 128) {  // timing probe only (WRONG results): no window loads, yk = 0
+    for (int i = tid; i < L::AR * L::AP; i += kThreads) A[i] = T(0);
+  } else {
+    load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+  }
   tmark(1);
   __syncthreads();
   tmark(2);
-  pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
+  const bool skip_passes = (p.diag & 64) != 0;  // timing probe only (WRONG results)
+  if (!skip_passes) pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
   tmark(3);
   __syncthreads();
   if (edge_cols) {
@@ -426,6 +436,14 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   }
   tmark(4);
   T st[KB][V][CW];
+  if (skip_passes) {
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+#pragma unroll
+      for (int u = 0; u < V; ++u)
+#pragma unroll
+        for (int w = 0; w < CW; ++w) st[k][u][w] = A[tid + u * 64 + w];
+  } else
   pass_b<T, R, EDGE>(p, A, PT, KT, GH, ty0, tx0, [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
 #pragma unroll
     for (int w = 0; w < CW; ++w) st[k][u][w] = g[w];
@@ -592,8 +610,18 @@ __device__ inline TileSeq tile_seq(unsigned ntiles, bool banded) {
   return {lo + j, nj, j < len ? (len - j + nj - 1) / nj : 0u};
 }
 
+// The kernel's first argument lives at offset 0 of the kernel-argument segment; the empty asm makes the
+// pointer opaque, so that loads through it are not treated as loop-invariant.
+template <typename P>
+__device__ inline const P& fresh_params(const P&) {
+  using KP = const __attribute__((address_space(4))) P;
+  KP* kp = (KP*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kp));
+  return *(const P*)kp;
+}
+
 template <int R>
-__global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> p, const float* __restrict__ x,
+__global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> p0, const float* __restrict__ x,
                                                              const float* __restrict__ xp, const float* __restrict__ b,
                                                              float* __restrict__ xn, double* __restrict__ partials,
                                                              int banded) {
@@ -603,6 +631,7 @@ __global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> 
   using C = PcCarve<T, R>;
   constexpr int V = L::V;
   constexpr int CW = L::CW;
+  const PgdParams<T>& p = p0;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   unsigned char* smem = smem_raw;
   T* PT = reinterpret_cast<T*>(smem + C::PT_OFF);
@@ -612,18 +641,27 @@ __global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> 
   const TileSeq seq = tile_seq(p.ntiles, banded != 0);
   if (seq.count == 0) return;  // (uniform over the workgroup)
   const int lt = threadIdx.x & (kThreads - 1);
+  // PXA_TUNE_PGD_DIAG bit 5: s_memtime stamps of the first wave of each role, iterations 0-3, of
+  // workgroups 0, 1, grid/2 and grid-1 (4 points per iteration: top, work done, past the first barrier(s),
+  // work done) -> g_tile_trace[slot][role][iteration][point]
+  const unsigned nb = gridDim.x, bid = blockIdx.x;
+  const int tslot = !(p.diag & 32) ? -1 : bid == 0 ? 0 : bid == 1 ? 1 : bid == nb / 2 ? 2 : bid == nb - 1 ? 3 : -1;
+  const int role = threadIdx.x >= kThreads ? 1 : 0;
+  auto tmark = [&](unsigned i, int pt) __attribute__((always_inline)) {
+    if (tslot >= 0 && i < 4 && (lt & 255) == 0) g_tile_trace[tslot * 32 + role * 16 + i * 4 + pt] = clock64();
+  };
   const bool want_part = partials != nullptr;
-  auto abuf = [&](unsigned i) { return reinterpret_cast<T*>(smem + (i & 1u) * C::A_BYTES); };
-  auto tile_of = [&](unsigned i) { return seq.first + i * seq.stride; };
+  auto abuf = [&](unsigned i) __attribute__((always_inline)) { return reinterpret_cast<T*>(smem + (i & 1u) * C::A_BYTES); };
+  auto tile_of = [&](unsigned i) __attribute__((always_inline)) { return seq.first + i * seq.stride; };
   if (threadIdx.x >= kThreads) {  // ---------------- producers (waves 4-7)
     Window<T, R> w;
     StagedB<T, R> hb;
-    auto issue = [&](unsigned i) {
+    auto issue = [&](unsigned i) __attribute__((always_inline)) {
       const TileRef t = tile_ref<T, R>(p, tile_of(i));
       if (t.interior) win_issue<T, R, false>(p, t.ty0, t.tx0, x + t.xoff, xp + t.xoff, w, lt);
       else win_issue<T, R, true>(p, t.ty0, t.tx0, x + t.xoff, xp + t.xoff, w, lt);
     };
-    auto stage_b = [&](unsigned i) {
+    auto stage_b = [&](unsigned i) __attribute__((always_inline)) {
       const TileRef t = tile_ref<T, R>(p, tile_of(i));
       if (t.interior) {
         load_staged<T, R, false>(p, t.ty0, t.tx0, b + t.boff, hb.v, lt);
@@ -633,7 +671,7 @@ __global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> 
         if (want_part) load_staged<T, R, true>(p, t.ty0, t.tx0, x + t.xoff, hb.x, lt);
       }
     };
-    auto epilogue = [&](unsigned i) {
+    auto epilogue = [&](unsigned i) __attribute__((always_inline)) {
       const unsigned tile = tile_of(i);
       const TileRef t = tile_ref<T, R>(p, tile);
       const T* A = abuf(i);
@@ -657,18 +695,23 @@ __global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> 
     win_store<T, R>(p, abuf(0), w, lt);
     if (seq.count > 1) issue(1);
     __syncthreads();  // B0: A[0] ready
+    const bool skip = (p.diag & 64) != 0;  // timing probe only (WRONG results): producers idle
     for (unsigned i = 0; i < seq.count; ++i) {
-      if (i >= 1) epilogue(i - 1);
-      stage_b(i);
+      tmark(i, 0);
+      if (i >= 1 && !skip) epilogue(i - 1);
+      if (!skip) stage_b(i);
+      tmark(i, 1);
       __syncthreads();  // B1
       if (tile_ref<T, R>(p, tile_of(i)).edge_cols) {
         ghost_cols_coop<T, R>(p.k1, PT, GH, tile_ref<T, R>(p, tile_of(i)).tx0, p.n1, threadIdx.x, kPcThreads);
         __syncthreads();  // B1'
       }
-      if (i + 1 < seq.count) {
+      tmark(i, 2);
+      if (i + 1 < seq.count && !skip) {
         win_store<T, R>(p, abuf(i + 1), w, lt);
         if (i + 2 < seq.count) issue(i + 2);
       }
+      tmark(i, 3);
       __syncthreads();  // B2
     }
     epilogue(seq.count - 1);
@@ -679,20 +722,30 @@ __global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> 
     }
     __syncthreads();  // B0
     for (unsigned i = 0; i < seq.count; ++i) {
+      // the launch parameters re-read from the kernel-argument segment in every iteration: hoisted out of
+      // the loop, the 2 x (4R + 1) G taps of both passes would stay live in SGPRs throughout and spill
+      const PgdParams<T>& p = fresh_params(p0);
       const TileRef t = tile_ref<T, R>(p, tile_of(i));
       const T* A = abuf(i);
-      if (t.interior) pass_a<T, R, false>(p, A, PT, KT, t.ty0, lt);
+      tmark(i, 0);
+      const bool cskip = (p.diag & 128) != 0;  // timing probe only (WRONG results): consumers idle
+      if (cskip) {
+      } else if (t.interior) pass_a<T, R, false>(p, A, PT, KT, t.ty0, lt);
       else pass_a<T, R, true>(p, A, PT, KT, t.ty0, lt);
+      tmark(i, 1);
       __syncthreads();  // B1
       if (t.edge_cols) {
         ghost_cols_coop<T, R>(p.k1, PT, GH, t.tx0, p.n1, threadIdx.x, kPcThreads);
         __syncthreads();  // B1'
       }
-      auto emit = [&](int, int, int gr, int gc, const T(&g)[CW], const T(&)[CW]) {
+      tmark(i, 2);
+      auto emit = [&](int, int, int gr, int gc, const T(&g)[CW], const T(&)[CW]) __attribute__((always_inline)) {
         *reinterpret_cast<float2*>(O + S::idx(gr - t.ty0, gc - t.tx0)) = make_float2(g[0], g[1]);
       };
-      if (t.interior) pass_b<T, R, false>(p, A, PT, KT, GH, t.ty0, t.tx0, emit, lt);
+      if (cskip) {
+      } else if (t.interior) pass_b<T, R, false>(p, A, PT, KT, GH, t.ty0, t.tx0, emit, lt);
       else pass_b<T, R, true>(p, A, PT, KT, GH, t.ty0, t.tx0, emit, lt);
+      tmark(i, 3);
       __syncthreads();  // B2
     }
   }

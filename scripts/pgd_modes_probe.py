@@ -29,8 +29,9 @@ def launch(a, pre):
                                a["out"].data_ptr(), None, _dev.stream())
 
 
-def window(a, pre, kern, n_launch):
+def window(a, pre, kern, n_launch, diag=0):
     prev = _dev.tuning(_dev.TUNE_PGD_KERNEL, kern)
+    pd = _dev.tuning(_dev.TUNE_PGD_DIAG, diag)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(n_launch):
@@ -38,10 +39,32 @@ def window(a, pre, kern, n_launch):
     e1.record()
     e1.synchronize()
     _dev.tuning(_dev.TUNE_PGD_KERNEL, prev)
+    _dev.tuning(_dev.TUNE_PGD_DIAG, pd)
     return e0.elapsed_time(e1) * 1000.0 / n_launch
 
 
+def diag_probe(sizes):
+    """tile kernel with its passes skipped (64) / its window loads skipped (128): WRONG results, timing only"""
+    for spec in sizes:
+        n, stack = (int(v) for v in (spec.split(":") + ["1"])[:2])
+        a, pre = setup(n, stack)
+        nl = max(5, int(2e6 / (n * n * stack) * 50) if n * n * stack < 2e7 else 10)
+        res = {d: [] for d in (0, 64, 128, 192, 256, 320)}
+        for d in res:
+            window(a, pre, 1, 3, d)
+        for _ in range(5):
+            for d in res:
+                res[d].append(window(a, pre, 1, nl, d))
+        for d, v in res.items():
+            lab = {0: "full", 64: "no passes", 128: "no window loads", 192: "neither", 256: "x window only",
+                   320: "x window, no passes"}[d]
+            print(f"n={n} stack={stack} tile kernel {lab:16s} {np.median(v):9.2f} us", flush=True)
+        del a
+
+
 def main():
+    if sys.argv[1:2] == ["diag"]:
+        return diag_probe(sys.argv[2:] or ["2048", "4096", "512:512"])
     sizes = sys.argv[1:] or ["2048", "4096", "512:512"]
     for spec in sizes:
         n, stack = (int(v) for v in (spec.split(":") + ["1"])[:2])
