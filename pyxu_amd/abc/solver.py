@@ -327,6 +327,7 @@ class Solver:
                 h.setFormatter(fmt)
                 logger.addHandler(h)
             logger.propagate = False
+            logger._pxa_direct = list(handlers)  # the record log lines may bypass LogRecord (_log_lines)
             return logger
 
         self._mstate.clear()
@@ -388,6 +389,7 @@ class Solver:
             ast["idx"] -= 1
             self._spec_rollback(token)
             with ast["lock"]:
+                self._flush_records()
                 self._record(idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, log_on)
             if log_on:
                 ast["logger"].info(f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
@@ -408,7 +410,7 @@ class Solver:
         _mw = (ast["wb_rate"] is not None) and (idx % ast["wb_rate"] == 0)
 
         log_on = not ast.get("internal")
-        if ast["pending"] and (_ms or _ml or _mw or idx - ast["pending"][0][0] >= self._RECORD_LAG):
+        if ast["pending"] and (_mw or idx - ast["pending"][0][0] >= self._RECORD_LAG):
             self._flush_records()
 
         try:
@@ -418,6 +420,7 @@ class Solver:
                 return self._step_speculative(idx, _ml, log_on)
             if _ms and ast["stop_crit"].stop(self._mstate):
                 with ast["lock"]:
+                    self._flush_records()
                     self._record(idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, log_on)
                 if log_on:
                     ast["logger"].info(f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
@@ -465,37 +468,81 @@ class Solver:
             ast["exception"] = e
             return False
 
-    _RECORD_LAG = 8  # steps between an iteration and the write of its deferred history record / log line
+    # steps between an iteration and the write of its deferred history record / log line: records and log
+    # lines are written in batches (one structured array and one file write per batch), also at stop_rate 1
+    _RECORD_LAG = 32
 
     def _record(self, it, data, stamp, ftype, log):
         """Append the history record of iteration `it` (stop-criterion info `data`, None = no record) and
         write its log line (solver.py:604-624)."""
+        self._record_batch([(it, data, stamp, ftype, log)])
+
+    def _record_batch(self, items):
+        """_record() for a run of deferred records, in order: consecutive records of one layout become one
+        structured array (the history is a list of arrays that stats() concatenates), and their log lines
+        are written with one call per handler (same text as one logger.info() per record)."""
         ast = self._astate
-        if data is not None:
-            key = (ftype, tuple(data))
-            cache = ast.setdefault("_hist_dtype", {})
-            dtype = cache.get(key)
-            if dtype is None:
-                dtype = cache[key] = np.dtype([("iteration", np.int64)] + [(k, ftype) for k in data])
-            rec = np.zeros(1, dtype=dtype)
-            rec["iteration"] = it
-            for k, v in data.items():
-                rec[k] = v
-            ast["history"].append(rec)
-        if log:
-            h = ast["history"][-1][0]
-            lines = [f"[{stamp}] Iteration {it:>_d}"]
-            for field, value in zip(h.dtype.names, h):
-                lines.append(f"\t{field}: {value}")
-            ast["logger"].info("\n".join(lines))
+        cache = ast.setdefault("_hist_dtype", {})
+        hist = ast["history"]
+        msgs = []
+        run, run_dtype = [], None
+
+        def close_run():
+            if run:
+                try:
+                    arr = np.array(run, dtype=run_dtype)
+                except (TypeError, ValueError):  # non-scalar info() values: field by field, as numpy assigns them
+                    arr = np.zeros(len(run), dtype=run_dtype)
+                    for i, r in enumerate(run):
+                        for name, v in zip(run_dtype.names, r):
+                            arr[i][name] = v
+                hist.append(arr)
+                run.clear()
+
+        for it, data, stamp, ftype, log in items:
+            if data is not None:
+                key = (ftype, tuple(data))
+                dtype = cache.get(key)
+                if dtype is None:
+                    dtype = cache[key] = np.dtype([("iteration", np.int64)] + [(k, ftype) for k in data])
+                if dtype is not run_dtype:
+                    close_run()
+                    run_dtype = dtype
+                run.append((it, *data.values()))
+            if log:
+                close_run()
+                h = hist[-1][-1]
+                lines = [f"[{stamp}] Iteration {it:>_d}"]
+                for field, value in zip(h.dtype.names, h):
+                    lines.append(f"\t{field}: {value}")
+                msgs.append("\n".join(lines))
+        close_run()
+        if msgs:
+            self._log_lines(msgs)
+
+    def _log_lines(self, msgs):
+        """logger.info(m) for each m: the solver's own handlers (``{levelname} -- {message}``, _init_logger) get
+        the formatted text in one write per batch; any other logger goes through logging."""
+        logger = self._astate["logger"]
+        handlers = getattr(logger, "_pxa_direct", None)
+        if handlers is None or handlers != logger.handlers or not logger.isEnabledFor(logging.INFO):
+            for m in msgs:
+                logger.info(m)
+            return
+        text = "".join(f"INFO -- {m}\n" for m in msgs)
+        for h in handlers:
+            with h.lock:
+                if h.stream is None and isinstance(h, logging.FileHandler):
+                    h.stream = h._open()
+                h.stream.write(text)
+                h.flush()
 
     def _flush_records(self):
         ast = self._astate
         if ast.get("pending"):
             with ast["lock"]:
                 items, ast["pending"] = ast["pending"], []
-                for e in items:
-                    self._record(*e)
+                self._record_batch(items)
 
     def _cleanup_logger(self):
         logger = logging.getLogger(str(self.workdir))

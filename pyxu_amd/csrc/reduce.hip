@@ -164,22 +164,31 @@ int launch_relerr(int64_t rows, int64_t n, const void* x, const void* p, void* x
   return last_launch_status();
 }
 
-// Fold of the fused PGD kernel's per-tile RelError partials (pgd_tv2d.hip: tile t wrote
+// Fold of the fused PGD kernel's per-(tile, wavefront) RelError partials (pgd_tv2d.hip: slot t wrote
 // part[2 t] = sum (x_new - x)^2 and part[2 t + 1] = sum x^2) into out[0][r] / out[1][r] for each stack row
-// r owning tiles [r per_row, (r + 1) per_row): one wavefront per (statistic, row), lane-strided sums in
-// a fixed order + the wave fold, so the result is deterministic run to run.
+// r owning slots [r per_row, (r + 1) per_row): one 256-thread workgroup per (statistic, row), thread-strided
+// sums with independent loads in flight, then the wave folds and a fixed-order sum of the 4 wave results, so
+// the result is deterministic run to run.  (One wavefront per pair was latency-bound: 33 us for the 8 192
+// slots of a 2048^2 image, every load a dependent round trip.)
 __global__ void __launch_bounds__(kBlock) tile_partials_fold_kernel(int64_t rows, int64_t per_row,
                                                                     const double* __restrict__ part,
                                                                     double* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // q = stat * rows + row
-  if (q >= 2 * rows) return;
+  __shared__ double red[kBlock / kWave];
+  const int64_t q = blockIdx.x;  // q = stat * rows + row
   const int64_t stat = q / rows, r = q - stat * rows;
   const double* pr = part + 2 * r * per_row + stat;
   double acc = 0.0;
-  for (int64_t k = lane; k < per_row; k += 64) acc += pr[2 * k];
+#pragma unroll 8
+  for (int64_t k = threadIdx.x; k < per_row; k += kBlock) acc += pr[2 * k];
   acc = wave_reduce<PXA_RED_SUMSQ>(acc);
-  if (lane == 0) out[q] = acc;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < kBlock / kWave; ++i) t += red[i];
+    out[q] = t;
+  }
 }
 
 // General Ln row statistic for the stop criteria (stop.py:222-297 -> pxlg.norm(ord=p)):
@@ -277,10 +286,9 @@ int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, co
 
 int pxa_tile_partials_fold(int64_t rows, int64_t per_row, const double* partials, double* out, void* stream) {
   PXA_CHECK_ARG(rows >= 1 && per_row >= 1 && partials != nullptr && out != nullptr);
-  const int64_t waves = 2 * rows, per_block = kBlock / kWave;
-  PXA_CHECK_ARG((waves + per_block - 1) / per_block <= 0x7fffffff);
-  hipLaunchKernelGGL(tile_partials_fold_kernel, dim3((unsigned)((waves + per_block - 1) / per_block)), dim3(kBlock), 0,
-                     as_stream(stream), rows, per_row, partials, out);
+  PXA_CHECK_ARG(2 * rows <= 0x7fffffff);
+  hipLaunchKernelGGL(tile_partials_fold_kernel, dim3((unsigned)(2 * rows)), dim3(kBlock), 0, as_stream(stream), rows,
+                     per_row, partials, out);
   return last_launch_status();
 }
 

@@ -258,6 +258,12 @@ class RelError(pxa.StoppingCriterion):
         return h
 
     def _decide(self, st, shape):
+        if st.shape[-1] == 1:  # one row: the same decision and value in host floats (no numpy temporaries)
+            n, d = float(st[0, 0]), float(st[1, 0])
+            decision = n <= self._eps * d
+            v = n / d if d != 0 else (np.inf if n > 0 else 0.0)
+            self._val = np.reshape(np.float64(0.0 if v != v else v), (*shape, 1))
+            return bool(decision)
         num = st[0].reshape(*shape, 1)
         den = st[1].reshape(*shape, 1)
         rule = np.all if self._satisfy_all else np.any
