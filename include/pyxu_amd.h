@@ -48,11 +48,12 @@ extern "C" {
 #define PXA_MODE_EDGE 4
 
 /* Kernel-selection knobs (pxa_tuning). */
-#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step: 0 default, 1 the tile kernel, 2 the pipelined producer /
-                                 consumer kernel (fp32, blur radius <= 6; else the tile kernel) */
+#define PXA_TUNE_PGD_KERNEL 0 /* reserved (kernel variants measured slower were removed; 0 = the tile kernel) */
 #define PXA_TUNE_NORMAL_DIAG 1 /* pxa_dense_normal timing probes (WRONG results, measurement only): 0 off,
                                   1 no x loads, 2 no cross-wave reduction, 3 no LDS accumulator */
-#define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel: bit 5 s_memtime phase trace (pxa_pgd_tile_trace) */
+#define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel: bit 5 s_memtime phase trace (pxa_pgd_tile_trace); timing
+                              probes with WRONG results: bit 6 skips passes A / B, bit 7 the window loads, bit 8
+                              loads x only (scripts/pgd_modes_probe.py diag) */
 #define PXA_TUNE_PGD_STAGGER 6 /* fused PGD tile kernel A/B probe: v = (sel << 8) | n delays the workgroups
                                   picked by `sel` in the first dispatch round by n x 1024 cycles (s_sleep) */
 #define PXA_TUNE_PDS_EVENTS 5 /* measurement hook: > 0 makes pxa_pds_step record HIP events around each
@@ -383,8 +384,8 @@ int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int6
  * alias x or x_prev.  If `partials` is not NULL, each (tile, wavefront) slot writes (sum (x_new-x)^2,
  * sum x^2) for RelError into partials[2*slot..] (double) — pxa_pgd_tv2d_partials_count() gives the
  * number of slots (tiles x 4; the slots of one image are contiguous).  prox codes: 0 none, 1 positive
- * orthant, 2 l1 with weight prox_w.  pxa_pgd_tv2d_last_kernel() is the kernel the calling thread
- * launched last: 1 the tile kernel, 2 the pipelined kernel (0 before any launch).
+ * orthant, 2 l1 with weight prox_w.  pxa_pgd_tv2d_last_kernel() is 1 once the calling thread has
+ * launched the tile kernel (0 before).
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
 int pxa_pgd_tv2d_last_kernel(void);

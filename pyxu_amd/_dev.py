@@ -163,7 +163,6 @@ def storage_exclusive(t) -> bool:
     return _USE_COUNT(t.untyped_storage()._cdata) <= 2
 
 
-TUNE_PGD_KERNEL = 0  # PXA_TUNE_PGD_KERNEL: 0 default, 1 tile kernel, 2 pipelined kernel (fp32, R <= 6)
 TUNE_NORMAL_DIAG = 1  # PXA_TUNE_NORMAL_DIAG: pxa_dense_normal timing probes (wrong results)
 TUNE_PGD_DIAG = 3  # PXA_TUNE_PGD_DIAG: bit 5 = s_memtime phase trace of the PGD tile kernel
 TUNE_PGD_STAGGER = 6  # PXA_TUNE_PGD_STAGGER: (sel << 8) | n, delayed first-round workgroups (A/B probe)

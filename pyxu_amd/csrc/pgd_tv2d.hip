@@ -539,257 +539,6 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
     pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
 }
 
-// =====================================================================================================
-// Pipelined form (fp32): the same per-tile arithmetic as pgd_tv2d_kernel (bit-identical x_new), with the
-// window traffic of tile i+1 in flight while tile i computes.
-//
-// The tile kernel serialises per workgroup: window load -> pass A -> pass B -> epilogue, and at 2048^2
-// its 2 048 workgroups run as two synchronous rounds of 1 024 (4 per CU): the whole chip loads, then the
-// whole chip computes (phase trace: ~10 k of 23.5 k cycles per tile in the window load; SQ_WAIT_ANY 42 %).
-// Here 2 persistent workgroups of 2 x 256 threads per CU walk a static list of tiles (XCD-banded) with two
-// roles, wave-uniform:
-//   consumers (waves 0-3): pass A (A[i] -> PT) | barrier | pass B (PT, A[i] -> O) | barrier
-//   producers (waves 4-7): epilogue of tile i-1 (O, A[i-1], H^T y -> x_new, RelError partials) and the
-//                          H^T y / x loads of tile i | barrier | yk of tile i+1 from registers loaded one
-//                          tile earlier -> A[i+1], then the loads of tile i+2's window | barrier
-// A is double-buffered and O has its own region, so one tile costs two barriers (three on edge-column
-// tiles: the cooperative ghost terms between pass A and pass B are computed by all 512 threads).  The
-// loads of tile i+2's x / x_prev window are issued at the end of tile i and consumed one whole tile later.
-// LDS: 2 A windows + PT + O + taps + ghost terms = 65 KB at R = 6 (two workgroups per CU); 128 VGPRs.
-constexpr int kPcThreads = 2 * kThreads;
-
-template <typename T, int R>
-struct PcCarve {
-  using L = Layout<T, R>;
-  static constexpr size_t A_BYTES = ((size_t)L::AR * L::AP * sizeof(T) + 15) / 16 * 16;
-  static constexpr size_t PT_OFF = 2 * A_BYTES;
-  static constexpr size_t O_OFF = PT_OFF + ((size_t)L::AC * L::PTP * sizeof(T) + 15) / 16 * 16;
-  static constexpr size_t KT_OFF = O_OFF + (size_t)TY * Stage<T, R>::OP * sizeof(T);
-  static constexpr size_t GH_OFF = KT_OFF + ((size_t)2 * kKT * sizeof(T) + 15) / 16 * 16;
-  static constexpr size_t BYTES = GH_OFF + kGhBytes<T, R>;
-};
-
-// geometry of one tile (the tile kernel's decode)
-struct TileRef {
-  int ty0, tx0;
-  int64_t xoff, boff;  // element offsets of the tile's image in x / x_prev / x_new and in H^T y
-  bool interior, edge_cols;
-};
-
-template <typename T, int R>
-__device__ inline TileRef tile_ref(const PgdParams<T>& p, unsigned tile) {
-  using L = Layout<T, R>;
-  const unsigned tpi = (unsigned)p.tiles0 * (unsigned)p.tiles1;
-  const unsigned s = tile / tpi;
-  const unsigned tr = tile - s * tpi;
-  const unsigned trow = tr / (unsigned)p.tiles1;
-  TileRef t;
-  t.ty0 = (int)trow * TY;
-  t.tx0 = (int)(tr - trow * (unsigned)p.tiles1) * TX;
-  const int64_t img = (int64_t)p.n0 * p.n1;
-  t.xoff = (int64_t)s * img;
-  t.boff = (int64_t)(s % (unsigned)p.y_images) * img;
-  t.interior = p.vec_ok && img <= 0x7fffffff && t.ty0 - 2 * R >= 0 && t.ty0 + TY + 2 * R <= p.n0 &&
-               t.tx0 - L::CA >= 0 && t.tx0 + TX + L::CA <= p.n1;
-  t.edge_cols = !t.interior && (t.tx0 < R || t.tx0 + TX > p.n1 - R);
-  return t;
-}
-
-// This workgroup's tiles: first, first + stride, ... (count of them).  banded: XCD g = blockIdx % 8 walks
-// its own contiguous band of tiles (the tile kernel's xcd_tile partition; needs gridDim % 8 == 0).
-struct TileSeq {
-  unsigned first, stride, count;
-};
-
-__device__ inline TileSeq tile_seq(unsigned ntiles, bool banded) {
-  const unsigned G = gridDim.x, b = blockIdx.x;
-  if (!banded) return {b, G, b < ntiles ? (ntiles - b + G - 1) / G : 0u};
-  const unsigned g = b & 7u, j = b >> 3, nj = (G - g + 7u) >> 3;
-  const unsigned q8 = ntiles >> 3, r8 = ntiles & 7u;
-  const unsigned lo = g * q8 + (g < r8 ? g : r8), len = q8 + (g < r8 ? 1u : 0u);
-  return {lo + j, nj, j < len ? (len - j + nj - 1) / nj : 0u};
-}
-
-// The kernel's first argument lives at offset 0 of the kernel-argument segment; the empty asm makes the
-// pointer opaque, so that loads through it are not treated as loop-invariant.
-template <typename P>
-__device__ inline const P& fresh_params(const P&) {
-  using KP = const __attribute__((address_space(4))) P;
-  KP* kp = (KP*)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(kp));
-  return *(const P*)kp;
-}
-
-template <int R>
-__global__ void __launch_bounds__(kPcThreads, 4) pgd_pc_kernel(PgdParams<float> p0, const float* __restrict__ x,
-                                                             const float* __restrict__ xp, const float* __restrict__ b,
-                                                             float* __restrict__ xn, double* __restrict__ partials,
-                                                             int banded) {
-  using T = float;
-  using L = Layout<T, R>;
-  using S = Stage<T, R>;
-  using C = PcCarve<T, R>;
-  constexpr int V = L::V;
-  constexpr int CW = L::CW;
-  const PgdParams<T>& p = p0;
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  unsigned char* smem = smem_raw;
-  T* PT = reinterpret_cast<T*>(smem + C::PT_OFF);
-  T* O = reinterpret_cast<T*>(smem + C::O_OFF);
-  T* KT = reinterpret_cast<T*>(smem + C::KT_OFF);
-  T* GH = reinterpret_cast<T*>(smem + C::GH_OFF);
-  const TileSeq seq = tile_seq(p.ntiles, banded != 0);
-  if (seq.count == 0) return;  // (uniform over the workgroup)
-  const int lt = threadIdx.x & (kThreads - 1);
-  // PXA_TUNE_PGD_DIAG bit 5: s_memtime stamps of the first wave of each role, iterations 0-3, of
-  // workgroups 0, 1, grid/2 and grid-1 (4 points per iteration: top, work done, past the first barrier(s),
-  // work done) -> g_tile_trace[slot][role][iteration][point]
-  const unsigned nb = gridDim.x, bid = blockIdx.x;
-  const int tslot = !(p.diag & 32) ? -1 : bid == 0 ? 0 : bid == 1 ? 1 : bid == nb / 2 ? 2 : bid == nb - 1 ? 3 : -1;
-  const int role = threadIdx.x >= kThreads ? 1 : 0;
-  auto tmark = [&](unsigned i, int pt) __attribute__((always_inline)) {
-    if (tslot >= 0 && i < 4 && (lt & 255) == 0) g_tile_trace[tslot * 32 + role * 16 + i * 4 + pt] = clock64();
-  };
-  const bool want_part = partials != nullptr;
-  auto abuf = [&](unsigned i) __attribute__((always_inline)) { return reinterpret_cast<T*>(smem + (i & 1u) * C::A_BYTES); };
-  auto tile_of = [&](unsigned i) __attribute__((always_inline)) { return seq.first + i * seq.stride; };
-  if (threadIdx.x >= kThreads) {  // ---------------- producers (waves 4-7)
-    Window<T, R> w;
-    StagedB<T, R> hb;
-    auto issue = [&](unsigned i) __attribute__((always_inline)) {
-      const TileRef t = tile_ref<T, R>(p, tile_of(i));
-      if (t.interior) win_issue<T, R, false>(p, t.ty0, t.tx0, x + t.xoff, xp + t.xoff, w, lt);
-      else win_issue<T, R, true>(p, t.ty0, t.tx0, x + t.xoff, xp + t.xoff, w, lt);
-    };
-    auto stage_b = [&](unsigned i) __attribute__((always_inline)) {
-      const TileRef t = tile_ref<T, R>(p, tile_of(i));
-      if (t.interior) {
-        load_staged<T, R, false>(p, t.ty0, t.tx0, b + t.boff, hb.v, lt);
-        if (want_part) load_staged<T, R, false>(p, t.ty0, t.tx0, x + t.xoff, hb.x, lt);
-      } else {
-        load_staged<T, R, true>(p, t.ty0, t.tx0, b + t.boff, hb.v, lt);
-        if (want_part) load_staged<T, R, true>(p, t.ty0, t.tx0, x + t.xoff, hb.x, lt);
-      }
-    };
-    auto epilogue = [&](unsigned i) __attribute__((always_inline)) {
-      const unsigned tile = tile_of(i);
-      const TileRef t = tile_ref<T, R>(p, tile);
-      const T* A = abuf(i);
-      double part_d = 0.0, part_x = 0.0;
-      int r0, cq;
-      S::lane(lt, r0, cq);
-#pragma unroll
-      for (int s = 0; s < StagedB<T, R>::NS; ++s) {
-        const int r = r0 + s * S::RPS;
-        T g[V], y[V];
-        ld_vec<T, V>(O + S::idx(r, V * cq), g);
-        ld_vec<T, V>(A + (r + 2 * R) * L::AP + L::CA + V * cq, y);
-        if (t.interior)
-          finish_vec<T, false>(p, t.ty0 + r, t.tx0 + V * cq, g, hb.v[s], y, hb.x[s], xn + t.xoff, want_part, part_d, part_x);
-        else
-          finish_vec<T, true>(p, t.ty0 + r, t.tx0 + V * cq, g, hb.v[s], y, hb.x[s], xn + t.xoff, want_part, part_d, part_x);
-      }
-      if (want_part) wave_partials(part_d, part_x, partials, tile * kPartWaves + (lt >> 6));
-    };
-    issue(0);
-    win_store<T, R>(p, abuf(0), w, lt);
-    if (seq.count > 1) issue(1);
-    __syncthreads();  // B0: A[0] ready
-    const bool skip = (p.diag & 64) != 0;  // timing probe only (WRONG results): producers idle
-    for (unsigned i = 0; i < seq.count; ++i) {
-      tmark(i, 0);
-      if (i >= 1 && !skip) epilogue(i - 1);
-      if (!skip) stage_b(i);
-      tmark(i, 1);
-      __syncthreads();  // B1
-      if (tile_ref<T, R>(p, tile_of(i)).edge_cols) {
-        ghost_cols_coop<T, R>(p.k1, PT, GH, tile_ref<T, R>(p, tile_of(i)).tx0, p.n1, threadIdx.x, kPcThreads);
-        __syncthreads();  // B1'
-      }
-      tmark(i, 2);
-      if (i + 1 < seq.count && !skip) {
-        win_store<T, R>(p, abuf(i + 1), w, lt);
-        if (i + 2 < seq.count) issue(i + 2);
-      }
-      tmark(i, 3);
-      __syncthreads();  // B2
-    }
-    epilogue(seq.count - 1);
-  } else {  // ---------------------------------------- consumers (waves 0-3)
-    if (lt < 2 * R + 1) {
-      KT[lt] = p.k0[lt];
-      KT[kKT + lt] = p.k1[lt];
-    }
-    __syncthreads();  // B0
-    for (unsigned i = 0; i < seq.count; ++i) {
-      // the launch parameters re-read from the kernel-argument segment in every iteration: hoisted out of
-      // the loop, the 2 x (4R + 1) G taps of both passes would stay live in SGPRs throughout and spill
-      const PgdParams<T>& p = fresh_params(p0);
-      const TileRef t = tile_ref<T, R>(p, tile_of(i));
-      const T* A = abuf(i);
-      tmark(i, 0);
-      const bool cskip = (p.diag & 128) != 0;  // timing probe only (WRONG results): consumers idle
-      if (cskip) {
-      } else if (t.interior) pass_a<T, R, false>(p, A, PT, KT, t.ty0, lt);
-      else pass_a<T, R, true>(p, A, PT, KT, t.ty0, lt);
-      tmark(i, 1);
-      __syncthreads();  // B1
-      if (t.edge_cols) {
-        ghost_cols_coop<T, R>(p.k1, PT, GH, t.tx0, p.n1, threadIdx.x, kPcThreads);
-        __syncthreads();  // B1'
-      }
-      tmark(i, 2);
-      auto emit = [&](int, int, int gr, int gc, const T(&g)[CW], const T(&)[CW]) __attribute__((always_inline)) {
-        *reinterpret_cast<float2*>(O + S::idx(gr - t.ty0, gc - t.tx0)) = make_float2(g[0], g[1]);
-      };
-      if (cskip) {
-      } else if (t.interior) pass_b<T, R, false>(p, A, PT, KT, GH, t.ty0, t.tx0, emit, lt);
-      else pass_b<T, R, true>(p, A, PT, KT, GH, t.ty0, t.tx0, emit, lt);
-      tmark(i, 3);
-      __syncthreads();  // B2
-    }
-  }
-}
-
-// CUs of the current device (cached per device ordinal)
-inline int device_cus() {
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cache[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cache[dev] = n;
-  }
-  return cache[dev];
-}
-
-template <int R>
-int launch_pgd_pc(const PgdParams<float>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
-                  hipStream_t s) {
-  using C = PcCarve<float, R>;
-  static_assert(C::BYTES <= 80 * 1024, "two pipelined workgroups per CU");
-  auto kern = pgd_pc_kernel<R>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::BYTES);
-    attr_set = true;
-  }
-  unsigned grid;
-  int banded;
-  if (p.ntiles >= 8) {
-    const unsigned g2 = 2u * (unsigned)device_cus();
-    grid = (p.ntiles < g2 ? p.ntiles : g2) & ~7u;
-    banded = 1;
-  } else {
-    grid = p.ntiles;
-    banded = 0;
-  }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kPcThreads), C::BYTES, s, p, (const float*)x, (const float*)xp,
-                     (const float*)b, (float*)xn, partials, banded);
-  return last_launch_status();
-}
-
 template <typename T, int R>
 int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
                hipStream_t s) {
@@ -871,22 +620,6 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.stagger = tuning(PXA_TUNE_PGD_STAGGER);
   p.round1 = 4u * 256u;
   int st;
-  // kernel selection (PXA_TUNE_PGD_KERNEL: 0 default, 1 tile kernel, 2 pipelined kernel)
-  const int ksel = tuning(PXA_TUNE_PGD_KERNEL);
-  if constexpr (sizeof(T) == 4) {
-    if (ksel == 2 && R <= 6) {
-      switch (R) {
-        case 1: st = launch_pgd_pc<1>(p, x, x_prev, hty, x_new, partials, s); break;
-        case 2: st = launch_pgd_pc<2>(p, x, x_prev, hty, x_new, partials, s); break;
-        case 3: st = launch_pgd_pc<3>(p, x, x_prev, hty, x_new, partials, s); break;
-        case 4: st = launch_pgd_pc<4>(p, x, x_prev, hty, x_new, partials, s); break;
-        case 5: st = launch_pgd_pc<5>(p, x, x_prev, hty, x_new, partials, s); break;
-        default: st = launch_pgd_pc<6>(p, x, x_prev, hty, x_new, partials, s); break;
-      }
-      if (st == PXA_OK) g_last_pgd_kernel = 2;
-      return st;
-    }
-  }
   switch (R) {
     case 1: st = launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s); break;
     case 2: st = launch_pgd<T, 2>(p, x, x_prev, hty, x_new, partials, s); break;

@@ -1,9 +1,9 @@
-"""A/B probe of the fused PGD launch (pxa_pgd_tv2d_step): the tile kernel (PXA_TUNE_PGD_KERNEL = 1) against
-the pipelined producer / consumer kernel (= 2), fp32, Gaussian sigma=2 (R = 6), TV, PositiveOrthant, at
-n x n images (`stack` images of n x n with per-image data when given as n:stack).
-Each configuration is timed as windows of back-to-back launches between two HIP events (the bench's
-LaunchTimer convention), the configurations interleaved over 5 rounds; prints the median per launch.
-usage: python scripts/pgd_modes_probe.py [n[:stack] ...]"""
+"""Timing probe of the fused PGD launch (pxa_pgd_tv2d_step), fp32, Gaussian sigma=2 (R = 6), TV, PositiveOrthant,
+at n x n images (`stack` images of n x n with per-image data when given as n:stack): the tile kernel as it is and
+with parts of its work skipped (PXA_TUNE_PGD_DIAG bits 6-8: WRONG results, timing only), which prices the
+window loads, the passes and the rest.  Each configuration is timed as windows of back-to-back launches between
+two HIP events (the bench's LaunchTimer convention), interleaved over 5 rounds; prints the median per launch.
+usage: python scripts/pgd_modes_probe.py diag [n[:stack] ...]"""
 import sys
 
 import numpy as np
@@ -30,7 +30,6 @@ def launch(a, pre):
 
 
 def window(a, pre, kern, n_launch, diag=0):
-    prev = _dev.tuning(_dev.TUNE_PGD_KERNEL, kern)
     pd = _dev.tuning(_dev.TUNE_PGD_DIAG, diag)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -38,7 +37,6 @@ def window(a, pre, kern, n_launch, diag=0):
         launch(a, pre)
     e1.record()
     e1.synchronize()
-    _dev.tuning(_dev.TUNE_PGD_KERNEL, prev)
     _dev.tuning(_dev.TUNE_PGD_DIAG, pd)
     return e0.elapsed_time(e1) * 1000.0 / n_launch
 
@@ -63,28 +61,7 @@ def diag_probe(sizes):
 
 
 def main():
-    if sys.argv[1:2] == ["diag"]:
-        return diag_probe(sys.argv[2:] or ["2048", "4096", "512:512"])
-    sizes = sys.argv[1:] or ["2048", "4096", "512:512"]
-    for spec in sizes:
-        n, stack = (int(v) for v in (spec.split(":") + ["1"])[:2])
-        a, pre = setup(n, stack)
-        nl = max(5, int(2e6 / (n * n * stack) * 50) if n * n * stack < 2e7 else 10)
-        ref = None
-        outs = {}
-        for kern in (1, 2):
-            window(a, pre, kern, 3)
-            outs[kern] = a["out"].clone()
-        same = bool(torch.equal(outs[1], outs[2]))
-        res = {1: [], 2: []}
-        for _ in range(5):
-            for kern in (1, 2):
-                res[kern].append(window(a, pre, kern, nl))
-        for kern, v in res.items():
-            name = {1: "tile", 2: "pipelined"}[kern]
-            print(f"n={n} stack={stack} kernel={name:9s} {np.median(v):9.2f} us  (min {min(v):.2f}, max {max(v):.2f})  "
-                  f"bit-identical={same}", flush=True)
-        del a, outs
+    return diag_probe([v for v in sys.argv[1:] if v != "diag"] or ["2048", "4096", "512:512"])
 
 
 if __name__ == "__main__":

@@ -17,12 +17,12 @@ g = torch.Generator(device="cuda").manual_seed(0)
 x, xp, b = (torch.rand((n, n), device="cuda", generator=g) for _ in range(3))
 out = torch.empty_like(x)
 t = taps(sigma)
-prev = [(k, _dev.tuning(k, v)) for k, v in ((_dev.TUNE_PGD_KERNEL, 1), (3, 32))]
+prev = [(_dev.TUNE_PGD_DIAG, _dev.tuning(_dev.TUNE_PGD_DIAG, 32))]
 for _ in range(10):
     _dev.pgd_tv2d_step(x, xp, b, out, 1, 1, n, n, t, t, 1.0, 1.0, 0.02, 0.01, 0.3, 0.5, 1, 0.0)
 torch.cuda.synchronize()
 buf = np.zeros(128, dtype=np.uint64)
-assert lib.pxa_pgd_march_trace(buf.ctypes.data_as(ct.c_void_p), 128) == 0
+assert lib.pxa_pgd_tile_trace(buf.ctypes.data_as(ct.c_void_p), 128) == 0
 for k, v in prev:
     _dev.tuning(k, v)
 names = ["load", "B1", "passA", "B2(+ghost)", "passB", "stage O+B", "epilogue"]

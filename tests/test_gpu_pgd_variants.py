@@ -63,27 +63,14 @@ def _plan(sh, stack, y_images, sigma, g_kind, fused=True, **kw):
         return s
 
 
-def _launch(s, x, xp, hty, a, parts=None, kernel=1):
+def _launch(s, x, xp, hty, a, parts=None):
     p, m = s._plan, s._mstate
     out = _dev.empty_like(x)
     _dev.pgd_tv2d_step(x, xp, hty, out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
                        p["h1"], p["lam"], p["mu"], a, m["tau"], p["prox"], m["tau"] * p["prox_scale"], partials=parts,
                        pre=p["pre"])
-    assert int(lib.pxa_pgd_tv2d_last_kernel()) == kernel
+    assert int(lib.pxa_pgd_tv2d_last_kernel()) == 1
     return out
-
-
-class _kernel:
-    """Select the fused PGD kernel (PXA_TUNE_PGD_KERNEL) inside a with-block."""
-
-    def __init__(self, k):
-        self.k = k
-
-    def __enter__(self):
-        self.prev = _dev.tuning(_dev.TUNE_PGD_KERNEL, self.k)
-
-    def __exit__(self, *exc):
-        _dev.tuning(_dev.TUNE_PGD_KERNEL, self.prev)
 
 
 def _misaligned(t):
@@ -124,41 +111,13 @@ def test_vector_and_scalar_paths_bit_exact(case):
     m, p = s._mstate, s._plan
     x, xp, hty = m["x"], m["x_prev"], p["hty"]
     pa, pb = _parts(s), _parts(s)
-    with _kernel(1):
-        a = _launch(s, x, xp, hty, 0.37, pa)
-        b = _launch(s, _misaligned(x), _misaligned(xp), _misaligned(hty), 0.37, pb)
-        c = _launch(s, x, xp, hty, 0.37)
+    a = _launch(s, x, xp, hty, 0.37, pa)
+    b = _launch(s, _misaligned(x), _misaligned(xp), _misaligned(hty), 0.37, pb)
+    c = _launch(s, x, xp, hty, 0.37)
     torch.cuda.synchronize()
     assert np.array_equal(to_NUMPY(a), to_NUMPY(b))
     assert np.array_equal(to_NUMPY(a), to_NUMPY(c))
     assert np.array_equal(to_NUMPY(pa), to_NUMPY(pb)) and np.all(to_NUMPY(pa) >= 0)
-
-
-def _radius(sigma):
-    return max(1, int(3.0 * sigma + 0.5))
-
-
-@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}-sig{c[3]}-{c[4]}")
-def test_pipelined_kernel_matches_tile_kernel(case):
-    """The pipelined producer / consumer kernel (PXA_TUNE_PGD_KERNEL = 2) against the tile kernel: x_new
-    and the per-wave RelError partials bit for bit, aligned and misaligned, on every shape class (radii
-    above 6 run the tile kernel under either setting)."""
-    sh, stack, y_images, sigma, g_kind = case
-    s = _plan(sh, stack, y_images, sigma, g_kind)
-    m, p = s._mstate, s._plan
-    x, xp, hty = m["x"], m["x_prev"], p["hty"]
-    pc_kernel = 2 if _radius(sigma) <= 6 else 1
-    outs = {}
-    for k, want in ((1, 1), (2, pc_kernel)):
-        pa = _parts(s)
-        with _kernel(k):
-            a = _launch(s, x, xp, hty, 0.37, pa, kernel=want)
-            b = _launch(s, _misaligned(x), _misaligned(xp), _misaligned(hty), 0.37, kernel=want)
-        torch.cuda.synchronize()
-        outs[k] = (to_NUMPY(a), to_NUMPY(b), to_NUMPY(pa))
-    assert np.array_equal(outs[1][0], outs[2][0])
-    assert np.array_equal(outs[1][1], outs[2][1])
-    assert np.array_equal(outs[1][2], outs[2][2]) and np.all(outs[2][2] >= 0)
 
 
 @pytest.mark.parametrize("stack,rows", [(1, 1), (6, 3)])
