@@ -385,6 +385,12 @@ class Solver:
             self.m_step()
         except Exception as e:  # raised only if the check says continue (then the reference calls m_step)
             err = e
+        # the host would now wait for the decision while the device runs the previous step: write the oldest
+        # deferred history record / log line meanwhile (one per check, so records never pile up at stop_rate 1)
+        if ast["pending"]:
+            with ast["lock"]:
+                if ast["pending"]:
+                    self._record_batch([ast["pending"].pop(0)], flush=False)
         if resolve():
             ast["idx"] -= 1
             self._spec_rollback(token)
@@ -477,7 +483,7 @@ class Solver:
         write its log line (solver.py:604-624)."""
         self._record_batch([(it, data, stamp, ftype, log)])
 
-    def _record_batch(self, items):
+    def _record_batch(self, items, flush=True):
         """_record() for a run of deferred records, in order: consecutive records of one layout become one
         structured array (the history is a list of arrays that stats() concatenates), and their log lines
         are written with one call per handler (same text as one logger.info() per record)."""
@@ -518,11 +524,12 @@ class Solver:
                 msgs.append("\n".join(lines))
         close_run()
         if msgs:
-            self._log_lines(msgs)
+            self._log_lines(msgs, flush)
 
-    def _log_lines(self, msgs):
+    def _log_lines(self, msgs, flush=True):
         """logger.info(m) for each m: the solver's own handlers (``{levelname} -- {message}``, _init_logger) get
-        the formatted text in one write per batch; any other logger goes through logging."""
+        the formatted text in one write per batch (flushed unless `flush` is False: the next batch, stats() or
+        the end of the run flushes it); any other logger goes through logging."""
         logger = self._astate["logger"]
         handlers = getattr(logger, "_pxa_direct", None)
         if handlers is None or handlers != logger.handlers or not logger.isEnabledFor(logging.INFO):
@@ -535,7 +542,8 @@ class Solver:
                 if h.stream is None and isinstance(h, logging.FileHandler):
                     h.stream = h._open()
                 h.stream.write(text)
-                h.flush()
+                if flush:
+                    h.flush()
 
     def _flush_records(self):
         ast = self._astate
