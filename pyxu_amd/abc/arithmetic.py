@@ -623,7 +623,12 @@ class ChainRule(Rule):
                 return self._rhs.adjoint(self._lhs.prox(self._rhs.apply(arr), tau))
             if self._lhs.has(P.QUADRATIC) and self._rhs.has(P.LINEAR):
                 Q, c, t = self._quad_spec()
-                return pxo.QuadraticFunc(shape=self.shape, Q=Q, c=c, t=t).prox(arr, tau)
+                # one QuadraticFunc per (memoised) spec, so that its per-instance caches (the constant c.grad)
+                # survive across prox calls (ADMM calls this once per outer iteration)
+                qf = self.__dict__.get("_quad_prox_fn")
+                if qf is None or qf[0] is not Q or qf[1] is not c or qf[2] is not t:
+                    qf = self._quad_prox_fn = (Q, c, t, pxo.QuadraticFunc(shape=self.shape, Q=Q, c=c, t=t))
+                return qf[3].prox(arr, tau)
             if self._lhs.has(P.LINEAR) and self._rhs.has(P.PROXIMABLE):
                 return ScaleRule(op=self._rhs, cst=self._lhs_scalar()).op().prox(arr, tau)
             if P.LINEAR in (self._lhs.properties() & self._rhs.properties()):

@@ -87,7 +87,9 @@ class CG(pxa.Solver):
                 return _dev.copy2d(t, _dev.empty(big.shape, t), rows, n, 0, n)
 
             mst["b"], mst["x"] = bcast(b), bcast(x0)
-        self._apply = self._make_apply(mst["x"])
+        key = (tuple(mst["x"].shape), mst["x"].dtype, str(mst["x"].device))
+        if getattr(self, "_apply_key", None) != key:  # (the operator is fixed per solver: reuse across fits)
+            self._apply, self._apply_key = self._make_apply(mst["x"]), key
         if x0 is None:
             # x = 0: A x = 0 exactly, so r = b - A x = b bit for bit -- skip the product (one full pass over
             # the operator per solve; QuadraticFunc.prox, i.e. every ADMM x-update, starts from zero)
@@ -95,11 +97,18 @@ class CG(pxa.Solver):
         else:
             mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._apply(mst["x"]))
         mst["conjugate_dir"] = _dev.copy(mst["residual"])
-        self._rr = None  # ||r||^2 of the current residual, carried from the previous step's beta
-        self._Ap_next = None  # A p of the current p, launched ahead by the previous step (see m_step)
         self._rr_hist = []  # host ||r||^2 (max over rows) of the last steps: convergence-rate estimate
         self._abs_eps = self._stop_eps()
-        mst[_ROWSTAT] = {}
+        # ||r0||^2 with an async host copy, published for the first stop check (AbsError on the residual:
+        # the same reduction, so the same bits) and reused by the first step's alpha; a sub-solver then
+        # launches A p0 before that check, so the device works while the host decides
+        r = mst["residual"]
+        hr0 = _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)))
+        self._rr = (hr0, r)  # ||r||^2 of the current residual (then carried from the previous step's beta)
+        mst[_ROWSTAT] = {"residual": (r, 2, hr0)}
+        self._Ap_next = None  # A p of the current p, launched ahead of the stop check (see m_step)
+        if self._astate.get("internal"):
+            self._Ap_next = self._apply(mst["conjugate_dir"])
 
     def _make_apply(self, like):
         """A.apply, or -- when A = s K^T K + d I for one dense K (ADMM's QuadraticFunc.prox operator,
