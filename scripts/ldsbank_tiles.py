@@ -154,3 +154,81 @@ if __name__ == "__main__":
         report(Geo(TY, TX, NT, R), "generic maps")
     else:
         report(Geo(32, 64, 256, 6, pbi_current, Stage64()), "current tile kernel")
+
+
+# ----------------------------------------------------------------------------- 64 x 128 tile, 1024 threads
+_BQ = {0: 0, 3: 1, 5: 2, 6: 3, 1: 0, 2: 1, 4: 2, 7: 3}
+_GQ = {0: 0, 3: 0, 5: 0, 6: 0, 1: 1, 2: 1, 4: 1, 7: 1}
+
+
+def pa_big(it):
+    """pass A item -> (row group a, column group b): per wave 16 row groups x 4 column groups; inside each
+    ds_read_b128 lane group 4 consecutive row groups x 4 column groups distinct mod 4"""
+    w, l = it >> 6, it & 63
+    h, q, lo = l >> 5, (l >> 2) & 7, l & 3
+    return lo + 4 * (2 * h + _GQ[q]), _BQ[q] + 4 * w
+
+
+def pb_big(it):
+    """pass B item: the 32 x 64 tile kernel's map inside each quadrant (it >> 8)"""
+    qd, i = it >> 8, it & 255
+    a, cb = pbi_current(i)
+    return a + 8 * (qd >> 1), cb + 32 * (qd & 1)
+
+
+class StageBig:
+    """O = four 32 x 64 quadrants in the tile kernel's layout; epilogue lanes: the tile kernel's map per quadrant"""
+    RPS = 16
+
+    @staticmethod
+    def idx(r, c):
+        qd = (r // 32) * 2 + (c // 64)
+        return qd * 2048 + Stage64.idx(r % 32, c % 64)
+
+    @staticmethod
+    def lane(tid):
+        qd, t = tid >> 8, tid & 255
+        r0, cq = Stage64.lane(t)
+        return r0 + 32 * (qd >> 1), cq + 16 * (qd & 1)
+
+
+def audit_big(R=6):
+    g = Geo(64, 128, 1024, R, pb_big, None)
+    V = 4
+    res = {}
+
+    def rec(name, cost, ideal):
+        c, _ = res.get(name, (0, ideal))
+        res[name] = (max(c, cost), ideal)
+
+    for wv in waves(g.NA * 4 * 10, g.NT):  # pass A with pa_big (items beyond NB column groups idle)
+        ab = [None if it is None else pa_big(it) for it in wv]
+        ab = [None if (x is None or x[1] >= g.NB) else x for x in ab]
+        for j in range(V + 4 * R):
+            rec("passA A reads (read_b128)", cost_read_b128([None if x is None else (V * x[0] + j) * g.AP + V * x[1] for x in ab]), 4)
+        for v in range(V):
+            rec("passA PT stores (write_b128)", cost_write([None if x is None else (V * x[1] + v) * g.PTP + V * x[0] for x in ab], 4), 8)
+    for wv in waves(g.NPB, g.NT):
+        ab = [None if it is None else pb_big(it) for it in wv]
+        for j in range(2 + 4 * R):
+            rec("passB PT reads (read_b128)", cost_read_b128([None if x is None else (g.CA - 2 * R + 2 * x[1] + j) * g.PTP + V * x[0] for x in ab]), 4)
+        for r in range(V + 2):
+            for off in (-2, 0, 2):
+                rec("passB TV A reads (read_b64)", cost_read_b64([None if x is None else (V * x[0] - 1 + r + 2 * R) * g.AP + g.CA + 2 * x[1] + off for x in ab]), 2)
+        for u in range(V):
+            rec("O stores (write_b64)", cost_write([None if x is None else StageBig.idx(V * x[0] + u, 2 * x[1]) for x in ab], 2), 4)
+    for w in range(16):
+        lanes = [StageBig.lane(w * 64 + l) for l in range(64)]
+        for s in range(2):
+            rec("epilogue O reads (read_b128)", cost_read_b128([StageBig.idx(r0 + 16 * s, V * cq) for r0, cq in lanes]), 4)
+            rec("epilogue A reads (read_b128)", cost_read_b128([(r0 + 16 * s + 2 * R) * g.AP + g.CA + V * cq for r0, cq in lanes]), 4)
+    # coverage checks
+    itemsA = sorted(pa_big(it) for it in range(1024) if pa_big(it)[1] < g.NB)
+    assert itemsA == sorted((a, b) for a in range(g.NA) for b in range(g.NB)), "pass A map"
+    itemsB = sorted(pb_big(it) for it in range(1024))
+    assert itemsB == sorted((a, c) for a in range(g.NA) for c in range(g.NCB)), "pass B map"
+    pix = sorted((r0 + 16 * s, cq) for t in range(1024) for s in range(2) for r0, cq in [StageBig.lane(t)])
+    assert pix == sorted((r, c) for r in range(64) for c in range(32)), "epilogue map"
+    print(f"== big tile 64 x 128, 1024 threads, R={R}: AP={g.AP} PTP={g.PTP} LDS A={g.AR * g.AP * 4} PT={g.AC * g.PTP * 4}")
+    for k, (c, i) in res.items():
+        print(f"   {k:34s} worst {c:3d} cycles (conflict-free {i}){'' if c <= i else '  <-- conflicts'}")

@@ -60,6 +60,9 @@ def diag_probe(sizes):
         del a
 
 
+
+
+
 def main():
     return diag_probe([v for v in sys.argv[1:] if v != "diag"] or ["2048", "4096", "512:512"])
 
