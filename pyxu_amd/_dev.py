@@ -86,6 +86,22 @@ def stream():
     return ct.c_void_p(_RAW_STREAM())
 
 
+_TSTREAM = (None, None)  # (raw hipStream_t, torch stream object) of the last record_event
+
+
+def record_event(ev):
+    """ev.record() on torch's current stream, without torch.cuda.current_stream()'s Python device lookup on
+    every call (a few microseconds, paid once per solver step at stop_rate 1): the torch stream object is
+    cached per raw stream."""
+    global _TSTREAM
+    torch = _torch()
+    key = (_RAW_STREAM() if _RAW_STREAM is not None else None, torch._C._cuda_getDevice())
+    if key[0] is None or key != _TSTREAM[0]:
+        _TSTREAM = (key, torch.cuda.current_stream())
+    ev.record(_TSTREAM[1])
+    return ev
+
+
 class LaunchTimer:
     """HIP-event windows around runs of back-to-back fused solver-step launches.
 

@@ -260,7 +260,7 @@ class Solver:
             import torch
 
             ev = torch.cuda.Event()
-            ev.record()
+            _dev.record_event(ev)
         prev = self._astate.get("wb_thread")
         ast = self._astate
 

@@ -29,7 +29,7 @@ class _HostRows:
         self._h = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True)
         self._h.copy_(dev, non_blocking=True)
         self._ev = torch.cuda.Event()
-        self._ev.record()
+        _dev.record_event(self._ev)
 
     def host(self):
         _dev.wait_event(self._ev)
@@ -45,7 +45,7 @@ class _KernelRows(_HostRows):
 
         self.dev, self._h = dev, host
         self._ev = torch.cuda.Event()
-        self._ev.record()
+        _dev.record_event(self._ev)
 
 
 class CG(pxa.Solver):

@@ -141,7 +141,7 @@ class Memorize(pxa.StoppingCriterion):
             host = torch.empty((2,), dtype=torch.float64, pin_memory=True)
             host.copy_(mm, non_blocking=True)  # D2H into pinned memory (ordered on the stream)
             ev = torch.cuda.Event()
-            ev.record()
+            _dev.record_event(ev)
             self._pending = (ev, host, x.numel(), mm)
             return False
         x = x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
@@ -347,7 +347,7 @@ class RelError(pxa.StoppingCriterion):
             x_copy = _dev.relerr_stats(x, self._x_prev, host, copy=not borrow)
             if borrow:
                 x_copy = x
-        ev.record()
+        _dev.record_event(ev)
         if h is not None:
             self._x_prev = x_copy
         shape = x.shape[:-1]

@@ -8,7 +8,7 @@ import pyxu_amd.abc as pxa
 import pyxu_amd.opt.solver as pxs
 import pyxu_amd.opt.stop as pxst
 from pyxu_amd import _dev
-f, g, _ = bench.build_problem(2048, 2048, seed=1)
+f, g, _ = bench.build_problem(int(sys.argv[1]) if len(sys.argv) > 1 else 2048, int(sys.argv[1]) if len(sys.argv) > 1 else 2048, seed=1)
 with pxrt.Precision(pxrt.Width.SINGLE):
     like = torch.empty((1,), dtype=torch.float32, device="cuda")
     s = pxs.PGD(f=f, g=g, show_progress=False, stop_rate=1)
@@ -20,4 +20,4 @@ with pxrt.Precision(pxrt.Width.SINGLE):
     for _ in range(300): next(gen)
     torch.cuda.synchronize(); pr.disable(); dt = time.perf_counter() - t0
     print("us/step", 1e6 * dt / 300)
-    pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
