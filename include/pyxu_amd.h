@@ -58,6 +58,7 @@ extern "C" {
                                   picked by `sel` in the first dispatch round by n x 1024 cycles (s_sleep) */
 #define PXA_TUNE_PDS_EVENTS 5 /* measurement hook: > 0 makes pxa_pds_step record HIP events around each
                                  of its kernels (pxa_pds_kernel_ms) */
+#define PXA_TUNE_PDS_UNROLL 7 /* A/B: 1 runs the PDS dual kernel's plane loop without unrolling (default 2) */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */

@@ -66,7 +66,7 @@ __device__ inline void ldv(const T* p, T (&v)[NV]) {
 // axis-0 forward neighbour w(p + 1) is loaded once and carried to the next step.  The in-plane block
 // index is XCD-banded (tile2d::xcd_tile) so that the row+1 neighbour is usually read from the L2 of the
 // same XCD, where the neighbouring block marches in step.
-template <typename T, int NV, bool ISO, bool PD3O>
+template <typename T, int NV, bool ISO, bool PD3O, int UNR = 2>
 __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __restrict__ w,
                                                           const T* __restrict__ z, T* __restrict__ zo) {
   const PdsGeom<T> g = p.g;
@@ -87,6 +87,7 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
   const bool row_nb = r + 1 < n1, col_nb = c + NV < n2;
   T wn0[NV];  // w at the current plane (carried from the previous step)
   ldv<T, NV>(ws + (int64_t)pb * M, wn0);
+#pragma unroll UNR
   for (int pl = pb; pl < pe; ++pl) {
     const int64_t off = (int64_t)pl * M;
     T wc[NV], wp[NV];
@@ -180,8 +181,15 @@ int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, co
              hipStream_t st) {
   const int64_t blocks = (M + (int64_t)kBlock * NV - 1) / ((int64_t)kBlock * NV);
   dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pc.g.stack);
-  if (iso)
+  const bool u1 = tuning(PXA_TUNE_PDS_UNROLL) == 1;  // A/B: the plane loop without unrolling
+  if (iso && u1)
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O, 1>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+                       (const T*)z, (T*)zo);
+  else if (iso)
     hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+                       (const T*)z, (T*)zo);
+  else if (u1)
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O, 1>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
                        (const T*)z, (T*)zo);
   else
     hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
