@@ -378,12 +378,20 @@ def bench_c2_4096(ctx, args):
     return rec
 
 
-C3_BYTES = {"pd3o": (76, 80), "cv": (68, 68)}  # (own compulsory B/voxel of the fused step, SURVEY §8(d) B/voxel)
-C3_KERNELS = ("pds_axis0_kernel (A: axis-0 march of S0 / S0^T)", "pds_plane_kernel (B: in-plane G + point-wise update)",
-              "pds_dual_kernel (C: z + sigma grad w, fenchel prox, relaxation)")
-# own compulsory bytes per voxel of each kernel: PD3O A u,z(3) in x,Q out; B Q,x,u,S^T y in w,u+ out;
-# C w,z(3) in z+(3) out.  CV: A x in Q out; B Q,x,S^T y,z(3) in w,x+ out; C as PD3O.
-C3_KERNEL_BYTES = {"pd3o": (24, 24, 28), "cv": (8, 32, 28)}
+# (own compulsory B/voxel of the fused step, SURVEY §8(d) B/voxel): the look-ahead step (pxa_pds_step_la,
+# default) and the three-launch step (pxa_pds_step, --c3-three-launch)
+C3_BYTES = {True: {"pd3o": (64, 80), "cv": (64, 68)}, False: {"pd3o": (76, 80), "cv": (68, 68)}}
+C3_KERNELS = {
+    True: ("pds_march_kernel (priming march; absent from primed steps)",
+           "pds_plane_kernel (B: in-plane G + point-wise update)",
+           "pds_march_kernel (D: z + sigma grad w, fenchel prox, relaxation + the next iteration's axis-0 march)"),
+    False: ("pds_axis0_kernel (A: axis-0 march of S0 / S0^T)", "pds_plane_kernel (B: in-plane G + point-wise update)",
+            "pds_dual_kernel (C: z + sigma grad w, fenchel prox, relaxation)")}
+# own compulsory bytes per voxel of each kernel.  Three-launch: PD3O A u,z(3) in x,Q out;
+# B Q,x,u,S^T y in w,u+ out; C w,z(3) in z+(3) out.  CV: A x in Q out; B Q,x,S^T y,z(3) in w,x+ out; C as PD3O.
+# Look-ahead: B as above but CV reads K^T z (1 field) instead of z (3); D w,z(3),u+ (CV x+) in z+(3),Q and
+# x+ (CV K^T z+) out; the priming march reads u (x), z(3) and writes x (K^T z), Q.
+C3_KERNEL_BYTES = {True: {"pd3o": (24, 24, 40), "cv": (24, 24, 40)}, False: {"pd3o": (24, 24, 28), "cv": (8, 32, 28)}}
 
 
 def bench_c3(ctx, args):
@@ -403,6 +411,7 @@ def bench_c3(ctx, args):
     from pyxu_amd import _dev
 
     n, K = args.c3_n, args.c3_steps
+    la = not args.c3_three_launch
     sh = (n, n, n)
     N = n ** 3
     out = {"workload": f"{n}^3 volume, S = Gaussian(sigma=2), K = Gradient (3 dirs), h = 0.01 L1 (anisotropic TV), g = None",
@@ -425,6 +434,7 @@ def bench_c3(ctx, args):
         h = 0.01 * pxo.L1Norm(dim=3 * N)
         for algo, klass in (("pd3o", pxs.PD3O), ("cv", pxs.CondatVu)):
             s = klass(f=f, g=None, h=h, K=Kop, show_progress=False, stop_rate=K)
+            s._LOOKAHEAD = la
             s.fit(x0=torch.zeros(N, device="cuda", dtype=torch.float32), stop_crit=pxst.MaxIter(10 ** 9) | pxst.RelError(eps=1e-30),
                   mode=pxa.Mode.MANUAL)
             it = s.steps()
@@ -438,16 +448,18 @@ def bench_c3(ctx, args):
                 nrec, ms = _dev.pds_kernel_ms(reset=True)
             finally:
                 _dev.tuning(_dev.TUNE_PDS_EVENTS, prev)
-            own, surv = C3_BYTES[algo]
+            own, surv = C3_BYTES[la][algo]
             step_ms = 1e3 * elapsed / K
             rec = {"value": round(K / elapsed, 3), "unit": "iterations/s", "ms_per_step": round(step_ms, 3),
-                   "fused_m_step": s._plan is not None, "stop_rate": K,
+                   "fused_m_step": s._plan is not None, "lookahead": bool(s._plan and s._plan["la"]), "stop_rate": K,
                    "frac_step_own": round(own * N / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                    "frac_step_survey": round(surv * N / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
             if nrec > 0:
                 kms = [m / nrec for m in ms]
                 rec["kernels"] = []
-                for name, t, b in zip(C3_KERNELS, kms, C3_KERNEL_BYTES[algo]):
+                for name, t, b in zip(C3_KERNELS[la], kms, C3_KERNEL_BYTES[la][algo]):
+                    if la and t == 0:
+                        continue  # primed steps run no priming march
                     ach = b * N / (t * 1e-3) / 1e9 if t > 0 else 0.0
                     rec["kernels"].append({"kernel": name, "kernel_ms": round(t, 4), "bytes_per_voxel": b,
                                            "achieved": round(ach, 1), "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)})
@@ -587,6 +599,7 @@ def main():
     ap.add_argument("--c4096-steps", type=int, default=50, help="c2_4096 record: timed PGD steps at 4096^2 (0 = skip)")
     ap.add_argument("--c3-n", type=int, default=1024, help="c3 record: volume edge (0 = skip)")
     ap.add_argument("--c3-steps", type=int, default=10)
+    ap.add_argument("--c3-three-launch", action="store_true", help="C3 with the three-launch pxa_pds_step (A/B)")
     ap.add_argument("--c5-images", type=int, default=512)
     ap.add_argument("--c5-n", type=int, default=512)
     ap.add_argument("--c5-steps", type=int, default=20)

@@ -58,7 +58,8 @@ extern "C" {
                                   picked by `sel` in the first dispatch round by n x 1024 cycles (s_sleep) */
 #define PXA_TUNE_PDS_EVENTS 5 /* measurement hook: > 0 makes pxa_pds_step record HIP events around each
                                  of its kernels (pxa_pds_kernel_ms) */
-#define PXA_TUNE_PDS_UNROLL 7 /* A/B: 1 runs the PDS dual kernel's plane loop without unrolling (default 2) */
+#define PXA_TUNE_PDS_MARCH 7 /* A/B of pxa_pds_step_la's kernel D: bit 0 one position per thread, bit 1 the
+                                plane loop unrolled by 2 */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */
@@ -426,9 +427,10 @@ int pxa_real_to_complex(int dtype, int64_t n, const void* x, void* z, void* stre
 /* x[i] = Re z[i] (FFT(real=True).adjoint output, fft.py:370-379); n complex elements. */
 int pxa_complex_real_part(int dtype, int64_t n, const void* z, void* x, void* stream);
 
-/* Measurement hook: with pxa_tuning(PXA_TUNE_PDS_EVENTS, 1), pxa_pds_step records HIP events around its
- * three kernels (at most 64 steps).  This call waits for the last of them and writes into ms_abc[3] the
- * summed durations of kernels A (axis-0 march), B (in-plane G + update) and C (dual update) over the
+/* Measurement hook: with pxa_tuning(PXA_TUNE_PDS_EVENTS, 1), pxa_pds_step / pxa_pds_step_la record HIP
+ * events around their kernels (at most 64 steps).  This call waits for the last of them and writes into
+ * ms_abc[3] the summed durations of kernels A (axis-0 march; the look-ahead step's priming march, 0 when
+ * primed), B (in-plane G + update) and C (dual update; kernel D in the look-ahead step) over the
  * recorded steps, then (reset != 0) forgets them.  Returns the number of steps (>= 0) or an error. */
 int pxa_pds_kernel_ms(double* ms_abc, int reset);
 /* ---------------------------------------------------------------------------------------------
@@ -454,6 +456,24 @@ int pxa_pds_step(int dtype, int algo, const int64_t* geom, const int32_t* ntaps,
                  const double* coefs, const double* diff, const double* scal, int prox, int h_kind, const void* x,
                  const void* u, const void* z, const void* hty, void* x_out, void* u_out, void* z_out, void* work_q,
                  void* work_w, int nseg, void* stream);
+
+/* Look-ahead form of pxa_pds_step (same problem class and arguments, pds_march.hpp): two launches per
+ * iteration, kernel B and kernel D = the dual update of this iteration fused with the axis-0 march of
+ * the next one, which is therefore already done when the next call starts (primed = 1).  A call with
+ * primed = 0 first runs that march for the current state (one extra launch).
+ *   PD3O : x is the current iterate x = prox_g(u - tau K^T z) (written here when primed = 0, else as the
+ *          previous call's x_out left it); reads u, z; writes u_out, z_out and x_out = the NEXT iterate
+ *          (the x the next call receives).  x_out != x.
+ *   CV   : reads x, z; writes x_out, z_out (x_out != x).  u / u_out are ignored.
+ *   work_kt (CV): K^T z of the current z (written when primed = 0), rewritten with K^T z_out.
+ *   work_q: G0 of the current march variable (same priming rule), rewritten for the next iteration.
+ *   z_out must not alias z.  u_out may alias u.  Returns as pxa_pds_step.
+ * The caller keeps (x, work_q, work_kt) of one call for the next one; any change of the state in
+ * between (a restart, a user-supplied z) requires primed = 0. */
+int pxa_pds_step_la(int dtype, int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs,
+                    const double* coefs, const double* diff, const double* scal, int prox, int h_kind, int primed,
+                    void* x, const void* u, const void* z, const void* hty, void* x_out, void* u_out, void* z_out,
+                    void* work_q, void* work_kt, void* work_w, int nseg, void* stream);
 
 #ifdef __cplusplus
 }

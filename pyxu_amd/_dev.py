@@ -182,8 +182,8 @@ def storage_exclusive(t) -> bool:
 TUNE_NORMAL_DIAG = 1  # PXA_TUNE_NORMAL_DIAG: pxa_dense_normal timing probes (wrong results)
 TUNE_PGD_DIAG = 3  # PXA_TUNE_PGD_DIAG: bit 5 = s_memtime phase trace of the PGD tile kernel
 TUNE_PGD_STAGGER = 6  # PXA_TUNE_PGD_STAGGER: (sel << 8) | n, delayed first-round workgroups (A/B probe)
-TUNE_PDS_UNROLL = 7  # PXA_TUNE_PDS_UNROLL: 1 = PDS dual kernel plane loop not unrolled (A/B)
 TUNE_PDS_EVENTS = 5  # PXA_TUNE_PDS_EVENTS: per-kernel HIP events inside pxa_pds_step (pds_kernel_ms)
+TUNE_PDS_MARCH = 7  # PXA_TUNE_PDS_MARCH: kernel D A/B (bit 0 one position per thread, bit 1 plane loop unrolled by 2)
 
 
 def tuning(key, value=-1):
@@ -816,6 +816,18 @@ def pds_step(algo, pre, x, u, z, hty, x_out, u_out, z_out, work_q, work_w, nseg=
     ev = _TIMER.begin() if _TIMER is not None else None
     check(lib.pxa_pds_step(dtcode(z), int(algo), *pre, p(x), p(u), p(z), p(hty), p(x_out), p(u_out), p(z_out),
                            p(work_q), p(work_w), int(nseg), stream()), "pxa_pds_step")
+    if ev is not None:
+        _TIMER.end(ev)
+
+
+def pds_step_la(algo, pre, primed, x, u, z, hty, x_out, u_out, z_out, work_q, work_kt, work_w, nseg=0):
+    """One look-ahead PD3O / Condat-Vu iteration (pxa_pds_step_la): kernel B + kernel D (dual update fused
+    with the next iteration's axis-0 march); `primed` = the previous call left x / work_q / work_kt."""
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    ev = _TIMER.begin() if _TIMER is not None else None
+    check(lib.pxa_pds_step_la(dtcode(z), int(algo), *pre, int(bool(primed)), p(x), p(u), p(z), p(hty), p(x_out),
+                              p(u_out), p(z_out), p(work_q), p(work_kt), p(work_w), int(nseg), stream()),
+          "pxa_pds_step_la")
     if ev is not None:
         _TIMER.end(ev)
 

@@ -94,6 +94,11 @@ EXPORTS = {
         i32,
         [i32, i32, P_i64, P_i32, P_i32, P_f64, P_f64, P_f64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp],
     ),
+    "pxa_pds_step_la": (
+        i32,
+        [i32, i32, P_i64, P_i32, P_i32, P_f64, P_f64, P_f64, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+         i32, vp],
+    ),
 }
 
 

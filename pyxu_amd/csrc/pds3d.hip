@@ -25,15 +25,17 @@
 //  * kernel B is the LDS-tiled in-plane normal-operator sweep of pgd_tv2d.hip (tile2d.hpp: two
 //    register-blocked 4R+1-tap passes with exact boundary-row corrections) over every plane, with the
 //    solver's point-wise update fused into its epilogue.
-//  * kernel C is the dual update: K w (one forward neighbour per direction, from cache), the Moreau
-//    form of fenchel_prox (operator.py:905-944) exactly as pxa_fenchel_prox_l1 / _l21 evaluate it,
-//    and the relaxation.
+//  * kernel C is the dual update: K w (one forward neighbour per direction, from cache), fenchel_prox
+//    (operator.py:905-944) as the projection onto the lam-ball of the dual norm that its Moreau form
+//    equals (pds3d.hpp dual_out), and the relaxation.
+//  * pxa_pds_step_la replaces kernels C and A by kernel D (pds_march.hpp): the dual update of iteration k
+//    fused with the axis-0 march of iteration k + 1, two launches per iteration.
 // Compulsory HBM traffic per voxel (fp32): PD3O A 24 B + B 24 B + C 28 B = 76 B (80 B);
 // Condat-Vu A 8 B + B 32 B + C 28 B = 68 B (SURVEY: 68 B).
 //
 // Parity: the step follows the reference's arithmetic per voxel except that G x replaces
 // S^T (S x - y) + ... (same operator, different fp32 rounding order: see pgd_tv2d.hip).
-#include "pds3d.hpp"
+#include "pds_march.hpp"
 
 namespace pxa {
 namespace pds {
@@ -42,17 +44,9 @@ namespace pds {
 template <typename T>
 struct PdsC {
   PdsGeom<T> g;
-  T sigma, t, rho, omr;  // t = (1 / sigma) * lam, as pxa_fenchel_prox_* computes it
+  T sigma, lam, rho, omr;
   int seg;               // planes per axis-0 segment
 };
-
-template <typename T>
-__device__ inline T soft_thr(T x, T tau) {  // L1Norm.prox (norm.py:47-52), as elementwise.hip
-  T m = fabs(x) - tau;
-  m = m > T(0) ? m : T(0);
-  T sg = x > T(0) ? T(1) : (x < T(0) ? T(-1) : T(0));
-  return m * sg;
-}
 
 template <typename T, int NV>
 __device__ inline void ldv(const T* p, T (&v)[NV]) {
@@ -66,11 +60,11 @@ __device__ inline void ldv(const T* p, T (&v)[NV]) {
 // axis-0 forward neighbour w(p + 1) is loaded once and carried to the next step.  The in-plane block
 // index is XCD-banded (tile2d::xcd_tile) so that the row+1 neighbour is usually read from the L2 of the
 // same XCD, where the neighbouring block marches in step.
-template <typename T, int NV, bool ISO, bool PD3O, int UNR = 2>
+template <typename T, int NV, bool ISO, bool PD3O>
 __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __restrict__ w,
                                                           const T* __restrict__ z, T* __restrict__ zo) {
   const PdsGeom<T> g = p.g;
-  const T sigma = p.sigma, thr = p.t, rho = p.rho, omr = p.omr;
+  const T sigma = p.sigma, lam = p.lam, rho = p.rho, omr = p.omr;
   const int n0 = g.n0, n1 = g.n1, n2 = g.n2, D = g.D;
   const int64_t M = (int64_t)n1 * n2, N = M * n0;
   const int a_first = 3 - D;
@@ -87,7 +81,6 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
   const bool row_nb = r + 1 < n1, col_nb = c + NV < n2;
   T wn0[NV];  // w at the current plane (carried from the previous step)
   ldv<T, NV>(ws + (int64_t)pb * M, wn0);
-#pragma unroll UNR
   for (int pl = pb; pl < pe; ++pl) {
     const int64_t off = (int64_t)pl * M;
     T wc[NV], wp[NV];
@@ -121,52 +114,29 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
       }
       ldv<T, NV>(zs + (int64_t)(ax - a_first) * N + off, zc[ax]);
 #pragma unroll
-      for (int e = 0; e < NV; ++e) {
-        const T kw = g.c0[ax] * wc[e] + g.c1[ax] * wn[e];  // forward difference (pxa_gradient2)
-        zin[ax][e] = T(1) * zc[ax][e] + sigma * kw;         // z + sigma K w
-      }
+      for (int e = 0; e < NV; ++e) zin[ax][e] = dual_in<T>(zc[ax][e], wc[e], wn[e], g.c0[ax], g.c1[ax], sigma);
     }
 #pragma unroll
     for (int e = 0; e < NV; ++e) wn0[e] = wp[e];
-    T zt[3][NV];
-    if constexpr (ISO) {
-      // fenchel_prox of lam L21 (groups over directions): pxa_fenchel_prox_l21
+    T zo3[3][NV];
 #pragma unroll
-      for (int e = 0; e < NV; ++e) {
-        T ss = T(0);
-#pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
-          if (ax < a_first) continue;
-          const T v = zin[ax][e] / sigma;
-          ss += v * v;
-        }
-        const T n = sqrt(ss);
-        const T f = T(1) - thr / (n > thr ? n : thr);
-#pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
-          if (ax < a_first) continue;
-          const T pr = (zin[ax][e] / sigma) * f;
-          zt[ax][e] = pr * (-sigma) + zin[ax][e];
-        }
-      }
-    } else {
+    for (int e = 0; e < NV; ++e) {
+      T zc1[3], zi1[3], zn1[3];
 #pragma unroll
       for (int ax = 0; ax < 3; ++ax) {
-        if (ax < a_first) continue;
-#pragma unroll
-        for (int e = 0; e < NV; ++e) {
-          const T pr = soft_thr<T>(zin[ax][e] / sigma, thr);  // pxa_fenchel_prox_l1
-          zt[ax][e] = pr * (-sigma) + zin[ax][e];
-        }
+        zc1[ax] = ax < a_first ? T(0) : zc[ax][e];
+        zi1[ax] = ax < a_first ? T(0) : zin[ax][e];
       }
+      dual_out<T, ISO, PD3O>(zc1, zi1, a_first, lam, rho, omr, zn1);
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) zo3[ax][e] = zn1[ax];
     }
 #pragma unroll
     for (int ax = 0; ax < 3; ++ax) {
       if (ax < a_first) continue;
       T zn[NV];
 #pragma unroll
-      for (int e = 0; e < NV; ++e)
-        zn[e] = PD3O ? omr * zc[ax][e] + rho * zt[ax][e] : rho * zt[ax][e] + omr * zc[ax][e];
+      for (int e = 0; e < NV; ++e) zn[e] = zo3[ax][e];
       T* zq = zos + (int64_t)(ax - a_first) * N + off;
       if constexpr (NV == kVecN<T>)
         *reinterpret_cast<typename Vec4<T>::type*>(zq) = *reinterpret_cast<const typename Vec4<T>::type*>(zn);
@@ -181,15 +151,8 @@ int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, co
              hipStream_t st) {
   const int64_t blocks = (M + (int64_t)kBlock * NV - 1) / ((int64_t)kBlock * NV);
   dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pc.g.stack);
-  const bool u1 = tuning(PXA_TUNE_PDS_UNROLL) == 1;  // A/B: the plane loop without unrolling
-  if (iso && u1)
-    hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O, 1>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
-                       (const T*)z, (T*)zo);
-  else if (iso)
+  if (iso)
     hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
-                       (const T*)z, (T*)zo);
-  else if (u1)
-    hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O, 1>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
                        (const T*)z, (T*)zo);
   else
     hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
@@ -229,12 +192,22 @@ static void pds_event(int k, hipStream_t st) {
   if (k == 3) ++E.used;
 }
 
+// Validated geometry, taps and scalars shared by the three-launch and the look-ahead step.
 template <typename T>
-int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs, const double* coefs,
-              const double* diff, const double* scal, int prox, int h_kind, const void* x, const void* u,
-              const void* z, const void* hty, void* x_out, void* u_out, void* z_out, void* work_q, void* work_w,
-              int nseg, hipStream_t st) {
-  PXA_CHECK_ARG(algo == 0 || algo == 1);
+struct PdsSetup {
+  PdsGeom<T> g;
+  double kw[3][2 * kMaxR + 1];
+  int R0, R;  // axis-0 radius (0: axis 0 not blurred), in-plane radius
+  bool id0;
+  T tau, sigma, rho, lam, pw, omr;
+  int64_t M;
+  int prox;
+  bool iso;
+};
+
+template <typename T>
+int pds_setup(const int64_t* geom, const int32_t* ntaps, const int32_t* offs, const double* coefs, const double* diff,
+              const double* scal, int prox, int h_kind, PdsSetup<T>& S) {
   PXA_CHECK_ARG(geom && ntaps && offs && coefs && diff && scal);
   const int64_t stack = geom[0], y_images = geom[1], n0 = geom[2], n1 = geom[3], n2 = geom[4], D = geom[5];
   PXA_CHECK_ARG(stack >= 1 && y_images >= 1 && stack % y_images == 0);
@@ -242,24 +215,18 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
   PXA_CHECK_ARG(D == 2 || D == 3);
   PXA_CHECK_ARG(stack <= 65535 && n0 * n1 * n2 <= ((int64_t)1 << 40));
   PXA_CHECK_ARG(prox >= 0 && prox <= 2 && (h_kind == 0 || h_kind == 1));
-  const bool pd3o = algo == 0;
-  PXA_CHECK_ARG(z && hty && z_out && work_w && x_out && (pd3o ? (u && u_out) : (x != nullptr)));
-  PXA_CHECK_ARG(pd3o || x_out != x);  // kernel B reads x windows (halos) while writing x_out
   for (int a = 0; a < 3; ++a) PXA_CHECK_ARG(ntaps[a] >= 1 && ntaps[a] <= 2 * kMaxR + 1);
-  double kw[3][2 * kMaxR + 1];
   int Ra[3];
   for (int a = 0; a < 3; ++a) {
-    Ra[a] = tap_window(ntaps[a], offs + a * (2 * kMaxR + 1), coefs + a * (2 * kMaxR + 1), kw[a]);
+    Ra[a] = tap_window(ntaps[a], offs + a * (2 * kMaxR + 1), coefs + a * (2 * kMaxR + 1), S.kw[a]);
     if (Ra[a] < 0) return PXA_ERR_UNSUPPORTED;
   }
   // axis 0 is the identity iff its window is exactly [1] at offset 0
-  bool id0 = Ra[0] == 0 && kw[0][kMaxR] == 1.0;
-  const int R0 = id0 ? 0 : (Ra[0] > 0 ? Ra[0] : 1);
-  if (!id0) PXA_CHECK_ARG(work_q != nullptr);
-  int R = Ra[1] > Ra[2] ? Ra[1] : Ra[2];
-  if (R < 1) R = 1;
-
-  PdsGeom<T> g;
+  S.id0 = Ra[0] == 0 && S.kw[0][kMaxR] == 1.0;
+  S.R0 = S.id0 ? 0 : (Ra[0] > 0 ? Ra[0] : 1);
+  S.R = Ra[1] > Ra[2] ? Ra[1] : Ra[2];
+  if (S.R < 1) S.R = 1;
+  PdsGeom<T>& g = S.g;
   g.stack = stack;
   g.y_images = y_images;
   g.n0 = (int)n0;
@@ -270,81 +237,120 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
     g.c0[a] = (T)diff[a];
     g.c1[a] = (T)diff[3 + a];
   }
-  const T tau = (T)scal[0], sigma = (T)scal[1], rho = (T)scal[2], lam = (T)scal[3], pw = (T)scal[4];
-  const T omr = (T)(1.0 - scal[2]);
-  const int64_t M = n1 * n2;
+  S.tau = (T)scal[0];
+  S.sigma = (T)scal[1];
+  S.rho = (T)scal[2];
+  S.lam = (T)scal[3];
+  S.pw = (T)scal[4];
+  S.omr = (T)(1.0 - scal[2]);
+  S.M = n1 * n2;
+  S.prox = prox;
+  S.iso = h_kind == 1;
+  return PXA_OK;
+}
+
+// axis-0 march parameters (kernels A and D); resolves nseg (< 1: auto)
+template <typename T>
+PdsA<T> make_a(const PdsSetup<T>& S, int& nseg) {
+  PdsA<T> pa;
+  pa.g = S.g;
+  for (int t = 0; t < 2 * kMaxR0 + 1; ++t) pa.k0[t] = T(0);
+  for (int t = -S.R0; t <= S.R0; ++t) pa.k0[t + S.R0] = (T)S.kw[0][t + kMaxR];
+  pa.tau = S.tau;
+  pa.pw = S.pw;
+  pa.prox = S.prox;
+  const int64_t n0 = S.g.n0;
+  if (nseg < 1) {
+    // auto: about 4096 workgroups in flight, segments >= 4 rings deep (halo recompute <= 1/2)
+    const int64_t blocks = S.g.stack * ((S.M + 2 * kAThreads - 1) / (2 * kAThreads));
+    const int64_t want = (4096 + blocks - 1) / blocks;
+    const int64_t cap = S.R0 > 0 ? n0 / (4 * (2 * S.R0 + 1)) : n0;
+    nseg = (int)(want < cap ? want : cap);
+    if (nseg < 1) nseg = 1;
+  }
+  if (nseg > n0) nseg = (int)n0;
+  pa.seg = (int)((n0 + nseg - 1) / nseg);
+  nseg = (int)((n0 + pa.seg - 1) / pa.seg);
+  return pa;
+}
+
+// kernel B: mode 0 PD3O, 1 Condat-Vu (K^T z from z), 2 Condat-Vu (K^T z given in `z`)
+template <typename T>
+int stage_b(const PdsSetup<T>& S, int mode, const void* q_src, const void* xin, const void* u, const void* z,
+            const void* hty, void* w, void* out, hipStream_t st) {
+  constexpr int V = kVecN<T>;
+  const int R = S.R;
+  PdsB<T> pb;
+  pb.g = S.g;
+  pb.tiles1 = (int)((S.g.n1 + TY - 1) / TY);
+  pb.tiles2 = (int)((S.g.n2 + TX - 1) / TX);
+  const int64_t ntiles = S.g.stack * S.g.n0 * pb.tiles1 * pb.tiles2;
+  PXA_CHECK_ARG(ntiles <= 0x7fffffff);
+  pb.ntiles = (unsigned)ntiles;
+  for (int j = 0; j < 2 * kMaxR + 1; ++j) pb.k1[j] = pb.k2[j] = T(0);
+  for (int t = -R; t <= R; ++t) {
+    pb.k1[t + R] = (T)S.kw[1][t + kMaxR];
+    pb.k2[t + R] = (T)S.kw[2][t + kMaxR];
+  }
+  for (int j = 0; j < kMaxG; ++j) pb.g1[j] = pb.g2[j] = T(0);
+  for (int d = -2 * R; d <= 2 * R; ++d) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int t = -R; t <= R; ++t) {
+      if (t + d < -R || t + d > R) continue;
+      s1 += S.kw[1][t + kMaxR] * S.kw[1][t + d + kMaxR];
+      s2 += S.kw[2][t + kMaxR] * S.kw[2][t + d + kMaxR];
+    }
+    pb.g1[d + 2 * R] = (T)s1;
+    pb.g2[d + 2 * R] = (T)s2;
+  }
+  pb.tau = S.tau;
+  pb.rho = S.rho;
+  pb.omr = S.omr;
+  pb.pw = S.pw;
+  pb.prox = S.prox;
+  pb.vec_ok = (S.g.n2 % V == 0) && aligned16(q_src) && aligned16(xin) && aligned16(hty) && aligned16(w) &&
+              aligned16(out) && aligned16(z) && (mode != 0 || aligned16(u));
+  PdsPtrs P{q_src, xin, u, z, hty, w, out};
+  return run_b(pb, mode, R, P, st);
+}
+
+template <typename T>
+int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs, const double* coefs,
+              const double* diff, const double* scal, int prox, int h_kind, const void* x, const void* u,
+              const void* z, const void* hty, void* x_out, void* u_out, void* z_out, void* work_q, void* work_w,
+              int nseg, hipStream_t st) {
+  PXA_CHECK_ARG(algo == 0 || algo == 1);
+  PdsSetup<T> S;
+  if (const int e = pds_setup<T>(geom, ntaps, offs, coefs, diff, scal, prox, h_kind, S)) return e;
+  const bool pd3o = algo == 0;
+  PXA_CHECK_ARG(z && hty && z_out && work_w && x_out && (pd3o ? (u && u_out) : (x != nullptr)));
+  PXA_CHECK_ARG(pd3o || x_out != x);  // kernel B reads x windows (halos) while writing x_out
+  if (!S.id0) PXA_CHECK_ARG(work_q != nullptr);
+  const PdsGeom<T>& g = S.g;
+  const int64_t M = S.M;
   constexpr int V = kVecN<T>;
 
   const bool evs = tuning(PXA_TUNE_PDS_EVENTS) > 0;
   if (evs) pds_event(0, st);
   // ---- kernel A
   const void* q_src = pd3o ? (const void*)x_out : x;  // kernel B's input plane stack
-  if (pd3o || !id0) {
-    PdsA<T> pa;
-    pa.g = g;
-    for (int t = 0; t < 2 * kMaxR0 + 1; ++t) pa.k0[t] = T(0);
-    for (int t = -R0; t <= R0; ++t) pa.k0[t + R0] = (T)kw[0][t + kMaxR];
-    pa.tau = tau;
-    pa.pw = pw;
-    pa.prox = prox;
-    if (nseg < 1) {
-      // auto: about 4096 workgroups in flight, segments >= 4 rings deep (halo recompute <= 1/2)
-      const int64_t blocks = stack * ((M + 2 * kAThreads - 1) / (2 * kAThreads));
-      const int64_t want = (4096 + blocks - 1) / blocks;
-      const int64_t cap = R0 > 0 ? n0 / (4 * (2 * R0 + 1)) : n0;
-      nseg = (int)(want < cap ? want : cap);
-      if (nseg < 1) nseg = 1;
-    }
-    if (nseg > n0) nseg = (int)n0;
-    pa.seg = (int)((n0 + nseg - 1) / nseg);
-    nseg = (int)((n0 + pa.seg - 1) / pa.seg);
+  if (pd3o || !S.id0) {
+    const PdsA<T> pa = make_a(S, nseg);
     const void* src = pd3o ? u : x;
-    const bool np2 = (n2 % 2 == 0) && ((uintptr_t)src % (2 * sizeof(T)) == 0) &&
+    const bool np2 = (g.n2 % 2 == 0) && ((uintptr_t)src % (2 * sizeof(T)) == 0) &&
                      ((uintptr_t)z % (2 * sizeof(T)) == 0) && ((uintptr_t)x_out % (2 * sizeof(T)) == 0) &&
-                     (id0 || (uintptr_t)work_q % (2 * sizeof(T)) == 0);
-    void* q = id0 ? x_out : work_q;  // R0 == 0 never writes q
-    const int e = run_a(pa, pd3o, R0, np2 ? 2 : 1, M, nseg, src, z, x_out, q, st);
+                     (S.id0 || (uintptr_t)work_q % (2 * sizeof(T)) == 0);
+    void* q = S.id0 ? x_out : work_q;  // R0 == 0 never writes q
+    const int e = run_a(pa, pd3o, S.R0, np2 ? 2 : 1, M, nseg, src, z, x_out, q, st);
     if (e) return e;
-    if (!id0) q_src = work_q;
+    if (!S.id0) q_src = work_q;
   }
   if (evs) pds_event(1, st);
 
   // ---- kernel B
   {
-    PdsB<T> pb;
-    pb.g = g;
-    pb.tiles1 = (int)((n1 + TY - 1) / TY);
-    pb.tiles2 = (int)((n2 + TX - 1) / TX);
-    const int64_t ntiles = stack * n0 * pb.tiles1 * pb.tiles2;
-    PXA_CHECK_ARG(ntiles <= 0x7fffffff);
-    pb.ntiles = (unsigned)ntiles;
-    for (int j = 0; j < 2 * kMaxR + 1; ++j) pb.k1[j] = pb.k2[j] = T(0);
-    for (int t = -R; t <= R; ++t) {
-      pb.k1[t + R] = (T)kw[1][t + kMaxR];
-      pb.k2[t + R] = (T)kw[2][t + kMaxR];
-    }
-    for (int j = 0; j < kMaxG; ++j) pb.g1[j] = pb.g2[j] = T(0);
-    for (int d = -2 * R; d <= 2 * R; ++d) {
-      double s1 = 0.0, s2 = 0.0;
-      for (int t = -R; t <= R; ++t) {
-        if (t + d < -R || t + d > R) continue;
-        s1 += kw[1][t + kMaxR] * kw[1][t + d + kMaxR];
-        s2 += kw[2][t + kMaxR] * kw[2][t + d + kMaxR];
-      }
-      pb.g1[d + 2 * R] = (T)s1;
-      pb.g2[d + 2 * R] = (T)s2;
-    }
-    pb.tau = tau;
-    pb.rho = rho;
-    pb.omr = omr;
-    pb.pw = pw;
-    pb.prox = prox;
-    const void* xin = pd3o ? (const void*)x_out : x;
-    void* out = pd3o ? u_out : x_out;
-    pb.vec_ok = (n2 % V == 0) && aligned16(q_src) && aligned16(xin) && aligned16(hty) && aligned16(work_w) &&
-                aligned16(out) && aligned16(z) && (!pd3o || aligned16(u));
-    PdsPtrs P{q_src, xin, u, z, hty, work_w, out};
-    const int e = run_b(pb, pd3o, R, P, st);
+    const int e = stage_b(S, pd3o ? 0 : 1, q_src, pd3o ? (const void*)x_out : x, u, z, hty, work_w,
+                          pd3o ? u_out : x_out, st);
     if (e) return e;
   }
   if (evs) pds_event(2, st);
@@ -353,33 +359,88 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
   {
     PdsC<T> pc;
     pc.g = g;
-    pc.sigma = sigma;
-    pc.t = (T(1) / sigma) * lam;
-    pc.rho = rho;
-    pc.omr = omr;
-    const bool vec = (n2 % V == 0) && aligned16(work_w) && aligned16(z) && aligned16(z_out);
+    pc.sigma = S.sigma;
+    pc.lam = S.lam;
+    pc.rho = S.rho;
+    pc.omr = S.omr;
+    const bool vec = (g.n2 % V == 0) && aligned16(work_w) && aligned16(z) && aligned16(z_out);
     const int nv = vec ? V : 1;
     // enough workgroups for 256 CUs: split the march into segments (no halo: w(p + 1) is a plain load)
-    const int64_t blocks = stack * ((M + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
+    const int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
     int cseg = (int)((4096 + blocks - 1) / blocks);
-    if (cseg > n0) cseg = (int)n0;
+    if (cseg > g.n0) cseg = g.n0;
     if (cseg < 1) cseg = 1;
-    pc.seg = (int)((n0 + cseg - 1) / cseg);
-    cseg = (int)((n0 + pc.seg - 1) / pc.seg);
-    const bool iso = h_kind == 1;
+    pc.seg = (int)((g.n0 + cseg - 1) / cseg);
+    cseg = (int)((g.n0 + pc.seg - 1) / pc.seg);
     int e;
     if (vec)
-      e = pd3o ? launch_c<T, V, true>(pc, iso, M, cseg, work_w, z, z_out, st)
-               : launch_c<T, V, false>(pc, iso, M, cseg, work_w, z, z_out, st);
+      e = pd3o ? launch_c<T, V, true>(pc, S.iso, M, cseg, work_w, z, z_out, st)
+               : launch_c<T, V, false>(pc, S.iso, M, cseg, work_w, z, z_out, st);
     else
-      e = pd3o ? launch_c<T, 1, true>(pc, iso, M, cseg, work_w, z, z_out, st)
-               : launch_c<T, 1, false>(pc, iso, M, cseg, work_w, z, z_out, st);
+      e = pd3o ? launch_c<T, 1, true>(pc, S.iso, M, cseg, work_w, z, z_out, st)
+               : launch_c<T, 1, false>(pc, S.iso, M, cseg, work_w, z, z_out, st);
     if (e) return e;
   }
   if (evs) pds_event(3, st);
   return PXA_OK;
 }
 
+// Look-ahead step (pds_march.hpp): [priming march] + kernel B + kernel D.  PD3O: x (current x; written by
+// the priming march unless primed), u -> u_out, z -> z_out, x_out = x of the next iteration.  Condat-Vu:
+// x -> x_out, z -> z_out, work_kt = K^T z (written by the priming march unless primed, then rewritten for
+// the next iteration).  work_q = G0 v (same priming rule; rewritten by kernel D).
+template <typename T>
+int pds_la_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs, const double* coefs,
+                 const double* diff, const double* scal, int prox, int h_kind, int primed, void* x, const void* u,
+                 const void* z, const void* hty, void* x_out, void* u_out, void* z_out, void* work_q, void* work_kt,
+                 void* work_w, int nseg, hipStream_t st) {
+  PXA_CHECK_ARG(algo == 0 || algo == 1);
+  PdsSetup<T> S;
+  if (const int e = pds_setup<T>(geom, ntaps, offs, coefs, diff, scal, prox, h_kind, S)) return e;
+  const bool pd3o = algo == 0;
+  PXA_CHECK_ARG(x && z && hty && z_out && work_w && x_out && x_out != x && z_out != z);
+  PXA_CHECK_ARG(pd3o ? (u && u_out) : (work_kt != nullptr));
+  if (!S.id0) PXA_CHECK_ARG(work_q != nullptr);
+  const PdsGeom<T>& g = S.g;
+  const int64_t M = S.M;
+  PdsD<T> pd;
+  pd.a = make_a(S, nseg);
+  pd.sigma = S.sigma;
+  pd.lam = S.lam;
+  pd.rho = S.rho;
+  pd.omr = S.omr;
+  // kernel D's per-thread pairs: even rows and 8-byte aligned streams
+  auto a2 = [](const void* p) { return p == nullptr || (uintptr_t)p % (2 * sizeof(T)) == 0; };
+  const bool np2 = (g.n2 % 2 == 0) && a2(x) && a2(u) && a2(z) && a2(x_out) && a2(u_out) && a2(z_out) &&
+                   a2(work_q) && a2(work_kt) && a2(work_w);
+  const int np = np2 ? 2 : 1;
+  // q is written only when axis 0 is blurred; kernel B then reads it, else v itself
+  void* q = S.id0 ? work_w : work_q;
+
+  const bool evs = tuning(PXA_TUNE_PDS_EVENTS) > 0;
+  if (evs) pds_event(0, st);
+  if (!primed) {  // the march of this iteration: v from (u or x, z) without a dual update
+    const int e = run_d(pd, pd3o, S.iso, false, S.R0, np, M, nseg, work_w, z, pd3o ? u : x, z_out,
+                        pd3o ? x : work_kt, q, st);
+    if (e) return e;
+  }
+  if (evs) pds_event(1, st);
+  {
+    const void* q_src = S.id0 ? (const void*)x : work_q;
+    const int e = pd3o ? stage_b(S, 0, q_src, x, u, z, hty, work_w, u_out, st)
+                       : stage_b(S, 2, q_src, x, nullptr, work_kt, hty, work_w, x_out, st);
+    if (e) return e;
+  }
+  if (evs) pds_event(2, st);
+  {
+    // dual update of this iteration + the next iteration's march
+    const int e = run_d(pd, pd3o, S.iso, true, S.R0, np, M, nseg, work_w, z, pd3o ? (const void*)u_out : x_out,
+                        z_out, pd3o ? x_out : work_kt, q, st);
+    if (e) return e;
+  }
+  if (evs) pds_event(3, st);
+  return PXA_OK;
+}
 
 }  // namespace pds
 }  // namespace pxa
@@ -412,6 +473,15 @@ int pxa_pds_step(int dtype, int algo, const int64_t* geom, const int32_t* ntaps,
   PXA_DISPATCH(dtype, T,
                return pds_entry<T>(algo, geom, ntaps, offs, coefs, diff, scal, prox, h_kind, x, u, z, hty, x_out, u_out,
                                    z_out, work_q, work_w, nseg, as_stream(stream)));
+}
+
+int pxa_pds_step_la(int dtype, int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs,
+                    const double* coefs, const double* diff, const double* scal, int prox, int h_kind, int primed,
+                    void* x, const void* u, const void* z, const void* hty, void* x_out, void* u_out, void* z_out,
+                    void* work_q, void* work_kt, void* work_w, int nseg, void* stream) {
+  PXA_DISPATCH(dtype, T,
+               return pds_la_entry<T>(algo, geom, ntaps, offs, coefs, diff, scal, prox, h_kind, primed, x, u, z, hty,
+                                      x_out, u_out, z_out, work_q, work_kt, work_w, nseg, as_stream(stream)));
 }
 
 }  // extern "C"

@@ -59,6 +59,52 @@ __device__ inline void stn(T* p, const T (&v)[NP]) {
   }
 }
 
+// ------------------------------------------------------------------ dual update of one position
+// z_new = relax(fenchel_prox_h(z + sigma K w)) for the directions a_first..2 of one position; kernels C
+// and D both go through these helpers, so the three-launch and the look-ahead steps produce the same bits.
+template <typename T>
+__device__ inline T dual_in(T zc, T wc, T wn, T c0, T c1, T sigma) {
+  const T kw = fma(c0, wc, c1 * wn);  // forward difference (pxa_gradient2)
+  return fma(sigma, kw, zc);          // z + sigma K w
+}
+
+// one direction's term of K^T z at a position: the flipped 2-tap adjoint c1 z[i - e_a] + c0 z[i]
+// (pxa_gradient2_adjoint).  Explicit fmas here and in the dual helpers: every kernel that evaluates these
+// expressions (A, B, C, D, in whatever inlined context) rounds them the same way.
+template <typename T>
+__device__ inline T kt_term(T c1, T zm, T c0, T zc) {
+  return fma(c1, zm, c0 * zc);
+}
+
+// fenchel_prox_{sigma h}(zin) for h = lam L1 / lam L21 (operator.py:905-944 evaluates the Moreau form
+// zin - sigma prox_{h / sigma}(zin / sigma)), evaluated as what that form equals: the projection onto the
+// dual-norm ball of radius lam (L1: the box [-lam, lam] per direction; L21: the l2 ball over the
+// directions).  Same value up to rounding, without the three fp32 divisions per position the Moreau form
+// costs (the fused kernels are VALU-heavy).  Then the relaxation (PD3O: (1 - rho) z + rho z_t; Condat-Vu:
+// rho z_t + (1 - rho) z).
+template <typename T, bool ISO, bool PD3O>
+__device__ inline void dual_out(const T (&zc)[3], const T (&zin)[3], int a_first, T lam, T rho, T omr, T (&zn)[3]) {
+  T zt[3];
+  if constexpr (ISO) {
+    T ss = T(0);
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      if (ax < a_first) continue;
+      ss = fma(zin[ax], zin[ax], ss);
+    }
+    const T nrm = sqrt(ss);
+    const T f = nrm > lam ? lam / nrm : T(1);
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) zt[ax] = zin[ax] * f;
+  } else {
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) zt[ax] = fmin(fmax(zin[ax], -lam), lam);
+  }
+#pragma unroll
+  for (int ax = 0; ax < 3; ++ax)
+    zn[ax] = ax < a_first ? T(0) : (PD3O ? fma(omr, zc[ax], rho * zt[ax]) : fma(rho, zt[ax], omr * zc[ax]));
+}
+
 // ------------------------------------------------------------------ kernel A: axis-0 march
 template <typename T>
 struct PdsA {
@@ -146,13 +192,13 @@ __global__ void __launch_bounds__(kAThreads) pds_axis0_kernel(PdsA<T> p, const T
         // flipped 2-tap adjoint per direction, summed over directions in order (pxa_gradient2_adjoint)
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
-          const T term = g.c1[a] * zm[k] + g.c0[a] * zc[k];
+          const T term = kt_term<T>(g.c1[a], zm[k], g.c0[a], zc[k]);
           kt[k] = (a == a_first) ? term : kt[k] + term;
         }
       }
       const T one = T(1), mtau = -tau;
 #pragma unroll
-      for (int k = 0; k < NP; ++k) v[k] = apply_prox<T>(prox, one * u[k] + mtau * kt[k], pw);
+      for (int k = 0; k < NP; ++k) v[k] = apply_prox<T>(prox, fma(mtau, kt[k], one * u[k]), pw);
       if (qp >= pb && qp < pe) stn<T, NP>(xw + off, v);
     }
     return r;
@@ -236,13 +282,14 @@ struct PdsPtrs {
   const void* q;    // G0 x (or x when axis 0 is not blurred)
   const void* x;    // x (PD3O: the x written by kernel A)
   const void* u;    // PD3O: u
-  const void* z;    // Condat-Vu: z (for K^T z)
+  const void* z;    // Condat-Vu: z (for K^T z; MODE 2: K^T z itself)
   const void* hty;  // S^T y
   void* w;          // w (input of K in the dual update)
   void* out;        // PD3O: u_new ; Condat-Vu: x_new
 };
 
-template <typename T, int R, bool EDGE, bool PD3O>
+// MODE: 0 PD3O; 1 Condat-Vu with K^T z gathered from z; 2 Condat-Vu with K^T z precomputed (kernel D)
+template <typename T, int R, bool EDGE, int MODE>
 __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned char* smem, int64_t img, int ty0,
                                 int tx0) {
   using L = Layout<T, R>;
@@ -391,7 +438,7 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
     ld_vec<T, V>(O + S::idx(r, V * cq), gv);
     ld(P.x, off, xv);
     ld(P.hty, bo, bv);
-    if constexpr (PD3O) {
+    if constexpr (MODE == 0) {
       T uv[V];
       ld(P.u, off, uv);
 #pragma unroll
@@ -404,8 +451,10 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
     } else {
       // K^T z at the lane's pixels: sum over directions of c1 z_d[i - e_a] + c0 z_d[i]
       T kt[V];
+      if constexpr (MODE == 2) ld(P.z, off, kt);  // written by kernel D (same expression, same bits)
 #pragma unroll
       for (int ax = 0; ax < 3; ++ax) {
+        if constexpr (MODE == 2) break;
         if (ax < a_first) continue;
         const int64_t zo = (s * g.D + (ax - a_first)) * N + (int64_t)plane * M + (int64_t)gr * n2 + gc;
         T zc[V], zm[V];
@@ -431,7 +480,7 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
         }
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          const T term = g.c1[ax] * zm[e] + g.c0[ax] * zc[e];
+          const T term = kt_term<T>(g.c1[ax], zm[e], g.c0[ax], zc[e]);
           kt[e] = (ax == a_first) ? term : kt[e] + term;
         }
       }
@@ -450,7 +499,7 @@ __device__ inline void pds_tile(const PdsB<T>& p, const PdsPtrs& P, unsigned cha
   }
 }
 
-template <typename T, int R, bool PD3O>
+template <typename T, int R, int MODE>
 __global__ void __launch_bounds__(kThreads, 4) pds_plane_kernel(PdsB<T> p, PdsPtrs P) {
   using L = Layout<T, R>;
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -463,9 +512,9 @@ __global__ void __launch_bounds__(kThreads, 4) pds_plane_kernel(PdsB<T> p, PdsPt
   const bool interior = p.vec_ok && (int64_t)p.g.n1 * p.g.n2 <= 0x7fffffff && ty0 - 2 * R >= 0 &&
                         ty0 + TY + 2 * R <= p.g.n1 && tx0 - L::CA >= 0 && tx0 + TX + L::CA <= p.g.n2;
   if (interior)
-    pds_tile<T, R, false, PD3O>(p, P, smem_raw, img, ty0, tx0);
+    pds_tile<T, R, false, MODE>(p, P, smem_raw, img, ty0, tx0);
   else
-    pds_tile<T, R, true, PD3O>(p, P, smem_raw, img, ty0, tx0);
+    pds_tile<T, R, true, MODE>(p, P, smem_raw, img, ty0, tx0);
 }
 
 // ------------------------------------------------------------------ host side
@@ -499,9 +548,9 @@ int dispatch_a(int R0, const PdsA<T>& pa, int np, int64_t M, int nseg, const voi
   }
 }
 
-template <typename T, int R, bool PD3O>
+template <typename T, int R, int MODE>
 int launch_b(const PdsB<T>& pb, const PdsPtrs& P, hipStream_t st) {
-  auto kern = pds_plane_kernel<T, R, PD3O>;
+  auto kern = pds_plane_kernel<T, R, MODE>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -513,17 +562,17 @@ int launch_b(const PdsB<T>& pb, const PdsPtrs& P, hipStream_t st) {
   return last_launch_status();
 }
 
-template <typename T, bool PD3O>
+template <typename T, int MODE>
 int dispatch_b(int R, const PdsB<T>& pb, const PdsPtrs& P, hipStream_t st) {
   switch (R) {
-    case 1: return launch_b<T, 1, PD3O>(pb, P, st);
-    case 2: return launch_b<T, 2, PD3O>(pb, P, st);
-    case 3: return launch_b<T, 3, PD3O>(pb, P, st);
-    case 4: return launch_b<T, 4, PD3O>(pb, P, st);
-    case 5: return launch_b<T, 5, PD3O>(pb, P, st);
-    case 6: return launch_b<T, 6, PD3O>(pb, P, st);
-    case 7: return launch_b<T, 7, PD3O>(pb, P, st);
-    default: return launch_b<T, 8, PD3O>(pb, P, st);
+    case 1: return launch_b<T, 1, MODE>(pb, P, st);
+    case 2: return launch_b<T, 2, MODE>(pb, P, st);
+    case 3: return launch_b<T, 3, MODE>(pb, P, st);
+    case 4: return launch_b<T, 4, MODE>(pb, P, st);
+    case 5: return launch_b<T, 5, MODE>(pb, P, st);
+    case 6: return launch_b<T, 6, MODE>(pb, P, st);
+    case 7: return launch_b<T, 7, MODE>(pb, P, st);
+    default: return launch_b<T, 8, MODE>(pb, P, st);
   }
 }
 
@@ -531,8 +580,8 @@ int run_a(const PdsA<float>& pa, bool pd3o, int R0, int np, int64_t M, int nseg,
           void* xo, void* q, hipStream_t st);
 int run_a(const PdsA<double>& pa, bool pd3o, int R0, int np, int64_t M, int nseg, const void* src, const void* z,
           void* xo, void* q, hipStream_t st);
-int run_b(const PdsB<float>& pb, bool pd3o, int R, const PdsPtrs& P, hipStream_t st);
-int run_b(const PdsB<double>& pb, bool pd3o, int R, const PdsPtrs& P, hipStream_t st);
+int run_b(const PdsB<float>& pb, int mode, int R, const PdsPtrs& P, hipStream_t st);
+int run_b(const PdsB<double>& pb, int mode, int R, const PdsPtrs& P, hipStream_t st);
 
 }  // namespace pds
 }  // namespace pxa

@@ -4,8 +4,12 @@
 namespace pxa {
 namespace pds {
 
-int run_b(const PdsB<double>& pb, bool pd3o, int R, const PdsPtrs& P, hipStream_t st) {
-  return pd3o ? dispatch_b<double, true>(R, pb, P, st) : dispatch_b<double, false>(R, pb, P, st);
+int run_b(const PdsB<double>& pb, int mode, int R, const PdsPtrs& P, hipStream_t st) {
+  switch (mode) {
+    case 0: return dispatch_b<double, 0>(R, pb, P, st);
+    case 1: return dispatch_b<double, 1>(R, pb, P, st);
+    default: return dispatch_b<double, 2>(R, pb, P, st);
+  }
 }
 
 }  // namespace pds

@@ -1,0 +1,390 @@
+// Kernel D of the look-ahead PD3O / Condat-Vu step: the dual update of iteration k fused with the
+// axis-0 march that opens iteration k + 1 (kernel A's job in the three-launch step of pds3d.hip).
+//
+// Iteration k ends with z_{k+1} = relax(fenchel_prox_h(z_k + sigma K w_k)) (kernel C); iteration k + 1
+// starts with K^T z_{k+1}: PD3O builds v = x_{k+1} = prox_g(u_{k+1} - tau K^T z_{k+1}) and marches G0 v,
+// Condat-Vu marches G0 x_{k+1} and kernel B needs K^T z_{k+1}.  Kernel D does both in one pass: at each
+// plane of its march a thread updates z at its own positions (stored) and recomputes z_{k+1} at the two
+// in-plane backward neighbours K^T z needs (row - 1 for the axis-1 direction, column - 1 for the
+// axis-2 one; the axis-0 neighbour is carried from the previous plane), so z_{k+1} is never re-read.
+// It writes z_{k+1}, Q = G0 v and (PD3O) x_{k+1} or (Condat-Vu) K^T z_{k+1}.  DUAL = false is the
+// first iteration's march (no dual update: z_{k+1} = z).
+//
+// Compulsory HBM traffic per voxel (fp32, R0 > 0): reads w, z (D fields), u or x; writes z, Q and x or
+// K^T z: 40 B at D = 3, against kernel C (28 B) + kernel A (24 B PD3O / 8 B Condat-Vu) in the
+// three-launch step.  Requires z_out != z: neighbours read z_k while other threads write z_{k+1}.
+#pragma once
+#include "pds3d.hpp"
+
+namespace pxa {
+namespace pds {
+
+template <typename T>
+struct PdsD {
+  PdsA<T> a;  // march parameters: geometry, axis-0 taps, tau, prox, segments
+  T sigma, lam, rho, omr;
+};
+
+template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, int UNR = 1>
+__global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T* __restrict__ w,
+                                                              const T* __restrict__ z, const T* __restrict__ src,
+                                                              T* __restrict__ zo, T* __restrict__ ao,
+                                                              T* __restrict__ q) {
+  constexpr int RING = 2 * R0 + 1;
+  // kernel arguments copied to registers (the lambdas capture by reference; see pds_axis0_kernel)
+  const PdsGeom<T> g = p.a.g;
+  const T tau = p.a.tau, pw = p.a.pw;
+  const int prox = p.a.prox;
+  const T sigma = p.sigma, lam = p.lam, rho = p.rho, omr = p.omr;
+  T k0[RING];
+#pragma unroll
+  for (int t = 0; t < RING; ++t) k0[t] = p.a.k0[t];
+  const int n0 = g.n0, n1 = g.n1, n2 = g.n2;
+  const int64_t M = (int64_t)n1 * n2;
+  const int64_t j0 = ((int64_t)xcd_tile(blockIdx.x, gridDim.x) * kAThreads + threadIdx.x) * NP;
+  if (j0 >= M) return;  // no barriers below
+  const int64_t s = blockIdx.z;
+  const int64_t N = M * n0;
+  const int row = (int)(j0 / n2), col = (int)(j0 - (int64_t)row * n2);
+  const T* ws = w + s * N + j0;
+  const T* zs = z + s * g.D * N + j0;
+  T* zw = zo + s * g.D * N + j0;
+  const T* in = src + s * N + j0;
+  T* aw = ao + s * N + j0;
+  T* qw = q + s * N + j0;
+  const int seg = p.a.seg;
+  const int pb = blockIdx.y * seg;
+  const int pe = pb + seg < n0 ? pb + seg : n0;
+  const int a_first = 3 - g.D;
+  const bool row_nb = row + 1 < n1, col_nb = col + NP < n2;
+
+  // z_{k+1} at the thread's own positions of the plane at offset `off`, from w there (wc) and at the next
+  // plane (wf)
+  auto own_z = [&](int64_t off, const T(&wc)[NP], const T(&wf)[NP], T(&zn)[3][NP]) __attribute__((always_inline)) {
+    T w1[NP], w2[NP], zc[3][NP];
+    if (row_nb) {
+      ldn<T, NP>(ws + off + n2, w1);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) w1[k] = T(0);
+    }
+#pragma unroll
+    for (int k = 0; k + 1 < NP; ++k) w2[k] = wc[k + 1];
+    w2[NP - 1] = col_nb ? ws[off + NP] : T(0);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if (a < a_first) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) zc[a][k] = T(0);
+      } else {
+        ldn<T, NP>(zs + (int64_t)(a - a_first) * N + off, zc[a]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      T c3[3], i3[3], n3[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const T wn = a == 0 ? wf[k] : (a == 1 ? w1[k] : w2[k]);
+        c3[a] = zc[a][k];
+        i3[a] = a < a_first ? T(0) : dual_in<T>(zc[a][k], wc[k], wn, g.c0[a], g.c1[a], sigma);
+      }
+      dual_out<T, ISO, PD3O>(c3, i3, a_first, lam, rho, omr, n3);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) zn[a][k] = n3[a];
+    }
+  };
+  // z_{k+1} (all directions) at one position: offset o from the thread's first position, row rr, column
+  // cc, plane qp (for aniso TV the unused directions are dead code)
+  auto one_z = [&](int64_t o, int qp, int rr, int cc, T(&n3)[3]) __attribute__((always_inline)) {
+    T c3[3], i3[3];
+    const T wc = ws[o];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if (a < a_first) {
+        c3[a] = i3[a] = T(0);
+        continue;
+      }
+      c3[a] = zs[(int64_t)(a - a_first) * N + o];
+      T wn;
+      if (a == 0)
+        wn = qp + 1 < n0 ? ws[o + M] : T(0);
+      else if (a == 1)
+        wn = rr + 1 < n1 ? ws[o + n2] : T(0);
+      else
+        wn = cc + 1 < n2 ? ws[o + 1] : T(0);
+      i3[a] = dual_in<T>(c3[a], wc, wn, g.c0[a], g.c1[a], sigma);
+    }
+    dual_out<T, ISO, PD3O>(c3, i3, a_first, lam, rho, omr, n3);
+  };
+
+  T wcar[NP];  // DUAL: w at the next plane to process (own positions), carried
+  T zp0[NP];   // z_{k+1} of direction 0 at the previous plane (axis-0 backward neighbour of K^T z)
+  const int f0 = pb - 2 * R0 > 0 ? pb - 2 * R0 : 0;  // first plane the march visits
+#pragma unroll
+  for (int k = 0; k < NP; ++k) zp0[k] = wcar[k] = T(0);
+  if constexpr (DUAL) {
+    ldn<T, NP>(ws + (int64_t)f0 * M, wcar);
+    if (g.D == 3 && f0 > 0) {
+      T wprev[NP], zt[3][NP];
+      ldn<T, NP>(ws + (int64_t)(f0 - 1) * M, wprev);
+      own_z((int64_t)(f0 - 1) * M, wprev, wcar, zt);
+#pragma unroll
+      for (int k = 0; k < NP; ++k) zp0[k] = zt[0][k];
+    }
+  } else {
+    if (g.D == 3 && f0 > 0) ldn<T, NP>(zs + (int64_t)(f0 - 1) * M, zp0);
+  }
+
+  struct VN {
+    T v[NP];
+  };
+  // one plane of the march (planes are visited in increasing order from f0): z_{k+1}, K^T z_{k+1}, v
+  auto load_v = [&](int qp) __attribute__((always_inline)) -> VN {
+    const int64_t off = (int64_t)qp * M;
+    const bool mine = qp >= pb && qp < pe;
+    T zn[3][NP], zr1[NP], zl2;
+    if constexpr (DUAL) {
+      T wf[NP];
+      if (qp + 1 < n0) {
+        ldn<T, NP>(ws + off + M, wf);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) wf[k] = T(0);
+      }
+      own_z(off, wcar, wf, zn);
+#pragma unroll
+      for (int k = 0; k < NP; ++k) wcar[k] = wf[k];
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        zr1[k] = T(0);
+        if (a_first <= 1 && row > 0) {
+          T n3[3];
+          one_z(off - n2 + k, qp, row - 1, col + k, n3);
+          zr1[k] = n3[1];
+        }
+      }
+      zl2 = T(0);
+      if (col > 0) {
+        T n3[3];
+        one_z(off - 1, qp, row, col - 1, n3);
+        zl2 = n3[2];
+      }
+      if (mine) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          if (a < a_first) continue;
+          stn<T, NP>(zw + (int64_t)(a - a_first) * N + off, zn[a]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        if (a < a_first) continue;
+        ldn<T, NP>(zs + (int64_t)(a - a_first) * N + off, zn[a]);
+      }
+#pragma unroll
+      for (int k = 0; k < NP; ++k) zr1[k] = T(0);
+      if (a_first <= 1 && row > 0) ldn<T, NP>(zs + (int64_t)(1 - a_first) * N + off - n2, zr1);
+      zl2 = col > 0 ? zs[(int64_t)(2 - a_first) * N + off - 1] : T(0);
+    }
+    // K^T z_{k+1}: flipped 2-tap adjoint per direction, summed over directions in order
+    // (pxa_gradient2_adjoint; the expression of pds_axis0_kernel and of kernel B's Condat-Vu epilogue)
+    T kt[NP];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if (a < a_first) continue;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const T zm = a == 0 ? zp0[k] : (a == 1 ? zr1[k] : (k == 0 ? zl2 : zn[2][k - 1]));
+        const T term = kt_term<T>(g.c1[a], zm, g.c0[a], zn[a][k]);
+        kt[k] = (a == a_first) ? term : kt[k] + term;
+      }
+      if (a == 0) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) zp0[k] = zn[0][k];
+      }
+    }
+    VN r;
+    T(&v)[NP] = r.v;
+    if constexpr (PD3O) {
+      T u[NP];
+      ldn<T, NP>(in + off, u);
+      const T one = T(1), mtau = -tau;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) v[k] = apply_prox<T>(prox, fma(mtau, kt[k], one * u[k]), pw);
+      if (mine) stn<T, NP>(aw + off, v);
+    } else {
+      ldn<T, NP>(in + off, v);
+      if (mine) stn<T, NP>(aw + off, kt);
+    }
+    return r;
+  };
+
+  if constexpr (R0 == 0) {
+    for (int qp = pb; qp < pe; ++qp) (void)load_v(qp);
+  } else {
+    T rv[RING][NP], rh[RING][NP];
+#pragma unroll
+    for (int r = 0; r < RING; ++r)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) rv[r][k] = rh[r][k] = T(0);
+    const int first = pb - 2 * R0, last = pe - 1 + 2 * R0;
+    if constexpr (UNR == 0) {
+      // the two register rings of pds_axis0_kernel with static slots (plane body unrolled RING times):
+      // no register moves per plane; slot = (plane - base) mod RING
+      for (int base = first; base <= last; base += RING) {
+        static_for<0, RING>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          const int qp = base + j;
+          if (qp > last) return;
+          if (qp >= 0 && qp < n0) {
+            const VN r = load_v(qp);
+#pragma unroll
+            for (int k = 0; k < NP; ++k) rv[j][k] = r.v[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) rv[j][k] = T(0);
+          }
+          const int ph = qp - R0;
+          constexpr int jh = (j - R0 + RING) % RING;
+          if (ph >= 0 && ph < n0) {
+            T acc[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) acc[k] = T(0);
+            static_for<0, RING>([&](auto TT) {
+              constexpr int t = decltype(TT)::value;
+              constexpr int slot = (j + 1 + t) % RING;
+#pragma unroll
+              for (int k = 0; k < NP; ++k) acc[k] = fma(k0[t], rv[slot][k], acc[k]);
+            });
+#pragma unroll
+            for (int k = 0; k < NP; ++k) rh[jh][k] = acc[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) rh[jh][k] = T(0);
+          }
+          const int i = qp - 2 * R0;
+          if (i >= pb) {
+            T acc[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) acc[k] = T(0);
+            static_for<0, RING>([&](auto TT) {
+              constexpr int t = decltype(TT)::value;
+              constexpr int slot = ((j - R0 - t) % RING + RING) % RING;
+#pragma unroll
+              for (int k = 0; k < NP; ++k) acc[k] = fma(k0[t], rh[slot][k], acc[k]);
+            });
+            stn<T, NP>(qw + (int64_t)i * M, acc);
+          }
+        });
+      }
+      return;
+    }
+    // Q = G0 v (the plain two-pass form of pds_axis0_kernel, same taps in the same order) with the two
+    // windows held as shift registers: one copy of the plane body.  rv[t] = v at plane qp - 2 R0 + t;
+    // rh[t] = (H0 v) at plane qp - 3 R0 + t.
+#pragma unroll UNR
+    for (int qp = first; qp <= last; ++qp) {
+#pragma unroll
+      for (int t = 0; t + 1 < RING; ++t)
+#pragma unroll
+        for (int k = 0; k < NP; ++k) rv[t][k] = rv[t + 1][k];
+      if (qp >= 0 && qp < n0) {
+        const VN r = load_v(qp);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) rv[RING - 1][k] = r.v[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) rv[RING - 1][k] = T(0);
+      }
+      // (H0 v)[qp - R0] = sum_t k0[t] v[qp - 2 R0 + t]; zero outside [0, n0) (Trim o S o Pad)
+      const int ph = qp - R0;
+      T h[NP];
+#pragma unroll
+      for (int k = 0; k < NP; ++k) h[k] = T(0);
+      if (ph >= 0 && ph < n0) {
+#pragma unroll
+        for (int t = 0; t < RING; ++t)
+#pragma unroll
+          for (int k = 0; k < NP; ++k) h[k] = fma(k0[t], rv[t][k], h[k]);
+      }
+#pragma unroll
+      for (int t = 0; t + 1 < RING; ++t)
+#pragma unroll
+        for (int k = 0; k < NP; ++k) rh[t][k] = rh[t + 1][k];
+#pragma unroll
+      for (int k = 0; k < NP; ++k) rh[RING - 1][k] = h[k];
+      // Q[i] = sum_t k0[t] (H0 v)[i + R0 - t],  i = qp - 2 R0
+      const int i = qp - 2 * R0;
+      if (i >= pb) {
+        T acc[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) acc[k] = T(0);
+#pragma unroll
+        for (int t = 0; t < RING; ++t)
+#pragma unroll
+          for (int k = 0; k < NP; ++k) acc[k] = fma(k0[t], rh[2 * R0 - t][k], acc[k]);
+        stn<T, NP>(qw + (int64_t)i * M, acc);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host side
+template <typename T, int R0, bool PD3O, bool ISO, bool DUAL>
+int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, const void* z, const void* src, void* zo,
+             void* ao, void* q, hipStream_t st) {
+  // A/B: bit 0 one position per thread, bit 1 plane loop unrolled by 2, bit 2 static-slot rings
+  const int knob = tuning(PXA_TUNE_PDS_MARCH);
+  if (knob & 1) np = 1;
+  const int64_t blocks = (M + (int64_t)kAThreads * np - 1) / ((int64_t)kAThreads * np);
+  dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pd.a.g.stack);
+#define PXA_D_LAUNCH(NP, U)                                                                                      \
+  hipLaunchKernelGGL((pds_march_kernel<T, R0, NP, PD3O, ISO, DUAL, U>), grid, dim3(kAThreads), 0, st, pd, (const T*)w, \
+                     (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q)
+  if (DUAL && (knob & 4)) {
+    if (np == 2)
+      PXA_D_LAUNCH(2, 0);
+    else
+      PXA_D_LAUNCH(1, 0);
+  } else if (DUAL && (knob & 2)) {
+    if (np == 2)
+      PXA_D_LAUNCH(2, 2);
+    else
+      PXA_D_LAUNCH(1, 2);
+  } else {
+    if (np == 2)
+      PXA_D_LAUNCH(2, 1);
+    else
+      PXA_D_LAUNCH(1, 1);
+  }
+#undef PXA_D_LAUNCH
+  return last_launch_status();
+}
+
+template <typename T, bool PD3O, bool ISO, bool DUAL>
+int dispatch_d(int R0, const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, const void* z, const void* src,
+               void* zo, void* ao, void* q, hipStream_t st) {
+  switch (R0) {
+    case 0: return launch_d<T, 0, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+    case 1: return launch_d<T, 1, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+    case 2: return launch_d<T, 2, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+    case 3: return launch_d<T, 3, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+    case 4: return launch_d<T, 4, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+    case 5: return launch_d<T, 5, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+    case 6: return launch_d<T, 6, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+    case 7: return launch_d<T, 7, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+    default: return launch_d<T, 8, PD3O, ISO, DUAL>(pd, np, M, nseg, w, z, src, zo, ao, q, st);
+  }
+}
+
+// run_d: dual = false is the priming march (ISO irrelevant)
+#define PXA_PDS_RUN_D(T)                                                                                         \
+  int run_d(const PdsD<T>& pd, bool pd3o, bool iso, bool dual, int R0, int np, int64_t M, int nseg, const void* w, \
+            const void* z, const void* src, void* zo, void* ao, void* q, hipStream_t st)
+PXA_PDS_RUN_D(float);
+PXA_PDS_RUN_D(double);
+
+}  // namespace pds
+}  // namespace pxa

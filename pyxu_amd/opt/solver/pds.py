@@ -75,6 +75,8 @@ class _PrimalDualSplitting(pxa.Solver):
         mst["tau"], mst["sigma"], delta = self._set_step_sizes(tau, sigma, gamma)
         mst["rho"] = self._set_momentum_term(rho, delta)
         self._spare = None
+        self._la = None  # look-ahead step: (state arrays it was computed for, x of the next iteration)
+        self._zspare = None
         self._plan = self._fused_plan(mst["x"]) if fused else None
 
     _FUSED_ALGO = None  # pxa_pds_step algo code of the subclass (0 PD3O, 1 CondatVu), None: no fused step
@@ -98,7 +100,24 @@ class _PrimalDualSplitting(pxa.Solver):
         p["w"] = _dev.empty_like(x)
         p["q"] = None if p["taps"][0] == ([0], [1.0]) else _dev.empty_like(x)
         p["nseg"] = 0  # axis-0 march segments (0: one per column; tuning knob of pxa_pds_step)
+        p["la"] = bool(self._LOOKAHEAD)
+        p["kt"] = _dev.empty_like(x) if p["la"] and self._FUSED_ALGO == 1 else None
         return p
+
+    # Two launches per iteration (pxa_pds_step_la: kernel B + the dual update fused with the next
+    # iteration's axis-0 march) instead of three (pxa_pds_step); False selects the three-launch step.
+    _LOOKAHEAD = True
+
+    def _primed(self, *state):
+        """True iff the previous look-ahead step left the march of this iteration done for exactly
+        these state arrays (any restart or state replacement re-primes)."""
+        la = self._la
+        return la is not None and len(la[0]) == len(state) and all(a is b for a, b in zip(la[0], state))
+
+    def _take_zspare(self, z):
+        zs = self._zspare
+        self._zspare = None
+        return zs if zs is not None and zs is not z else _dev.empty_like(z)
 
     @staticmethod
     def _owned(t, extra=0):
@@ -184,6 +203,20 @@ class CondatVu(_PrimalDualSplitting):
         if self._plan is not None:
             p = self._plan
             x, z = mst["x"], mst["z"]
+            if p["la"]:
+                primed = self._primed(x, z)
+                self._la = None
+                out = self._spare
+                if out is None or out is x:
+                    out = _dev.empty_like(x)
+                z_out = self._take_zspare(z)
+                _dev.pds_step_la(1, p["pre"], primed, x, None, z, p["hty"], out, None, z_out, p["q"], p["kt"], p["w"],
+                                 nseg=p["nseg"])
+                mst["x"], mst["z"] = out, z_out
+                self._la = ((out, z_out), None)
+                self._spare = x if (sys.getrefcount(x) == 2 and _dev.storage_exclusive(x)) else None
+                self._zspare = z if (sys.getrefcount(z) == 2 and _dev.storage_exclusive(z)) else None
+                return
             out = self._spare
             if out is None or out is x:
                 out = _dev.empty_like(x)
@@ -277,6 +310,27 @@ class PD3O(_PrimalDualSplitting):
         if self._plan is not None:
             p = self._plan
             x, u, z = mst["x"], mst["u"], mst["z"]
+            if p["la"]:
+                # this iteration's x is the previous call's look-ahead x (primed) or computed here
+                primed = self._primed(x, u, z)
+                x_cur = self._la[1] if primed else None
+                self._la = None  # drop its references before the ownership checks
+                if x_cur is None:
+                    x_cur = x if self._owned(x, extra=1) else _dev.empty_like(x)
+                x_next = self._spare
+                if x_next is None or x_next is x_cur:
+                    x_next = _dev.empty_like(x)
+                u_out = u if self._owned(u, extra=1) else _dev.empty_like(u)
+                z_out = self._take_zspare(z)
+                _dev.pds_step_la(0, p["pre"], primed, x_cur, u, z, p["hty"], x_next, u_out, z_out, p["q"], None,
+                                 p["w"], nseg=p["nseg"])
+                mst["x"], mst["u"], mst["z"] = x_cur, u_out, z_out
+                self._la = ((x_cur, u_out, z_out), x_next)
+                del x_next, u_out
+                # the previous iterate's arrays are reused when nothing else holds them
+                self._spare = x if (x is not x_cur and sys.getrefcount(x) == 2 and _dev.storage_exclusive(x)) else None
+                self._zspare = z if (sys.getrefcount(z) == 2 and _dev.storage_exclusive(z)) else None
+                return
             x_out = x if self._owned(x, extra=1) else _dev.empty_like(x)
             u_out = u if self._owned(u, extra=1) else _dev.empty_like(u)
             z_out = z if self._owned(z, extra=1) else _dev.empty_like(z)

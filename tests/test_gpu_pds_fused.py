@@ -172,3 +172,74 @@ def test_pds_fused_stacked_rows_and_no_input_mutation(algo):
             s1 = ALGOS[algo](f=f, g=g, h=h, K=K, show_progress=False)
             s1.fit(x0=D(x0[r]), stop_crit=pxst.MaxIter(5))
             assert rel_err(xs[r], to_NUMPY(s1._mstate["x"])) <= 1e-6
+
+
+LA_CASES = [c for i, c in enumerate(CASES) if i in (0, 1, 2, 4, 5, 6)]
+
+
+def _run(algo, case, n, lookahead, x0, interrupt=None):
+    sh, sigma, h_kind, g_kind, dt, batch = case
+    import pyxu_amd.abc as pxa
+
+    with pxrt.Precision(W(dt)):
+        f, g, h, K, _ = _problem(sh, sigma, h_kind, g_kind, dt, batch_axis=batch)
+        s = ALGOS[algo](f=f, g=g, h=h, K=K, show_progress=False)
+        s._LOOKAHEAD = lookahead
+        s.fit(x0=D(x0), stop_crit=pxst.MaxIter(10 ** 6), mode=pxa.Mode.MANUAL)
+        it = s.steps()
+        for k in range(n):
+            if interrupt is not None and k == interrupt:
+                # a replaced state array (same values) invalidates the look-ahead: the step re-primes
+                s._mstate["z"] = s._mstate["z"].clone()
+            next(it)
+        assert s._plan is not None and s._plan["la"] == lookahead
+        return {k: to_NUMPY(v) for k, v in s._mstate.items() if k in ("x", "u", "z")}
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+@pytest.mark.parametrize("case", LA_CASES, ids=lambda c: f"{'x'.join(map(str, c[0]))}-s{c[1]}-{c[2]}-{c[3]}-{np.dtype(c[4]).name}{'-batch' if c[5] else ''}")
+def test_pds_lookahead_matches_three_launch(algo, case):
+    """pxa_pds_step_la (kernel B + kernel D: the dual update fused with the next march) against the
+    three-launch step: the same expressions through the same device helpers, so the same bits."""
+    N = int(np.prod(case[0]))
+    x0 = np.random.default_rng(5).uniform(0, 1, N).astype(case[4])
+    a = _run(algo, case, 6, True, x0)
+    b = _run(algo, case, 6, False, x0)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), (k, rel_err(a[k], b[k]))
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+def test_pds_lookahead_reprimes_after_state_change(algo):
+    case = ((17, 40, 70), 2.0, "iso", "pos", np.float32, False)
+    x0 = np.random.default_rng(6).uniform(0, 1, int(np.prod(case[0]))).astype(np.float32)
+    a = _run(algo, case, 5, True, x0, interrupt=3)
+    b = _run(algo, case, 5, True, x0)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_pds_lookahead_segments_bit_exact(algo):
+    """Kernel D's axis-0 segments recompute their halo planes (z, K^T z, v) with the same arithmetic."""
+    sh = (37, 40, 64)
+    N = int(np.prod(sh))
+    x0 = np.random.default_rng(3).uniform(0, 1, N).astype(np.float32)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        f, g, h, K, _ = _problem(sh, 2.0, "iso", "pos", np.float32)
+        s = (pxs.PD3O if algo == 0 else pxs.CondatVu)(f=f, g=g, h=h, K=K, show_progress=False)
+        s.fit(x0=D(x0), stop_crit=pxst.MaxIter(3))
+        p, m = s._plan, s._mstate
+        outs = []
+        for nseg in (1, 3, 37):
+            x = _dev.copy(m["x"])
+            u = _dev.copy(m["u"]) if algo == 0 else None
+            xo, zo = _dev.empty_like(m["x"]), _dev.empty_like(m["z"])
+            uo = _dev.empty_like(m["x"]) if algo == 0 else None
+            kt = _dev.empty_like(m["x"]) if algo == 1 else None
+            q = _dev.empty_like(m["x"])
+            _dev.pds_step_la(algo, p["pre"], False, x, u, m["z"], p["hty"], xo, uo, zo, q, kt, p["w"], nseg=nseg)
+            outs.append([to_NUMPY(t) for t in (x, xo, zo, q) + ((uo,) if algo == 0 else (kt,))])
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
