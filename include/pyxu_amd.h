@@ -58,8 +58,8 @@ extern "C" {
                                   picked by `sel` in the first dispatch round by n x 1024 cycles (s_sleep) */
 #define PXA_TUNE_PDS_EVENTS 5 /* measurement hook: > 0 makes pxa_pds_step record HIP events around each
                                  of its kernels (pxa_pds_kernel_ms) */
-#define PXA_TUNE_PDS_MARCH 7 /* A/B of pxa_pds_step_la's kernel D: bit 0 one position per thread, bit 1 the
-                                plane loop unrolled by 2 */
+#define PXA_TUNE_PDS_MARCH 7 /* A/B of pxa_pds_step_la's kernel D: bit 0 lets a thread own two positions
+                                (default one) */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */

@@ -183,7 +183,7 @@ TUNE_NORMAL_DIAG = 1  # PXA_TUNE_NORMAL_DIAG: pxa_dense_normal timing probes (wr
 TUNE_PGD_DIAG = 3  # PXA_TUNE_PGD_DIAG: bit 5 = s_memtime phase trace of the PGD tile kernel
 TUNE_PGD_STAGGER = 6  # PXA_TUNE_PGD_STAGGER: (sel << 8) | n, delayed first-round workgroups (A/B probe)
 TUNE_PDS_EVENTS = 5  # PXA_TUNE_PDS_EVENTS: per-kernel HIP events inside pxa_pds_step (pds_kernel_ms)
-TUNE_PDS_MARCH = 7  # PXA_TUNE_PDS_MARCH: kernel D A/B (bit 0 one position per thread, bit 1 plane loop unrolled by 2)
+TUNE_PDS_MARCH = 7  # PXA_TUNE_PDS_MARCH: kernel D A/B (bit 0: two positions per thread)
 
 
 def tuning(key, value=-1):

@@ -25,7 +25,7 @@ struct PdsD {
   T sigma, lam, rho, omr;
 };
 
-template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, int UNR = 1>
+template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL>
 __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T* __restrict__ w,
                                                               const T* __restrict__ z, const T* __restrict__ src,
                                                               T* __restrict__ zo, T* __restrict__ ao,
@@ -230,61 +230,11 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
 #pragma unroll
       for (int k = 0; k < NP; ++k) rv[r][k] = rh[r][k] = T(0);
     const int first = pb - 2 * R0, last = pe - 1 + 2 * R0;
-    if constexpr (UNR == 0) {
-      // the two register rings of pds_axis0_kernel with static slots (plane body unrolled RING times):
-      // no register moves per plane; slot = (plane - base) mod RING
-      for (int base = first; base <= last; base += RING) {
-        static_for<0, RING>([&](auto J) {
-          constexpr int j = decltype(J)::value;
-          const int qp = base + j;
-          if (qp > last) return;
-          if (qp >= 0 && qp < n0) {
-            const VN r = load_v(qp);
-#pragma unroll
-            for (int k = 0; k < NP; ++k) rv[j][k] = r.v[k];
-          } else {
-#pragma unroll
-            for (int k = 0; k < NP; ++k) rv[j][k] = T(0);
-          }
-          const int ph = qp - R0;
-          constexpr int jh = (j - R0 + RING) % RING;
-          if (ph >= 0 && ph < n0) {
-            T acc[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) acc[k] = T(0);
-            static_for<0, RING>([&](auto TT) {
-              constexpr int t = decltype(TT)::value;
-              constexpr int slot = (j + 1 + t) % RING;
-#pragma unroll
-              for (int k = 0; k < NP; ++k) acc[k] = fma(k0[t], rv[slot][k], acc[k]);
-            });
-#pragma unroll
-            for (int k = 0; k < NP; ++k) rh[jh][k] = acc[k];
-          } else {
-#pragma unroll
-            for (int k = 0; k < NP; ++k) rh[jh][k] = T(0);
-          }
-          const int i = qp - 2 * R0;
-          if (i >= pb) {
-            T acc[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) acc[k] = T(0);
-            static_for<0, RING>([&](auto TT) {
-              constexpr int t = decltype(TT)::value;
-              constexpr int slot = ((j - R0 - t) % RING + RING) % RING;
-#pragma unroll
-              for (int k = 0; k < NP; ++k) acc[k] = fma(k0[t], rh[slot][k], acc[k]);
-            });
-            stn<T, NP>(qw + (int64_t)i * M, acc);
-          }
-        });
-      }
-      return;
-    }
     // Q = G0 v (the plain two-pass form of pds_axis0_kernel, same taps in the same order) with the two
     // windows held as shift registers: one copy of the plane body.  rv[t] = v at plane qp - 2 R0 + t;
-    // rh[t] = (H0 v) at plane qp - 3 R0 + t.
-#pragma unroll UNR
+    // rh[t] = (H0 v) at plane qp - 3 R0 + t.  (Static ring slots as in pds_axis0_kernel, i.e. the plane
+    // body unrolled RING times, measured no faster: profiles/r03z_pds_march_ring_ab.txt.)
+#pragma unroll 1
     for (int qp = first; qp <= last; ++qp) {
 #pragma unroll
       for (int t = 0; t + 1 < RING; ++t)
@@ -335,31 +285,17 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
 template <typename T, int R0, bool PD3O, bool ISO, bool DUAL>
 int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, const void* z, const void* src, void* zo,
              void* ao, void* q, hipStream_t st) {
-  // A/B: bit 0 one position per thread, bit 1 plane loop unrolled by 2, bit 2 static-slot rings
-  const int knob = tuning(PXA_TUNE_PDS_MARCH);
-  if (knob & 1) np = 1;
+  // one position per thread by default (occupancy 7 against 4 with two: faster at 1024^3,
+  // profiles/r03z_pds_march_ring_ab.txt); PXA_TUNE_PDS_MARCH bit 0 allows two (A/B)
+  if (!(tuning(PXA_TUNE_PDS_MARCH) & 1)) np = 1;
   const int64_t blocks = (M + (int64_t)kAThreads * np - 1) / ((int64_t)kAThreads * np);
   dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pd.a.g.stack);
-#define PXA_D_LAUNCH(NP, U)                                                                                      \
-  hipLaunchKernelGGL((pds_march_kernel<T, R0, NP, PD3O, ISO, DUAL, U>), grid, dim3(kAThreads), 0, st, pd, (const T*)w, \
-                     (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q)
-  if (DUAL && (knob & 4)) {
-    if (np == 2)
-      PXA_D_LAUNCH(2, 0);
-    else
-      PXA_D_LAUNCH(1, 0);
-  } else if (DUAL && (knob & 2)) {
-    if (np == 2)
-      PXA_D_LAUNCH(2, 2);
-    else
-      PXA_D_LAUNCH(1, 2);
-  } else {
-    if (np == 2)
-      PXA_D_LAUNCH(2, 1);
-    else
-      PXA_D_LAUNCH(1, 1);
-  }
-#undef PXA_D_LAUNCH
+  if (np == 2)
+    hipLaunchKernelGGL((pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL>), grid, dim3(kAThreads), 0, st, pd, (const T*)w,
+                       (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
+  else
+    hipLaunchKernelGGL((pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL>), grid, dim3(kAThreads), 0, st, pd, (const T*)w,
+                       (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
   return last_launch_status();
 }
 

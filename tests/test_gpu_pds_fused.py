@@ -243,3 +243,18 @@ def test_pds_lookahead_segments_bit_exact(algo):
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+def test_pds_lookahead_two_positions_per_thread_bit_exact(algo):
+    """Kernel D with two positions per thread (PXA_TUNE_PDS_MARCH bit 0) gives the default's bits."""
+    case = ((17, 40, 70), 2.0, "iso", "pos", np.float32, False)
+    x0 = np.random.default_rng(7).uniform(0, 1, int(np.prod(case[0]))).astype(np.float32)
+    a = _run(algo, case, 4, True, x0)
+    prev = _dev.tuning(_dev.TUNE_PDS_MARCH, 1)
+    try:
+        b = _run(algo, case, 4, True, x0)
+    finally:
+        _dev.tuning(_dev.TUNE_PDS_MARCH, prev)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
