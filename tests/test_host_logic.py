@@ -496,3 +496,20 @@ def test_distributed_device_path_has_no_torch_kernels():
         if pat.search(line) and not fallback and "gloo host staging" not in line and "gloo CPU tests" not in line:
             bad.append((i, line.strip()))
     assert not bad, bad
+
+
+def test_pds_lookahead_priming_rule():
+    """The look-ahead PDS step reuses its march only for exactly the state arrays it left."""
+    import pyxu_amd.opt.solver as pxs
+
+    s = object.__new__(pxs.PD3O)
+    a, b, c, d = object(), object(), object(), object()
+    s._la = None
+    assert not s._primed(a, b, c)
+    s._la = ((a, b, c), d)
+    assert s._primed(a, b, c)
+    assert not s._primed(a, b, d)  # a replaced z re-primes
+    assert not s._primed(a, b)  # a different state layout
+    cv = object.__new__(pxs.CondatVu)
+    cv._la = ((a, b), None)
+    assert cv._primed(a, b) and not cv._primed(b, a)
