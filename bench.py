@@ -458,8 +458,8 @@ def bench_c3(ctx, args):
                 kms = [m / nrec for m in ms]
                 rec["kernels"] = []
                 for name, t, b in zip(C3_KERNELS[la], kms, C3_KERNEL_BYTES[la][algo]):
-                    if la and t == 0:
-                        continue  # primed steps run no priming march
+                    if la and name.startswith("pds_march_kernel (priming") and t < 0.01 * sum(kms):
+                        continue  # primed steps run no priming march (the window holds two back-to-back events)
                     ach = b * N / (t * 1e-3) / 1e9 if t > 0 else 0.0
                     rec["kernels"].append({"kernel": name, "kernel_ms": round(t, 4), "bytes_per_voxel": b,
                                            "achieved": round(ach, 1), "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)})
