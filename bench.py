@@ -461,8 +461,15 @@ def bench_c3(ctx, args):
                     if la and name.startswith("pds_march_kernel (priming") and t < 0.01 * sum(kms):
                         continue  # primed steps run no priming march (the window holds two back-to-back events)
                     ach = b * N / (t * 1e-3) / 1e9 if t > 0 else 0.0
-                    rec["kernels"].append({"kernel": name, "kernel_ms": round(t, 4), "bytes_per_voxel": b,
-                                           "achieved": round(ach, 1), "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)})
+                    ent = {"kernel": name, "kernel_ms": round(t, 4), "bytes_per_voxel": b,
+                           "achieved": round(ach, 1), "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+                    short = name.split(" ")[0]
+                    if la and short in ("pds_plane_kernel", "pds_march_kernel") and not name.startswith("pds_march_kernel (priming"):
+                        tr, src = measured_traffic(f"{short}_{algo}", f"{n}^3")
+                        ent["traffic"], ent["traffic_source"] = tr, src
+                        if tr:
+                            ent["traffic_bytes_per_voxel"] = round(tr / N, 2)
+                    rec["kernels"].append(ent)
                 kt = sum(kms)
                 rec["roofline"] = {"bound": "hbm", "achieved": round(own * N / (kt * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": round(own * N / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
