@@ -95,8 +95,9 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
     }
   };
   // z_{k+1} (all directions) at one position: offset o from the thread's first position, row rr, column
-  // cc, plane qp (for aniso TV the unused directions are dead code)
-  auto one_z = [&](int64_t o, int qp, int rr, int cc, T(&n3)[3]) __attribute__((always_inline)) {
+  // cc, plane qp (for aniso TV the unused directions are dead code).  The forward neighbour along
+  // direction `back` is the thread's own position, whose w (own_w) is already in a register.
+  auto one_z = [&](int64_t o, int qp, int rr, int cc, int back, T own_w, T(&n3)[3]) __attribute__((always_inline)) {
     T c3[3], i3[3];
     const T wc = ws[o];
 #pragma unroll
@@ -107,7 +108,9 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
       }
       c3[a] = zs[(int64_t)(a - a_first) * N + o];
       T wn;
-      if (a == 0)
+      if (a == back)
+        wn = own_w;
+      else if (a == 0)
         wn = qp + 1 < n0 ? ws[o + M] : T(0);
       else if (a == 1)
         wn = rr + 1 < n1 ? ws[o + n2] : T(0);
@@ -152,7 +155,10 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
 #pragma unroll
         for (int k = 0; k < NP; ++k) wf[k] = T(0);
       }
-      own_z(off, wcar, wf, zn);
+      T wc0[NP];
+#pragma unroll
+      for (int k = 0; k < NP; ++k) wc0[k] = wcar[k];
+      own_z(off, wc0, wf, zn);
 #pragma unroll
       for (int k = 0; k < NP; ++k) wcar[k] = wf[k];
 #pragma unroll
@@ -160,14 +166,14 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
         zr1[k] = T(0);
         if (a_first <= 1 && row > 0) {
           T n3[3];
-          one_z(off - n2 + k, qp, row - 1, col + k, n3);
+          one_z(off - n2 + k, qp, row - 1, col + k, 1, wc0[k], n3);
           zr1[k] = n3[1];
         }
       }
       zl2 = T(0);
       if (col > 0) {
         T n3[3];
-        one_z(off - 1, qp, row, col - 1, n3);
+        one_z(off - 1, qp, row, col - 1, 2, wc0[0], n3);
         zl2 = n3[2];
       }
       if (mine) {
