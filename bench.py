@@ -25,7 +25,11 @@ Sub-records on the same line (north_star):
   "c4": configs[3], ADMM with a dense 8192 x 65536 K (MFMA/GEMV dense path) + lam L1; K row-sharded
         over the ranks (one RCCL all-reduce of the 65536-vector per CG iteration);
   "c3": configs[2], PD3O and Condat-Vu on a 1024^3 volume (Gaussian S, anisotropic TV), with the
-        per-kernel times of the fused three-launch step (single GPU: replicas only at N > 1).
+        per-kernel times of the fused look-ahead step, two launches per iteration: kernel B and kernel D
+        (--c3-three-launch: the three-launch step A / B / C; single GPU: replicas only at N > 1);
+  "k4": SURVEY §8(d)'s "Gradient + prox" kernel alone (pxa_tv_dual_update) at 2048^2 and 1024^3;
+  "dense_mfma": the dense LinOp's MFMA path (8192 x 65536 K, B = 64 / 128 right-hand sides) in TFLOP/s.
+Every sub-record carries a `cpu_baseline` (the oracle on the host's cores, bounded sample).
 
 Roofline convention.  `frac` is the dominant kernel's time against ITS OWN compulsory bytes (every array
 it must read or write, once): the fused PGD launch reads x, x_prev, H^T y and writes x_new = 16 B/pixel.  `frac_survey` keeps SURVEY §8(d)'s 48 B/pixel figure for the same time; that model is not a
@@ -47,6 +51,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 KERNEL = "pgd_tv2d_kernel"
 SURVEY_BYTES_PER_PIXEL = 48  # 8 reads + 4 writes of fp32 per pixel per PGD iteration
+MFMA_F32_PEAK_TF = 157.3  # dense fp32 MFMA peak (MI355X_MICROARCH.md, Matrix cores: = the f32 vector peak)
 CPU_THREADS_MAX = 16  # the GPU box's CPU share per GPU (gpurun: 16)
 # pxa_pgd_tv2d_last_kernel() -> (mode name, own compulsory bytes per pixel): the arrays the launch reads / writes
 PGD_MODES = {1: ("x, x_prev, H^T y -> x_new", 16)}
@@ -224,6 +229,69 @@ def cpu_baseline(n0, n1, seed, budget_s, threads, lam=0.01, mu=0.01, sigma=2.0):
     run(iters)
     dt = time.perf_counter() - t0
     return iters / dt, iters, dt
+
+
+def cpu_threads():
+    return max(1, min(CPU_THREADS_MAX, os.cpu_count() or 1))
+
+
+def cpu_baseline_c5(n, images, seed, budget_s, threads, lam=0.01, mu=0.01, sigma=2.0):
+    """C5 (independent n x n TV-deblur images, each its own y): the oracle PGD on `images` of them, one image per
+    worker thread (oracle.parallel.pgd_tv_images_threaded); image-iterations/s is size-independent in the
+    number of images, so a bounded sample of the 512-image batch measures the batch's rate."""
+    import oracle as orc
+    from oracle.parallel import pgd_tv_images_threaded
+
+    sh = (n, n)
+    taps, c = orc.gaussian_taps(sigma, 3.0, np.float32)
+    blur = dict(arg_shape=sh, kernel=[taps, taps], center=[c, c])
+    ys = []
+    for i in range(images):
+        rng = np.random.default_rng((seed, i))
+        y = orc.stencil_apply(phantom(sh, rng).reshape(-1), sh, [taps, taps], [c, c])
+        ys.append((y + (0.01 * rng.standard_normal(n * n)).astype(np.float32)).astype(np.float32))
+    x0s = [np.zeros(n * n, np.float32)] * images
+    tau = np.float32(1 / np.float32(1.0 + (lam / mu) * 8.0))
+    pos = lambda z, t: orc.positive_orthant_prox(z)
+    t0 = time.perf_counter()
+    pgd_tv_images_threaded(x0s, blur, ys, lam, mu, pos, tau, 1, threads)
+    t1 = time.perf_counter() - t0
+    iters = int(max(2, min(500, budget_s / max(t1, 1e-3))))
+    t0 = time.perf_counter()
+    pgd_tv_images_threaded(x0s, blur, ys, lam, mu, pos, tau, iters, threads)
+    dt = time.perf_counter() - t0
+    return images * iters / dt, iters, dt
+
+
+def cpu_baseline_c4(M, N, threads, steps=4, lam=0.01):
+    """C4: CG steps of the ADMM x-update (QuadraticFunc.prox, operator.py:1273-1291 -> cg.py:125-153) on the
+    host: the oracle's CG (oracle.cg) on K^T K + I/tau with NumPy BLAS on `threads` threads, a dense M x N fp32 K
+    generated on the host.  Returns (ms per CG iteration, BLAS threads actually used)."""
+    import oracle as orc
+
+    try:
+        from threadpoolctl import threadpool_info, threadpool_limits
+    except ImportError:  # pragma: no cover
+        threadpool_limits, threadpool_info = None, None
+    rng = np.random.default_rng(5)
+    K = rng.standard_normal((M, N), dtype=np.float32)
+    K *= np.float32(1.0 / np.sqrt(M))
+    b = rng.standard_normal(N).astype(np.float32)
+    A = lambda p: (K.T @ (K @ p.T)).T.astype(p.dtype) + np.float32(1.0) * p
+    ctxm = threadpool_limits(limits=threads, user_api="blas") if threadpool_limits else None
+    try:
+        used = max((i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"), default=1) \
+            if threadpool_info else threads
+        orc.cg(A, b, max_iter=1)  # page-in, BLAS warm-up
+        t0 = time.perf_counter()
+        orc.cg(A, b, eps=0.0, max_iter=1)
+        t1 = time.perf_counter()
+        orc.cg(A, b, eps=0.0, max_iter=1 + steps)
+        t2 = time.perf_counter()
+    finally:
+        if ctxm is not None:
+            ctxm.restore_original_limits()
+    return 1e3 * ((t2 - t1) - (t1 - t0)) / steps, used
 
 
 # ----------------------------------------------------------------------------- timing helpers
@@ -589,6 +657,128 @@ def bench_c4(ctx, args):
     return rec
 
 
+def _event_ms(fn, reps, warm=2):
+    """Average duration of `fn()` over `reps` back-to-back launches, HIP events on the launch stream (torch's
+    current stream, which every pyxu_amd entry point launches on)."""
+    import torch
+
+    for _ in range(warm):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def bench_k4(ctx, args):
+    """SURVEY §8(d) "Gradient + prox" kernel K4: z <- (1 - rho) z + rho fenchel_prox_{sigma h}(z + sigma Grad w),
+    h = lam L1, standalone (pxa_tv_dual_update: kernel C of the three-launch PDS step) on a 2048^2 image and a
+    1024^3 volume.  Own bytes = (2D + 1) N 4 (w and z read, z written): SURVEY's figure."""
+    import torch
+
+    from pyxu_amd import _dev
+
+    out = {"kernel": "pds_dual_kernel (pxa_tv_dual_update)",
+           "op": "z <- (1-rho) z + rho fenchel_prox_{sigma lam L1}(z + sigma Grad w)"}
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    for key, sh, reps in (("2d_2048", (2048, 2048), 50), ("3d_1024", (args.c3_n,) * 3, 10)):
+        if sh[0] <= 0 or key[:2] not in args.k4_which.split(","):
+            continue
+        D = len(sh)
+        N = int(np.prod(sh))
+        w = torch.randn(N, generator=gen, device="cuda", dtype=torch.float32)
+        z = torch.randn(D * N, generator=gen, device="cuda", dtype=torch.float32).mul_(0.01)
+        zo = torch.empty_like(z)
+        geom = (1, 1, *sh, 2) if D == 2 else (1, *sh, 3)
+        run = lambda: _dev.tv_dual_update(w, z, geom, [-1.0] * 3, [1.0] * 3, 0.28, 0.01, 1.0, 0, relax=0, out=zo)
+        ms = _event_ms(run, reps)
+        own = (2 * D + 1) * N * 4
+        ach = own / (ms * 1e-3) / 1e9
+        tkey = "x".join(map(str, sh))
+        tr, src = measured_traffic("pds_dual_kernel", tkey)
+        out[key] = {"shape": list(sh), "kernel_ms": round(ms, 5), "launches_timed": reps,
+                    "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr, "traffic_source": src,
+                                 "bytes_per_launch": own, "bytes_model": f"(2D+1) N 4 = {(2 * D + 1) * 4} B/pixel"}}
+        del w, z, zo
+        torch.cuda.empty_cache()
+    return out
+
+
+def bench_dense_mfma(ctx, args):
+    """north_star's dense MFMA path (SURVEY §8(d) C4, B >= 40): Y = X K^T and Y = X K for a dense 8192 x 65536
+    K and B stacked right-hand sides (pxa_dense_matmat, v_mfma_f32_32x32x2_f32), HIP-event timed; against the
+    fp32 MFMA peak (MI355X_MICROARCH.md: 157.3 TF/s dense)."""
+    import torch
+
+    from pyxu_amd import _dev
+
+    M, N = args.c4_m, args.c4_n
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    A = torch.randn((M, N), generator=gen, device="cuda", dtype=torch.float32).mul_(1.0 / np.sqrt(M))
+    out = {"op": "pxa_dense_matmat fp32 (v_mfma_f32_32x32x2_f32)", "M": M, "N": N, "peak_tflops": MFMA_F32_PEAK_TF}
+    for B in args.mfma_b:
+        for name, trans in (("apply", 0), ("adjoint", 1)):
+            X = torch.randn((B, M if trans else N), generator=gen, device="cuda", dtype=torch.float32)
+            ms = _event_ms(lambda: _dev.dense_matmat(A, X, trans), 5)
+            tf = 2.0 * M * N * B / (ms * 1e-3) / 1e12
+            out[f"{name}_b{B}"] = {"B": B, "kernel_ms": round(ms, 4), "tflops": round(tf, 2),
+                                   "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TF,
+                                                "unit": "TFLOP/s", "frac": round(tf / MFMA_F32_PEAK_TF, 4),
+                                                "traffic": None}}
+            mb = measured_mfma_busy(f"{name}_b{B}")
+            if mb is not None:
+                out[f"{name}_b{B}"]["mfma_busy"] = mb
+            del X
+    del A
+    torch.cuda.empty_cache()
+    return out
+
+
+def measured_mfma_busy(key):
+    """SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CYCLES x 4 SIMDs) of the dense MFMA kernel from the committed rocprofv3
+    PMC pass (profiles/mfma_busy.json, scripts/pmc_mfma.py), or None.  Not measured in this run."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "mfma_busy.json")) as fh:
+            ent = json.load(fh).get(key)
+    except (OSError, ValueError):
+        return None
+    return ent
+
+
+def sub_cpu_baselines(sub, args):
+    """The oracle on the host beside each sub-record (north_star: every GPU number next to the NumPy path on
+    the node's host cores, core count stated); bounded samples, rank 0, N = 1 only."""
+    th = cpu_threads()
+    model = cpu_model()
+    budget = args.sub_cpu_seconds
+    if "c2_4096" in sub:
+        v, it, dt = cpu_baseline(4096, 4096, seed=4321, budget_s=budget, threads=th)
+        sub["c2_4096"]["cpu_baseline"] = {
+            "value": round(v, 4), "unit": "image-iterations/s", "cores": th, "kind": "port",
+            "sample": f"oracle/ NumPy restatement of the reference PGD path, same 4096x4096 problem, slab-parallel over "
+                      f"{th} threads: {it} iterations in {dt:.1f} s on {model}"}
+    if "c5" in sub:
+        imgs = th
+        v, it, dt = cpu_baseline_c5(args.c5_n, imgs, seed=77, budget_s=budget, threads=th)
+        sub["c5"]["cpu_baseline"] = {
+            "value": round(v, 3), "unit": "image-iterations/s", "cores": th, "kind": "port",
+            "sample": f"oracle PGD on {imgs} of the {args.c5_images} independent {args.c5_n}^2 images (one image per "
+                      f"thread, {th} threads): {it} iterations each in {dt:.1f} s on {model}"}
+    if "c4" in sub:
+        ms, used = cpu_baseline_c4(args.c4_m, args.c4_n, th)
+        per_outer = sub["c4"].get("cg_iters_per_outer") or 13.0
+        sub["c4"]["cpu_baseline"] = {
+            "value": round(1e3 / (ms * per_outer), 4), "unit": "ADMM outer iterations/s", "ms_per_cg_iter": round(ms, 2),
+            "cores": used, "kind": "port",
+            "sample": f"oracle CG (cg.py:125-153) on K^T K + I/tau, dense {args.c4_m}x{args.c4_n} fp32 K on the host, "
+                      f"NumPy BLAS on {used} threads, 4 timed CG iterations, outer rate at the GPU run's "
+                      f"{per_outer} CG iterations per outer iteration, on {model}"}
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -616,6 +806,12 @@ def main():
     ap.add_argument("--c4-steps", type=int, default=4)
     ap.add_argument("--c4-warmup", type=int, default=1)
     ap.add_argument("--c4-lam", type=float, default=0.01)
+    ap.add_argument("--mfma-b", type=lambda s: [int(v) for v in s.split(",") if v], default=[64, 128],
+                    help="dense_mfma record: stacked right-hand sides (empty = skip)")
+    ap.add_argument("--no-k4", action="store_true", help="skip the k4 (Gradient + prox kernel) record")
+    ap.add_argument("--k4-which", default="2d,3d", help="k4 record: shapes to time (2d = 2048^2, 3d = c3-n^3)")
+    ap.add_argument("--sub-cpu-seconds", type=float, default=5.0,
+                    help="CPU-baseline budget of the c2_4096 / c5 / c4 sub-records in s (0 = skip)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -651,7 +847,8 @@ def main():
     ctx = Ctx(world, rank, dist, coll_device="cpu" if backend == "gloo" else "cuda")
 
     if args.only:
-        fn = {"c2_4096": bench_c2_4096, "c5": bench_c5, "c4": bench_c4, "c3": bench_c3}[args.only]
+        fn = {"c2_4096": bench_c2_4096, "c5": bench_c5, "c4": bench_c4, "c3": bench_c3, "k4": bench_k4,
+              "dense_mfma": bench_dense_mfma}[args.only]
         rec = fn(ctx, args)
         if rank == 0:
             print(json.dumps({"only": args.only, **rec}), flush=True)
@@ -689,6 +886,14 @@ def main():
         if args.c3_n > 0:
             sub["c3"] = bench_c3(ctx, args)
             torch.cuda.empty_cache()
+        if not args.no_k4:
+            sub["k4"] = bench_k4(ctx, args)
+            torch.cuda.empty_cache()
+        if args.mfma_b:
+            sub["dense_mfma"] = bench_dense_mfma(ctx, args)
+            torch.cuda.empty_cache()
+        if args.sub_cpu_seconds > 0 and world == 1:
+            sub_cpu_baselines(sub, args)
 
     if rank == 0:
         value = world * args.steps / elapsed_max

@@ -457,6 +457,18 @@ int pxa_pds_step(int dtype, int algo, const int64_t* geom, const int32_t* ntaps,
                  const void* u, const void* z, const void* hty, void* x_out, void* u_out, void* z_out, void* work_q,
                  void* work_w, int nseg, void* stream);
 
+/* The dual update of the PDS step on its own (kernel C of pxa_pds_step; SURVEY.md §8(d) "Gradient +
+ * prox", K4): z_out = relax(fenchel_prox_{sigma h}(z + sigma K w)) with K = Gradient over the D trailing
+ * axes (forward differences, zero boundary: diff.py:1113-1265), h = lam L1 (h_kind 0) or lam L21 over the
+ * D directions (h_kind 1); fenchel_prox (abc/operator.py:905-944) evaluated as the projection onto the
+ * dual-norm ball of radius lam that its Moreau form equals.  relax 0: PD3O's
+ * (1 - rho) z + rho z_t (opt/solver/pds.py:760), 1: Condat-Vu's rho z_t + (1 - rho) z (pds.py:441).
+ *   geom = {stack, n0, n1, n2, D}: w is (stack, n0, n1, n2); z and z_out are (stack, D, n0, n1, n2)
+ *          direction-major, direction d on axis d + 3 - D (D = 2 requires n0 = 1: images).
+ *   diff = {c0[3], c1[3]} as in pxa_pds_step.  z_out may alias z, not w. */
+int pxa_tv_dual_update(int dtype, int relax, const int64_t* geom, const double* diff, double sigma, double lam,
+                       double rho, int h_kind, const void* w, const void* z, void* z_out, void* stream);
+
 /* Look-ahead form of pxa_pds_step (same problem class and arguments, pds_march.hpp): two launches per
  * iteration, kernel B and kernel D = the dual update of this iteration fused with the axis-0 march of
  * the next one, which is therefore already done when the next call starts (primed = 1).  A call with

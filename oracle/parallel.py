@@ -21,7 +21,7 @@ import numpy as np
 
 from oracle import pyxu_np as orc
 
-__all__ = ["pgd_tv_threaded"]
+__all__ = ["pgd_tv_threaded", "pgd_tv_images_threaded"]
 
 
 def _slabs(n0, parts):
@@ -71,3 +71,19 @@ def pgd_tv_threaded(x0, blur, y, lam, mu, prox, tau, n_iter, threads, d=75):
             list(pool.map(work, [(lo, hi, a, x, x_prev, out) for lo, hi in slabs]))
             x_prev, x = x, out
     return x.reshape(-1), x_prev.reshape(-1)
+
+
+def pgd_tv_images_threaded(x0s, blur, ys, lam, mu, prox, tau, n_iter, threads, d=75):
+    """``pyxu_np.pgd`` on each of several INDEPENDENT images (batched stacks, config C5: each image its own
+    data y), one image per worker thread at a time -- the reference's stacked-problem parallelism
+    (independent leading dims) on a thread pool.  Every image runs the single-thread
+    oracle unchanged.  Returns the list of final iterates."""
+    sh = tuple(blur["arg_shape"])
+
+    def one(args):
+        x0, y = args
+        grad = lambda v: orc.deblur_tv_grad(v, blur, y, lam, mu, dict(arg_shape=sh))
+        return orc.pgd(x0, grad, prox, tau, n_iter, d=d)[0]
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as pool:
+        return list(pool.map(one, zip(x0s, ys)))

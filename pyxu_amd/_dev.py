@@ -832,6 +832,24 @@ def pds_step_la(algo, pre, primed, x, u, z, hty, x_out, u_out, z_out, work_q, wo
         _TIMER.end(ev)
 
 
+def tv_dual_update(w, z, geom, c0, c1, sigma, lam, rho, h_kind, relax=0, out=None):
+    """z_out = relax(fenchel_prox_{sigma h}(z + sigma Grad w)), h = lam L1 (h_kind 0) / lam L21 (1):
+    the PDS dual update alone (pxa_tv_dual_update).  geom = (stack, n0, n1, n2, D); relax 0 PD3O, 1 CV."""
+    w = require(w, "w")
+    z = require(z, "z")
+    if w.dtype != z.dtype:
+        raise TypeError("pyxu_amd: w and z must share a dtype")
+    stack, n0, n1, n2, D = (int(v) for v in geom)
+    if w.numel() != stack * n0 * n1 * n2 or z.numel() != D * w.numel():
+        raise ValueError(f"pyxu_amd: tv_dual_update geometry {tuple(geom)} does not match w {tuple(w.shape)}, "
+                         f"z {tuple(z.shape)}")
+    out = empty_like(z) if out is None else require(out, "out")
+    check(lib.pxa_tv_dual_update(dtcode(z), int(relax), i64_array([stack, n0, n1, n2, D]),
+                                 f64_array(list(c0) + list(c1)), float(sigma), float(lam), float(rho), int(h_kind),
+                                 ptr(w), ptr(z), ptr(out), stream()), "pxa_tv_dual_update")
+    return out
+
+
 def pds_kernel_ms(reset=True):
     """(steps, [ms A, ms B, ms C] summed) of the pxa_pds_step calls recorded under TUNE_PDS_EVENTS."""
     buf = (ct.c_double * 3)()

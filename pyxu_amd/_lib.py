@@ -94,6 +94,7 @@ EXPORTS = {
         i32,
         [i32, i32, P_i64, P_i32, P_i32, P_f64, P_f64, P_f64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp],
     ),
+    "pxa_tv_dual_update": (i32, [i32, i32, P_i64, P_f64, f64, f64, f64, i32, vp, vp, vp, vp]),
     "pxa_pds_step_la": (
         i32,
         [i32, i32, P_i64, P_i32, P_i32, P_f64, P_f64, P_f64, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,

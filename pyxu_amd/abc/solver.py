@@ -390,7 +390,10 @@ class Solver:
         if ast["pending"]:
             with ast["lock"]:
                 if ast["pending"]:
-                    self._record_batch([ast["pending"].pop(0)], flush=False)
+                    # unflushed at most _RECORD_LAG lines: a reader of solver.log lags by at most one batch
+                    n = ast.get("unflushed", 0) + 1
+                    ast["unflushed"] = 0 if n >= self._RECORD_LAG else n
+                    self._record_batch([ast["pending"].pop(0)], flush=n >= self._RECORD_LAG)
         if resolve():
             ast["idx"] -= 1
             self._spec_rollback(token)
@@ -458,6 +461,7 @@ class Solver:
             return True
         except Exception as e:
             self._flush_records()
+            self._flush_log()  # lines written unflushed by speculative checks reach the file first
             msg = f"[{dt.datetime.now()}] Something went wrong -> EXCEPTION RAISED"
             if ast.get("internal"):
                 ast["exception"] = e
@@ -544,6 +548,15 @@ class Solver:
                 h.stream.write(text)
                 if flush:
                     h.flush()
+        if flush:
+            self._astate["unflushed"] = 0
+
+    def _flush_log(self):
+        for h in getattr(self._astate.get("logger"), "_pxa_direct", None) or ():
+            with h.lock:
+                if h.stream is not None:
+                    h.flush()
+        self._astate["unflushed"] = 0
 
     def _flush_records(self):
         ast = self._astate

@@ -160,6 +160,59 @@ int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, co
   return last_launch_status();
 }
 
+// Kernel C over a whole (stack, n0, n1, n2) geometry: z_out = relax(fenchel_prox_h(z + sigma K w)).  The
+// march is split into axis-0 segments so that about 4096 workgroups are in flight (no halo: w(p + 1) is a
+// plain load).  pd3o selects the relaxation order: (1 - rho) z + rho z_t, else rho z_t + (1 - rho) z.
+template <typename T>
+int run_c(const PdsGeom<T>& g, T sigma, T lam, T rho, T omr, bool pd3o, bool iso, const void* w, const void* z,
+          void* z_out, hipStream_t st) {
+  constexpr int V = kVecN<T>;
+  const int64_t M = (int64_t)g.n1 * g.n2;
+  PdsC<T> pc;
+  pc.g = g;
+  pc.sigma = sigma;
+  pc.lam = lam;
+  pc.rho = rho;
+  pc.omr = omr;
+  const bool vec = (g.n2 % V == 0) && aligned16(w) && aligned16(z) && aligned16(z_out);
+  const int nv = vec ? V : 1;
+  const int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
+  int cseg = (int)((4096 + blocks - 1) / blocks);
+  if (cseg > g.n0) cseg = g.n0;
+  if (cseg < 1) cseg = 1;
+  pc.seg = (int)((g.n0 + cseg - 1) / cseg);
+  cseg = (int)((g.n0 + pc.seg - 1) / pc.seg);
+  if (vec)
+    return pd3o ? launch_c<T, V, true>(pc, iso, M, cseg, w, z, z_out, st) : launch_c<T, V, false>(pc, iso, M, cseg, w, z, z_out, st);
+  return pd3o ? launch_c<T, 1, true>(pc, iso, M, cseg, w, z, z_out, st) : launch_c<T, 1, false>(pc, iso, M, cseg, w, z, z_out, st);
+}
+
+// pxa_tv_dual_update: kernel C alone (the "Gradient + prox" kernel of SURVEY §8(d), K4)
+template <typename T>
+int dual_entry(int relax, const int64_t* geom, const double* diff, double sigma, double lam, double rho, int h_kind,
+               const void* w, const void* z, void* z_out, hipStream_t st) {
+  PXA_CHECK_ARG(geom && diff && w && z && z_out && z_out != w);
+  PXA_CHECK_ARG(relax == 0 || relax == 1);
+  PXA_CHECK_ARG(h_kind == 0 || h_kind == 1);
+  const int64_t stack = geom[0], n0 = geom[1], n1 = geom[2], n2 = geom[3], D = geom[4];
+  PXA_CHECK_ARG(stack >= 1 && stack <= 65535 && n0 >= 1 && n1 >= 1 && n2 >= 1);
+  PXA_CHECK_ARG(n0 <= 0x7fffffff && n1 <= 0x7fffffff && n2 <= 0x7fffffff && n0 * n1 * n2 <= ((int64_t)1 << 40));
+  PXA_CHECK_ARG(D == 2 || D == 3);
+  PXA_CHECK_ARG(D == 3 || n0 == 1);
+  PdsGeom<T> g;
+  g.stack = stack;
+  g.y_images = 1;
+  g.n0 = (int)n0;
+  g.n1 = (int)n1;
+  g.n2 = (int)n2;
+  g.D = (int)D;
+  for (int a = 0; a < 3; ++a) {
+    g.c0[a] = (T)diff[a];
+    g.c1[a] = (T)diff[3 + a];
+  }
+  return run_c<T>(g, (T)sigma, (T)lam, (T)rho, (T)(1.0 - rho), relax == 0, h_kind == 1, w, z, z_out, st);
+}
+
 // dense tap window (index t + R) of one axis from (offset, coefficient) lists; returns the radius or -1
 inline int tap_window(int nt, const int32_t* off, const double* coef, double (&k)[2 * kMaxR + 1]) {
   for (double& v : k) v = 0.0;
@@ -328,7 +381,6 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
   if (!S.id0) PXA_CHECK_ARG(work_q != nullptr);
   const PdsGeom<T>& g = S.g;
   const int64_t M = S.M;
-  constexpr int V = kVecN<T>;
 
   const bool evs = tuning(PXA_TUNE_PDS_EVENTS) > 0;
   if (evs) pds_event(0, st);
@@ -356,31 +408,7 @@ int pds_entry(int algo, const int64_t* geom, const int32_t* ntaps, const int32_t
   if (evs) pds_event(2, st);
 
   // ---- kernel C
-  {
-    PdsC<T> pc;
-    pc.g = g;
-    pc.sigma = S.sigma;
-    pc.lam = S.lam;
-    pc.rho = S.rho;
-    pc.omr = S.omr;
-    const bool vec = (g.n2 % V == 0) && aligned16(work_w) && aligned16(z) && aligned16(z_out);
-    const int nv = vec ? V : 1;
-    // enough workgroups for 256 CUs: split the march into segments (no halo: w(p + 1) is a plain load)
-    const int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
-    int cseg = (int)((4096 + blocks - 1) / blocks);
-    if (cseg > g.n0) cseg = g.n0;
-    if (cseg < 1) cseg = 1;
-    pc.seg = (int)((g.n0 + cseg - 1) / cseg);
-    cseg = (int)((g.n0 + pc.seg - 1) / pc.seg);
-    int e;
-    if (vec)
-      e = pd3o ? launch_c<T, V, true>(pc, S.iso, M, cseg, work_w, z, z_out, st)
-               : launch_c<T, V, false>(pc, S.iso, M, cseg, work_w, z, z_out, st);
-    else
-      e = pd3o ? launch_c<T, 1, true>(pc, S.iso, M, cseg, work_w, z, z_out, st)
-               : launch_c<T, 1, false>(pc, S.iso, M, cseg, work_w, z, z_out, st);
-    if (e) return e;
-  }
+  if (const int e = run_c<T>(g, S.sigma, S.lam, S.rho, S.omr, pd3o, S.iso, work_w, z, z_out, st)) return e;
   if (evs) pds_event(3, st);
   return PXA_OK;
 }
@@ -473,6 +501,12 @@ int pxa_pds_step(int dtype, int algo, const int64_t* geom, const int32_t* ntaps,
   PXA_DISPATCH(dtype, T,
                return pds_entry<T>(algo, geom, ntaps, offs, coefs, diff, scal, prox, h_kind, x, u, z, hty, x_out, u_out,
                                    z_out, work_q, work_w, nseg, as_stream(stream)));
+}
+
+int pxa_tv_dual_update(int dtype, int relax, const int64_t* geom, const double* diff, double sigma, double lam,
+                       double rho, int h_kind, const void* w, const void* z, void* z_out, void* stream) {
+  PXA_DISPATCH(dtype, T,
+               return dual_entry<T>(relax, geom, diff, sigma, lam, rho, h_kind, w, z, z_out, as_stream(stream)));
 }
 
 int pxa_pds_step_la(int dtype, int algo, const int64_t* geom, const int32_t* ntaps, const int32_t* offs,

@@ -110,6 +110,9 @@ def gather_slabs(x_local, n_global, group=None):
     rank, w = world(group)
     if w == 1:
         return x_local
+    # the pad below copies by raw pointer and all_gather needs dense storage: permuted / strided views of a
+    # slab are made contiguous first
+    x_local = x_local.contiguous()
     sizes = [shard_range(n_global, r, w)[1] - shard_range(n_global, r, w)[0] for r in range(w)]
     if x_local.shape[0] != sizes[rank]:
         raise ValueError(f"rank {rank} holds {x_local.shape[0]} rows, expected {sizes[rank]}")

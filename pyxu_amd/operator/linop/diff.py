@@ -495,8 +495,37 @@ class _Directional(pxa.LinOp):
         self._w_host = np.ascontiguousarray(w.reshape(G, J, N) if per_pixel else w)
         self._w = to_device(self._w_host.reshape(-1))
         self._name = name
-        # sqrt(#groups) * max|w| * sqrt(J) * L(diff): the product bound of the reference's chain
-        self.lipschitz = float(np.sqrt(G) * np.max(np.abs(self._w_host)) * np.sqrt(J // K) * float(diff.lipschitz))
+        self.lipschitz = self._chain_lipschitz(self._w_host, G, J, K, float(diff.lipschitz))
+
+    @staticmethod
+    def _chain_lipschitz(w, G, J, K, L_diff):
+        """The Lipschitz constant the reference's ``Sum * DiagonalOp * diff`` chain carries (ChainRule:
+        product of the factors' constants, arithmetic.py:1190-1204, evaluated left to right):
+          * Sum over the J summed components: sqrt(J) (reduce.py:103-106);
+          * the diagonal part: one DiagonalOp per (group g, run of K consecutive terms) -- max|w|, or 0 / 1
+            when the weights are allclose to 0 / 1 (NullOp / IdentityOp, base.py:236-243, 330) -- stacked
+            vertically: sqrt(sum L_b^2), or sqrt(max L_b^2) when only the first block is non-zero
+            (blocks.py:684-708); a single block is the DiagonalOp itself (DirectionalDerivative);
+          * L(diff).
+        With J == 1 the reference's Sum is square and the composition loses its constant (inf): kept."""
+        if J == 1:
+            return float("inf")
+        Ls = []
+        for g in range(G):
+            for c in range(J // K):
+                blk = w[g, c * K:(c + 1) * K]
+                if np.allclose(blk, 0):
+                    Ls.append(0.0)
+                elif np.allclose(blk, 1):
+                    Ls.append(1.0)
+                else:
+                    Ls.append(float(np.abs(blk).max()))
+        if len(Ls) == 1:
+            L_dop = Ls[0]
+        else:
+            sq = np.array(Ls) ** 2
+            L_dop = float(np.sqrt(sq.max() if np.allclose(sq.sum(), sq[0]) else sq.sum()))
+        return float(np.sqrt(J)) * L_dop * L_diff
 
     def _weights(self, x):
         w = self._w

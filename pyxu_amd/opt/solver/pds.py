@@ -110,9 +110,21 @@ class _PrimalDualSplitting(pxa.Solver):
 
     def _primed(self, *state):
         """True iff the previous look-ahead step left the march of this iteration done for exactly
-        these state arrays (any restart or state replacement re-primes)."""
+        these state arrays, unmodified since (any restart or state replacement re-primes).  An array
+        edited in place through torch bumps its version counter, which is recorded with it; an edit that
+        bypasses torch (raw pointers) must call ``reset_lookahead()``."""
         la = self._la
-        return la is not None and len(la[0]) == len(state) and all(a is b for a, b in zip(la[0], state))
+        return (la is not None and len(la[0]) == len(state)
+                and all(a is b and v == getattr(b, "_version", v) for (a, v), b in zip(la[0], state)))
+
+    @staticmethod
+    def _la_key(*state):
+        return tuple((t, getattr(t, "_version", None)) for t in state)
+
+    def reset_lookahead(self):
+        """Forget the look-ahead march of the next iteration: the next m_step re-primes from the current
+        state.  Call after writing the solver state (``_mstate`` x / u / z) in place outside torch."""
+        self._la = None
 
     def _take_zspare(self, z):
         zs = self._zspare
@@ -213,7 +225,7 @@ class CondatVu(_PrimalDualSplitting):
                 _dev.pds_step_la(1, p["pre"], primed, x, None, z, p["hty"], out, None, z_out, p["q"], p["kt"], p["w"],
                                  nseg=p["nseg"])
                 mst["x"], mst["z"] = out, z_out
-                self._la = ((out, z_out), None)
+                self._la = (self._la_key(out, z_out), None)
                 self._spare = x if (sys.getrefcount(x) == 2 and _dev.storage_exclusive(x)) else None
                 self._zspare = z if (sys.getrefcount(z) == 2 and _dev.storage_exclusive(z)) else None
                 return
@@ -325,7 +337,7 @@ class PD3O(_PrimalDualSplitting):
                 _dev.pds_step_la(0, p["pre"], primed, x_cur, u, z, p["hty"], x_next, u_out, z_out, p["q"], None,
                                  p["w"], nseg=p["nseg"])
                 mst["x"], mst["u"], mst["z"] = x_cur, u_out, z_out
-                self._la = ((x_cur, u_out, z_out), x_next)
+                self._la = (self._la_key(x_cur, u_out, z_out), x_next)
                 del x_next, u_out
                 # the previous iterate's arrays are reused when nothing else holds them
                 self._spare = x if (x is not x_cur and sys.getrefcount(x) == 2 and _dev.storage_exclusive(x)) else None

@@ -1,0 +1,53 @@
+# usage: bash scripts/gpu_r04.sh <tag> <stage>
+# GPU calls of round 4.  Stages:
+#   new    the tests added this round, the k4 / dense_mfma records, the headline at the driver's flags,
+#          the counter list, k4 traffic and dense MFMA-busy passes
+#   full   the whole -m gpu suite, smoke, the default bench line
+#   prof   rocprofv3 kernel trace of the headline + the PMC passes of profiles/ (traffic, SQ, MFMA busy)
+# Test failures (rc 1) do not stop the run; any other failure (fault, abort, timeout) ends it there.
+set -o pipefail
+T=${1:-r04}
+S=${2:-new}
+O=gpurun_out/$T
+mkdir -p $O
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>: run with a time limit; stop the script unless rc in {0, 1}
+  local name=$1 lim=$2; shift 2
+  echo "== $name"
+  timeout -k 10 $lim "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -3 $O/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+PT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+P=$O/prof
+mkdir -p $P
+DRV="python3 bench.py --steps 20 --warmup 5 --no-sub --cpu-seconds 0"
+if [ "$S" = "new" ]; then
+  export PXA_PARITY_RECORD=$O/small_weights.jsonl
+  step newtests 900 $PT -m gpu tests/test_gpu_small_weights.py tests/test_gpu_directional.py tests/test_gpu_distributed.py \
+       tests/test_gpu_solver_engine.py "tests/test_gpu_pds_fused.py::test_tv_dual_update_vs_oracle"
+  unset PXA_PARITY_RECORD
+  step k4 300 python3 bench.py --only k4
+  step dense 300 python3 bench.py --only dense_mfma
+  step drv1 120 $DRV
+  step drv2 120 $DRV
+  step drv3 120 $DRV
+  step long 120 python3 bench.py --steps 200 --warmup 20 --no-sub --cpu-seconds 0
+  step list 120 rocprofv3 -L
+  for w in 2d 3d; do
+    step k4fetch$w 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/k4fetch$w -o run --output-format csv -- python3 bench.py --only k4 --k4-which $w
+    step k4write$w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/k4write$w -o run --output-format csv -- python3 bench.py --only k4 --k4-which $w
+  done
+  step mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d $P/mfma -o run --output-format csv -- python3 bench.py --only dense_mfma
+  python3 scripts/pmc_traffic.py $P/k4fetch2d $P/k4write2d "pds_dual_kernel" pds_dual_kernel@2048x2048 $P/traffic_k4.json $T || true
+  python3 scripts/pmc_traffic.py $P/k4fetch3d $P/k4write3d "pds_dual_kernel" pds_dual_kernel@1024x1024x1024 $P/traffic_k4.json $T || true
+  grep -h "" $O/small_weights.jsonl 2>/dev/null || true
+fi
+if [ "$S" = "full" ]; then
+  step pytest 1200 $PT tests -m gpu
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step bench 900 python bench.py --steps 20 --warmup 5
+fi
+echo done

@@ -201,8 +201,10 @@ def gpu_slab_ops(rank, world, shape):
             xa = op.adjoint(yl).reshape(2, hi - lo, M)
             Y = pd.gather_slabs(ya.permute(2, 0, 1, 3).contiguous(), shape[0]).permute(1, 2, 0, 3).reshape(2, K * N)
             X = pd.gather_slabs(xa.permute(1, 0, 2).contiguous(), shape[0]).permute(1, 0, 2).reshape(2, N)
+            # a permuted (non-contiguous) slab view, uneven shards (23 planes over 2 ranks): same result
+            X_nc = pd.gather_slabs(xa.permute(1, 0, 2), shape[0]).permute(1, 0, 2).reshape(2, N)
             full = make(shape)
-            out[name] = dict(apply=to_NUMPY(Y), adjoint=to_NUMPY(X), apply_ref=to_NUMPY(full.apply(to_device(x))),
+            out[name] = dict(apply=to_NUMPY(Y), adjoint=to_NUMPY(X), adjoint_nc=to_NUMPY(X_nc), apply_ref=to_NUMPY(full.apply(to_device(x))),
                              adjoint_ref=to_NUMPY(full.adjoint(to_device(y))))
     return out
 

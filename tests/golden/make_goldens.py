@@ -284,7 +284,8 @@ def gen_directional():
                     op = make_dir_op(pxo, kind, kw, dt)
                     x = rng.standard_normal((2, op.dim)).astype(dt)
                     z = rng.standard_normal((2, op.codim)).astype(dt)
-                    rec.update(x=x, y=op.apply(x), z=z, adj=op.adjoint(z), shape=np.array(op.shape), raises="")
+                    rec.update(x=x, y=op.apply(x), z=z, adj=op.adjoint(z), shape=np.array(op.shape), raises="",
+                               lipschitz=float(op.lipschitz))
                 except Exception as e:  # noqa: BLE001
                     rec.update(raises=f"{type(e).__name__}: {e}")
             save(f"directional_{w}_c{ci}", **rec)

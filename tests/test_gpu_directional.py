@@ -47,6 +47,12 @@ def test_directional_golden(name):
     assert y.dtype == dt and a.dtype == dt
     assert rel_err(y, g["y"]) <= TOL[dt], (kind, rel_err(y, g["y"]))
     assert rel_err(a, g["adj"]) <= TOL[dt], (kind, rel_err(a, g["adj"]))
+    # the step-size input of the PDS solvers: the reference's Lipschitz constant of the same operator
+    L_ref = float(g["lipschitz"])
+    if np.isinf(L_ref):
+        assert np.isinf(op.lipschitz), (kind, op.lipschitz)
+    else:
+        assert abs(float(op.lipschitz) - L_ref) <= 1e-6 * L_ref, (kind, float(op.lipschitz), L_ref)
 
 
 BIG = [

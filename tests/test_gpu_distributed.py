@@ -47,3 +47,4 @@ def test_slab_halo_ops_match_unsharded():
             o = res[r][name]
             assert rel_err(o["apply"], res[0][name]["apply_ref"]) <= 1e-6
             assert rel_err(o["adjoint"], res[0][name]["adjoint_ref"]) <= 1e-6
+            np.testing.assert_array_equal(o["adjoint_nc"], o["adjoint"])

@@ -71,7 +71,8 @@ def test_pgd_tv_512_100_iterations(g_kind):
 @pytest.mark.parametrize("algo", ["pd3o", "cv"])
 def test_pds_aniso_tv_128cube_20_iterations(algo):
     """PD3O / Condat-Vu at 128^3 (Gaussian(sigma=2) blur + 0.01 L1 o Grad, g = None), 20 iterations of the
-    fused three-launch step, x and z checked at k = 1, 10, 20."""
+    solver's default fused step (the look-ahead step, pxa_pds_step_la: kernel B + kernel D per iteration),
+    x and z checked at k = 1, 10, 20."""
     sh = (128, 128, 128)
     N = int(np.prod(sh))
     lam = 0.01

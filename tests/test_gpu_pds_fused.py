@@ -258,3 +258,30 @@ def test_pds_lookahead_two_positions_per_thread_bit_exact(algo):
         _dev.tuning(_dev.TUNE_PDS_MARCH, prev)
     for k in a:
         assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("h_kind", ["l1", "iso"])
+@pytest.mark.parametrize("sh", [(67, 129), (9, 33, 70), (5, 64, 128)], ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("relax", [0, 1])
+def test_tv_dual_update_vs_oracle(dt, h_kind, sh, relax):
+    """pxa_tv_dual_update (kernel C alone): relax(fenchel_prox_{sigma h}(z + sigma Grad w))
+    against the oracle's reference arithmetic (operator.py:905-944, diff.py:1113-1265; pds.py:760 / 441)."""
+    rng = np.random.default_rng(3)
+    N = int(np.prod(sh))
+    Dd = len(sh)
+    w = rng.standard_normal(N).astype(dt)
+    z = (0.05 * rng.standard_normal(Dd * N)).astype(dt)
+    sigma, lam, rho = 0.37, 0.05, 0.7
+    geom = (1, 1, *sh, 2) if Dd == 2 else (1, *sh, 3)
+    out = to_NUMPY(_dev.tv_dual_update(D(w), D(z), geom, [-1.0] * 3, [1.0] * 3, sigma, lam, rho,
+                                       0 if h_kind == "l1" else 1, relax=relax))
+    d = np.dtype(dt).type
+    if h_kind == "iso":
+        hp = lambda v, t: orc.l21_prox(v, t * d(lam), (Dd, *sh))
+    else:
+        hp = lambda v, t: orc.l1_prox(v, t * d(lam))
+    zin = z + d(sigma) * orc.gradient_apply(w, arg_shape=sh)
+    zt = orc.fenchel_prox(hp, zin, sigma)
+    ref = (d(1 - rho) * z + d(rho) * zt) if relax == 0 else (d(rho) * zt + d(1 - rho) * z)
+    assert rel_err(out, ref) <= TOL[dt], rel_err(out, ref)

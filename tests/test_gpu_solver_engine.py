@@ -135,3 +135,25 @@ def test_speculative_stop_checks_match_synchronous(stop_rate, mode, monkeypatch)
         if k == "duration":
             continue
         np.testing.assert_array_equal(h_s[k], h_n[k], err_msg=k)
+
+
+def test_async_log_lags_by_at_most_one_batch(tmp_path):
+    """ASYNC fit of the fused PGD with speculative checks at stop_rate 1: solver.log, read while the worker
+    runs, trails the iteration count by at most two record batches (Solver._RECORD_LAG lines written
+    unflushed), and holds every record's line once the solver stopped."""
+    lag = pxa.Solver._RECORD_LAG
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        f, g, N = _pgd_problem()
+        s = pxs.PGD(f=f, g=g, show_progress=False, folder=tmp_path / "l", stop_rate=1)
+        s.fit(x0=to_device(np.zeros(N, np.float32)), stop_crit=pxst.MaxIter(3000), mode=pxa.Mode.ASYNC)
+        assert s._plan is not None and s._spec_supported()
+        worst = 0
+        while s.busy():
+            before = s._astate["idx"]
+            lines = s.logfile.read_text().count("] Iteration ")
+            worst = max(worst, before - lines)
+            time.sleep(0.005)
+        s.stop()
+        _, h = s.stats()
+    assert worst <= 2 * lag + 4, worst
+    assert s.logfile.read_text().count("] Iteration ") == len(h["iteration"])

@@ -499,17 +499,48 @@ def test_distributed_device_path_has_no_torch_kernels():
 
 
 def test_pds_lookahead_priming_rule():
-    """The look-ahead PDS step reuses its march only for exactly the state arrays it left."""
+    """The look-ahead PDS step reuses its march only for exactly the state arrays it left, unmodified
+    (an in-place edit of the state between steps must re-prime)."""
+    import torch
+
     import pyxu_amd.opt.solver as pxs
 
     s = object.__new__(pxs.PD3O)
-    a, b, c, d = object(), object(), object(), object()
+    a, b, c, d = (torch.zeros(3) for _ in range(4))
     s._la = None
     assert not s._primed(a, b, c)
-    s._la = ((a, b, c), d)
+    s._la = (s._la_key(a, b, c), d)
     assert s._primed(a, b, c)
     assert not s._primed(a, b, d)  # a replaced z re-primes
     assert not s._primed(a, b)  # a different state layout
+    b.add_(1.0)  # the user edits u in place (MANUAL mode): its version counter moves
+    assert not s._primed(a, b, c)
+    s._la = (s._la_key(a, b, c), d)
+    assert s._primed(a, b, c)
+    s.reset_lookahead()
+    assert not s._primed(a, b, c)
     cv = object.__new__(pxs.CondatVu)
-    cv._la = ((a, b), None)
+    cv._la = (cv._la_key(a, b), None)
     assert cv._primed(a, b) and not cv._primed(b, a)
+
+
+def test_directional_lipschitz_chain_rule():
+    """The directional operators' Lipschitz constant is the reference's Sum * DiagonalOp * diff chain
+    product (diff.py:2171-2173; reduce.py:103-106; base.py:236-243, 330; blocks.py:684-708).  Values
+    below were printed by the reference in this container (fp64); the goldens carry the rest
+    (test_gpu_directional.py::test_directional_golden)."""
+    from pyxu_amd.operator.linop.diff import _Directional, _unit
+
+    L_grad2 = float(np.sqrt(8.0))  # forward-difference Gradient on a 2-D grid
+    chain = _Directional._chain_lipschitz
+    # DirectionalDerivative((7, 9), order 1, (0.3, -1.2)) -> 3.8805700005813275
+    w = _unit(np.array([0.3, -1.2]), np.float64)[None]
+    assert abs(chain(w, 1, 2, 2, L_grad2) - 3.8805700005813275) < 1e-12
+    # DirectionalDerivative((5, 6), order 1, (0, 1)): weights not allclose to 0 / 1 -> 4.000000000000001
+    w = _unit(np.array([0.0, 1.0]), np.float64)[None]
+    assert abs(chain(w, 1, 2, 2, L_grad2) - 4.0) < 1e-12
+    # DirectionalGradient((5, 6), [(1, 0), (0, 1)]): vstack of two DiagonalOps -> 5.6568542494923815
+    w = np.stack([_unit(np.array(d), np.float64) for d in ((1.0, 0.0), (0.0, 1.0))])
+    assert abs(chain(w, 2, 2, 2, L_grad2) - 5.6568542494923815) < 1e-12
+    # 1-D: the reference's square Sum loses the constant in the composition -> inf
+    assert np.isinf(chain(np.ones((1, 1)), 1, 1, 1, 2.0))
