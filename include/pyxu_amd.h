@@ -51,6 +51,9 @@ extern "C" {
 #define PXA_TUNE_PGD_KERNEL 0 /* reserved (kernel variants measured slower were removed; 0 = the tile kernel) */
 #define PXA_TUNE_NORMAL_DIAG 1 /* pxa_dense_normal timing probes (WRONG results, measurement only): 0 off,
                                   1 no x loads, 2 no cross-wave reduction, 3 no LDS accumulator */
+#define PXA_TUNE_DENSE_KERNEL 2 /* A/B of the fp32 MFMA dense path (pxa_dense_matmat, B >= 32): 0 the LDS-staged
+                                   kernel, 1 the register-streamed kernel of rounds 1-3 (same results up to
+                                   summation order) */
 #define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel: bit 5 s_memtime phase trace (pxa_pgd_tile_trace); timing
                               probes with WRONG results: bit 6 skips passes A / B, bit 7 the window loads, bit 8
                               loads x only (scripts/pgd_modes_probe.py diag) */

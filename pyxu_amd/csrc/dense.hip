@@ -263,6 +263,184 @@ __global__ void __launch_bounds__(kBlock) splitk_sum_kernel(int64_t n, int split
   }
 }
 
+// ---- LDS-staged MFMA GEMM (B >= kLdsMinB, 16-B aligned rows): the MFMA-bound regime of the dense LinOp.
+// A 256-thread workgroup owns a (64 BP) x 128 output tile -- all of a B <= 128 stack, so A is streamed from
+// HBM exactly once -- as 2 x 2 waves of (32 BP) x 64 (BP x 2 blocks of 32 x 32, one v_mfma_f32_32x32x2_f32
+// accumulator each).  K advances by kLdsKt = 32 per stage: the stage's X rows and A rows (apply: A[q][k],
+// k contiguous; adjoint: A[k][q], q contiguous) are copied global -> registers -> LDS (double-buffered,
+// one barrier per stage; the next stage's global loads are in flight during this stage's MFMAs).  Operand
+// fetch follows the fragment map above (lane half h takes k = 8 h + s of a 16-deep block, 8 consecutive k
+// per lane = two ds_read_b128 of a [row][k] image, row pitch 36 floats: conflict-free under the
+// MI355X_MICROARCH.md §LDS bank model, scripts/ldsbank.py; the adjoint's [k][q] image is read with
+// ds_read_b32, 32 consecutive q per lane group).  K is split over the workgroups of a 1-D grid with the
+// split index fastest, so that with 8 splits each XCD works on one K slice of X (L2-resident); the partial
+// products are summed in a fixed order by splitk_sum_kernel (deterministic run to run).
+constexpr int kLdsMinB = 32;
+constexpr int kLdsKt = 32;
+constexpr int kLdsPitch = kLdsKt + 4;  // [row][k] image pitch (floats)
+constexpr int kLdsQPitch = 128 + 4;    // [k][q] image pitch (adjoint's A)
+
+template <bool TRANS, int BP>
+struct LdsGemm {
+  static constexpr int PT = 64 * BP, QT = 128;
+  static constexpr int XS = PT * kLdsPitch;                               // floats per X stage
+  static constexpr int AS = TRANS ? kLdsKt * kLdsQPitch : QT * kLdsPitch;  // floats per A stage
+  static constexpr int XCH = PT * kLdsKt / 4 / 256;                       // 16-B X chunks per thread per stage
+  static constexpr int ACH = QT * kLdsKt / 4 / 256;                       // 16-B A chunks per thread per stage
+  static constexpr size_t LDS = (size_t)2 * (XS + AS) * sizeof(float);
+};
+
+template <bool TRANS, int BP>
+__global__ void __launch_bounds__(256, 2) mfma_lds_kernel(int64_t P, int64_t Q, int64_t K, int64_t kchunk, int splits,
+                                                          int gq, const float* __restrict__ X,
+                                                          const float* __restrict__ A, float* __restrict__ Y) {
+  using G = LdsGemm<TRANS, BP>;
+  extern __shared__ __align__(16) float lds[];
+  float* Xs = lds;               // [2][PT][kLdsPitch]
+  float* As = lds + 2 * G::XS;   // [2][QT][kLdsPitch] or [2][kLdsKt][kLdsQPitch]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+  const unsigned L = blockIdx.x;
+  const int z = (int)(L % (unsigned)splits);
+  const unsigned t = L / (unsigned)splits;
+  const int64_t q0 = (int64_t)(t % (unsigned)gq) * G::QT;
+  const int64_t p0 = (int64_t)(t / (unsigned)gq) * G::PT;
+  const int64_t kb = (int64_t)z * kchunk;
+  const int64_t ke = kb + kchunk < K ? kb + kchunk : K;
+  const int wp0 = (wave >> 1) * 32 * BP, wq0 = (wave & 1) * 64;
+
+  float4 xr[G::XCH], ar[G::ACH];  // one stage in flight, global -> registers
+  auto load_stage = [&](int64_t k0) {
+#pragma unroll
+    for (int u = 0; u < G::XCH; ++u) {
+      const int c = tid + 256 * u, row = c >> 3, part = c & 7;
+      const int64_t p = p0 + row, k = k0 + 4 * part;
+      xr[u] = (p < P && k < ke) ? *reinterpret_cast<const float4*>(X + p * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < G::ACH; ++u) {
+      const int c = tid + 256 * u;
+      if (!TRANS) {
+        const int row = c >> 3, part = c & 7;
+        const int64_t q = q0 + row, k = k0 + 4 * part;
+        ar[u] = (q < Q && k < ke) ? *reinterpret_cast<const float4*>(A + q * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const int kr = c >> 5, part = c & 31;
+        const int64_t k = k0 + kr, q = q0 + 4 * part;
+        ar[u] = (k < ke && q < Q) ? *reinterpret_cast<const float4*>(A + k * Q + q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  auto store_stage = [&](int buf) {
+    float* xs = Xs + buf * G::XS;
+    float* as = As + buf * G::AS;
+#pragma unroll
+    for (int u = 0; u < G::XCH; ++u) {
+      const int c = tid + 256 * u;
+      *reinterpret_cast<float4*>(xs + (c >> 3) * kLdsPitch + 4 * (c & 7)) = xr[u];
+    }
+#pragma unroll
+    for (int u = 0; u < G::ACH; ++u) {
+      const int c = tid + 256 * u;
+      if (!TRANS)
+        *reinterpret_cast<float4*>(as + (c >> 3) * kLdsPitch + 4 * (c & 7)) = ar[u];
+      else
+        *reinterpret_cast<float4*>(as + (c >> 5) * kLdsQPitch + 4 * (c & 31)) = ar[u];
+    }
+  };
+
+  f32x16 acc[BP][2];
+#pragma unroll
+  for (int bp = 0; bp < BP; ++bp)
+#pragma unroll
+    for (int bq = 0; bq < 2; ++bq)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[bp][bq][r] = 0.f;
+
+  load_stage(kb);
+  store_stage(0);
+  __syncthreads();
+  int buf = 0;
+  for (int64_t k0 = kb; k0 < ke; k0 += kLdsKt) {
+    const bool next = k0 + kLdsKt < ke;
+    if (next) load_stage(k0 + kLdsKt);
+    const float* xs = Xs + buf * G::XS;
+    const float* as = As + buf * G::AS;
+#pragma unroll
+    for (int k16 = 0; k16 < kLdsKt; k16 += 16) {
+      float xf[BP][8], af[2][8];
+#pragma unroll
+      for (int bp = 0; bp < BP; ++bp) {
+        const float* src = xs + (wp0 + 32 * bp + r32) * kLdsPitch + k16 + 8 * h;
+        const float4 lo = *reinterpret_cast<const float4*>(src), hi = *reinterpret_cast<const float4*>(src + 4);
+        xf[bp][0] = lo.x; xf[bp][1] = lo.y; xf[bp][2] = lo.z; xf[bp][3] = lo.w;
+        xf[bp][4] = hi.x; xf[bp][5] = hi.y; xf[bp][6] = hi.z; xf[bp][7] = hi.w;
+      }
+#pragma unroll
+      for (int bq = 0; bq < 2; ++bq) {
+        if (!TRANS) {
+          const float* src = as + (wq0 + 32 * bq + r32) * kLdsPitch + k16 + 8 * h;
+          const float4 lo = *reinterpret_cast<const float4*>(src), hi = *reinterpret_cast<const float4*>(src + 4);
+          af[bq][0] = lo.x; af[bq][1] = lo.y; af[bq][2] = lo.z; af[bq][3] = lo.w;
+          af[bq][4] = hi.x; af[bq][5] = hi.y; af[bq][6] = hi.z; af[bq][7] = hi.w;
+        } else {
+#pragma unroll
+          for (int s = 0; s < 8; ++s) af[bq][s] = as[(k16 + 8 * h + s) * kLdsQPitch + wq0 + 32 * bq + r32];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int bp = 0; bp < BP; ++bp)
+#pragma unroll
+          for (int bq = 0; bq < 2; ++bq)
+            acc[bp][bq] = __builtin_amdgcn_mfma_f32_32x32x2f32(xf[bp][s], af[bq][s], acc[bp][bq], 0, 0, 0);
+    }
+    if (next) store_stage(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  float* Yz = Y + (int64_t)z * P * Q;
+#pragma unroll
+  for (int bp = 0; bp < BP; ++bp)
+#pragma unroll
+    for (int bq = 0; bq < 2; ++bq) {
+      const int64_t q = q0 + wq0 + 32 * bq + r32;
+      if (q >= Q) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = p0 + wp0 + 32 * bp + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < P) Yz[row * Q + q] = acc[bp][bq][r];
+      }
+    }
+}
+
+struct LdsPlan {
+  int bp, gq;
+  int64_t tiles, splits, kchunk;
+};
+
+inline LdsPlan lds_plan(int64_t P, int64_t Q, int64_t K) {
+  LdsPlan m;
+  m.bp = P > 64 ? 2 : 1;
+  const int64_t pt = 64 * m.bp;
+  m.gq = (int)((Q + 127) / 128);
+  m.tiles = m.gq * ((P + pt - 1) / pt);
+  int64_t splits = (512 + m.tiles - 1) / m.tiles;  // two workgroups per CU
+  const int64_t max_splits = (K + 511) / 512;      // >= 512 k (16 stages) per slice
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  m.kchunk = ((K + splits - 1) / splits + kLdsKt - 1) / kLdsKt * kLdsKt;
+  m.splits = (K + m.kchunk - 1) / m.kchunk;
+  return m;
+}
+
+// the LDS kernel's operand contract: whole 16-B chunks of rows (X, A) everywhere, at most 128 stacked rows
+// per workgroup column
+inline bool lds_ok(bool trans, int64_t P, int64_t Q, int64_t K, const float* X, const float* A) {
+  return P >= kLdsMinB && P <= 1024 && aligned16(X) && aligned16(A) && K % 4 == 0 && (!trans || Q % 4 == 0);
+}
+
 struct MfmaPlan {
   int ptl;
   int64_t gx, gy, splits, kchunk;
@@ -283,9 +461,35 @@ inline MfmaPlan mfma_plan(int64_t P, int64_t Q, int64_t K) {
   return m;
 }
 
+template <bool TRANS, int BP>
+int launch_lds(const LdsPlan& m, int64_t P, int64_t Q, int64_t K, const float* X, const float* A, float* out,
+               hipStream_t s) {
+  using G = LdsGemm<TRANS, BP>;
+  auto kern = mfma_lds_kernel<TRANS, BP>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+    attr = true;
+  }
+  const int64_t blocks = m.tiles * m.splits;
+  if (blocks > 0x7fffffff) return PXA_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), G::LDS, s, P, Q, K, m.kchunk, (int)m.splits, m.gq, X, A,
+                     out);
+  return last_launch_status();
+}
+
 template <bool TRANS>
 int launch_mfma(int64_t P, int64_t Q, int64_t K, const float* X, const float* A, float* Y, float* work,
                 hipStream_t s) {
+  if (lds_ok(TRANS, P, Q, K, X, A) && tuning(PXA_TUNE_DENSE_KERNEL) == 0) {
+    const LdsPlan m = lds_plan(P, Q, K);
+    float* out = m.splits > 1 ? work : Y;
+    if (m.splits > 1 && work == nullptr) return PXA_ERR_ARG;
+    const int e = m.bp == 2 ? launch_lds<TRANS, 2>(m, P, Q, K, X, A, out, s) : launch_lds<TRANS, 1>(m, P, Q, K, X, A, out, s);
+    if (e || m.splits == 1) return e;
+    hipLaunchKernelGGL(splitk_sum_kernel, dim3(grid_for(P * Q)), dim3(kBlock), 0, s, P * Q, (int)m.splits, work, Y);
+    return last_launch_status();
+  }
   const MfmaPlan m = mfma_plan(P, Q, K);
   const bool vec = aligned16(X) && (K % 4 == 0) && (TRANS || aligned16(A));
   float* out = m.splits > 1 ? work : Y;

@@ -27,10 +27,12 @@ DRV="python3 bench.py --steps 20 --warmup 5 --no-sub --cpu-seconds 0"
 if [ "$S" = "new" ]; then
   export PXA_PARITY_RECORD=$O/small_weights.jsonl
   step newtests 900 $PT -m gpu tests/test_gpu_small_weights.py tests/test_gpu_directional.py tests/test_gpu_distributed.py \
-       tests/test_gpu_solver_engine.py "tests/test_gpu_pds_fused.py::test_tv_dual_update_vs_oracle"
+       tests/test_gpu_solver_engine.py "tests/test_gpu_pds_fused.py::test_tv_dual_update_vs_oracle" \
+       "tests/test_gpu_parity.py::test_dense_mfma_vs_fp64" "tests/test_gpu_parity.py::test_dense_lds_kernel_matches_register_kernel"
   unset PXA_PARITY_RECORD
   step k4 300 python3 bench.py --only k4
   step dense 300 python3 bench.py --only dense_mfma
+  step densereg 300 python3 scripts/bench_dense.py
   step drv1 120 $DRV
   step drv2 120 $DRV
   step drv3 120 $DRV

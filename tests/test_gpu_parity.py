@@ -24,6 +24,7 @@ import pyxu_amd.operator as pxo  # noqa: E402
 import pyxu_amd.opt.solver as pxs  # noqa: E402
 import pyxu_amd.opt.stop as pxst  # noqa: E402
 import pyxu_amd.runtime as pxrt  # noqa: E402
+from pyxu_amd import _dev  # noqa: E402
 from pyxu_amd.util import to_device, to_NUMPY  # noqa: E402
 
 OP_TOL = {np.float32: 1e-5, np.float64: 1e-12}
@@ -137,8 +138,10 @@ def test_dense_golden(name):
         assert rel_err(to_NUMPY(op.adjoint(D(g["z"]))), g["adj"]) <= OP_TOL[dt] * 10
 
 
-@pytest.mark.parametrize("B", [2, 9, 32, 33, 64])  # MFMA path: one and two 32-row tiles per wave, ragged
-@pytest.mark.parametrize("MN", [(96, 640), (300, 1030), (2048, 4096)])  # ragged Q / K, split-K
+# MFMA paths: the register-streamed kernel (B < 32, or rows not in whole 16-B chunks) and the LDS-staged
+# kernel (B >= 32: 64- and 128-row workgroup tiles, several P tiles at B = 161, ragged P / Q, split-K)
+@pytest.mark.parametrize("B", [2, 9, 32, 33, 64, 100, 128, 161])
+@pytest.mark.parametrize("MN", [(96, 640), (300, 1030), (260, 1028), (2048, 4096)])
 def test_dense_mfma_vs_fp64(MN, B):
     """fp32 matrix-core path of _ExplicitLinOp (B >= 2 stacked inputs) vs an fp64 host product.
     fp32 sums over K terms carry ~sqrt(K) eps inherent error (SURVEY App. A #13): norm-wise 1e-5."""
@@ -158,6 +161,27 @@ def test_dense_mfma_vs_fp64(MN, B):
     with pxrt.Precision(pxrt.Width.SINGLE):
         y1 = to_NUMPY(op.apply(D(X[-1])))
     assert rel_err(y[-1], y1) <= 1e-5
+
+
+@pytest.mark.parametrize("trans", [0, 1])
+def test_dense_lds_kernel_matches_register_kernel(trans):
+    """PXA_TUNE_DENSE_KERNEL A/B: the LDS-staged MFMA kernel and the register-streamed one compute the same
+    product (fp32, different summation split): norm-wise 1e-6 apart, both within 1e-5 of fp64."""
+    M, N, B = 1024, 8192, 128
+    rng = np.random.default_rng(9)
+    A = rng.standard_normal((M, N)).astype(np.float32)
+    X = rng.standard_normal((B, M if trans else N)).astype(np.float32)
+    Ad, Xd = D(A), D(X)
+    out = {}
+    for knob in (0, 1):
+        prev = _dev.tuning(_dev.TUNE_DENSE_KERNEL, knob)
+        try:
+            out[knob] = to_NUMPY(_dev.dense_matmat(Ad, Xd, trans))
+        finally:
+            _dev.tuning(_dev.TUNE_DENSE_KERNEL, prev)
+    ref = X.astype(np.float64) @ (A.astype(np.float64) if trans else A.astype(np.float64).T)
+    assert rel_err(out[0], ref) <= 1e-5 and rel_err(out[1], ref) <= 1e-5
+    assert rel_err(out[0], out[1]) <= 1e-6
 
 
 # ----------------------------------------------------------------------------- solver trajectories
