@@ -723,7 +723,7 @@ def bench_dense_mfma(ctx, args):
     for B in args.mfma_b:
         for name, trans in (("apply", 0), ("adjoint", 1)):
             X = torch.randn((B, M if trans else N), generator=gen, device="cuda", dtype=torch.float32)
-            ms = _event_ms(lambda: _dev.dense_matmat(A, X, trans), 5)
+            ms = _event_ms(lambda: _dev.dense_matmat(A, X, trans), 20, warm=5)
             tf = 2.0 * M * N * B / (ms * 1e-3) / 1e12
             out[f"{name}_b{B}"] = {"B": B, "kernel_ms": round(ms, 4), "tflops": round(tf, 2),
                                    "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TF,

@@ -54,15 +54,17 @@ extern "C" {
 #define PXA_TUNE_DENSE_KERNEL 2 /* A/B of the fp32 MFMA dense path (pxa_dense_matmat, B >= 32): 0 the LDS-staged
                                    kernel, 1 the register-streamed kernel of rounds 1-3 (same results up to
                                    summation order) */
-#define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel: bit 5 s_memtime phase trace (pxa_pgd_tile_trace); timing
-                              probes with WRONG results: bit 6 skips passes A / B, bit 7 the window loads, bit 8
-                              loads x only (scripts/pgd_modes_probe.py diag) */
-#define PXA_TUNE_PGD_STAGGER 6 /* fused PGD tile kernel A/B probe: v = (sel << 8) | n delays the workgroups
-                                  picked by `sel` in the first dispatch round by n x 1024 cycles (s_sleep) */
+#define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel, PROBE BUILD ONLY (make -C pyxu_amd/csrc probe; the production
+                              library ignores it): bit 5 s_memtime phase trace (pxa_pgd_tile_trace); timing probes
+                              with WRONG results: bit 6 skips passes A / B, bit 7 the window loads, bit 8 loads x only
+                              (scripts/pgd_modes_probe.py diag) */
+#define PXA_TUNE_PGD_STAGGER 6 /* fused PGD tile kernel A/B probe, PROBE BUILD ONLY: v = (sel << 8) | n delays the
+                                  workgroups picked by `sel` in the first dispatch round by n x 1024 cycles */
 #define PXA_TUNE_PDS_EVENTS 5 /* measurement hook: > 0 makes pxa_pds_step record HIP events around each
                                  of its kernels (pxa_pds_kernel_ms) */
-#define PXA_TUNE_PDS_MARCH 7 /* A/B of pxa_pds_step_la's kernel D: bit 0 lets a thread own two positions
-                                (default one) */
+#define PXA_TUNE_PDS_MARCH 7 /* A/B of the PDS dual-update kernels: bit 0 lets kernel D's threads own two
+                                positions (default one); bit 1 turns off the non-temporal policy of the
+                                read-once / write-once streams of kernels C and D (default on) */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */

@@ -60,7 +60,7 @@ __device__ inline void ldv(const T* p, T (&v)[NV]) {
 // axis-0 forward neighbour w(p + 1) is loaded once and carried to the next step.  The in-plane block
 // index is XCD-banded (tile2d::xcd_tile) so that the row+1 neighbour is usually read from the L2 of the
 // same XCD, where the neighbouring block marches in step.
-template <typename T, int NV, bool ISO, bool PD3O>
+template <typename T, int NV, bool ISO, bool PD3O, bool NT>
 __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __restrict__ w,
                                                           const T* __restrict__ z, T* __restrict__ zo) {
   const PdsGeom<T> g = p.g;
@@ -112,7 +112,10 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
         for (int e = 0; e + 1 < NV; ++e) wn[e] = wc[e + 1];
         wn[NV - 1] = col_nb ? ws[off + NV] : T(0);
       }
-      ldv<T, NV>(zs + (int64_t)(ax - a_first) * N + off, zc[ax]);
+      if (NT)
+        ldn_nt<T, NV>(zs + (int64_t)(ax - a_first) * N + off, zc[ax]);
+      else
+        ldv<T, NV>(zs + (int64_t)(ax - a_first) * N + off, zc[ax]);
 #pragma unroll
       for (int e = 0; e < NV; ++e) zin[ax][e] = dual_in<T>(zc[ax][e], wc[e], wn[e], g.c0[ax], g.c1[ax], sigma);
     }
@@ -138,7 +141,9 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
 #pragma unroll
       for (int e = 0; e < NV; ++e) zn[e] = zo3[ax][e];
       T* zq = zos + (int64_t)(ax - a_first) * N + off;
-      if constexpr (NV == kVecN<T>)
+      if (NT)
+        stn_nt<T, NV>(zq, zn);
+      else if constexpr (NV == kVecN<T>)
         *reinterpret_cast<typename Vec4<T>::type*>(zq) = *reinterpret_cast<const typename Vec4<T>::type*>(zn);
       else
         zq[0] = zn[0];
@@ -151,11 +156,18 @@ int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, co
              hipStream_t st) {
   const int64_t blocks = (M + (int64_t)kBlock * NV - 1) / ((int64_t)kBlock * NV);
   dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pc.g.stack);
-  if (iso)
-    hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+  const bool nt = (tuning(PXA_TUNE_PDS_MARCH) & 2) == 0;
+  if (iso && nt)
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O, true>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+                       (const T*)z, (T*)zo);
+  else if (iso)
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O, false>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+                       (const T*)z, (T*)zo);
+  else if (nt)
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O, true>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
                        (const T*)z, (T*)zo);
   else
-    hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+    hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O, false>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
                        (const T*)z, (T*)zo);
   return last_launch_status();
 }

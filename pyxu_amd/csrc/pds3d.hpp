@@ -59,6 +59,33 @@ __device__ inline void stn(T* p, const T (&v)[NP]) {
   }
 }
 
+// Non-temporal (streaming) forms of ldn / stn for arrays a kernel reads or writes exactly once: they do not
+// displace the re-read neighbour rows (w at row + 1 / row - 1) from the XCD's 4 MB L2, which 128 marching
+// workgroups per XCD otherwise turn over within about one plane.
+template <typename T, int NP>
+__device__ inline void ldn_nt(const T* p, T (&v)[NP]) {
+  if constexpr (NP == 1) {
+    v[0] = __builtin_nontemporal_load(p);
+  } else {
+    typedef T vt __attribute__((ext_vector_type(NP)));
+    const vt r = __builtin_nontemporal_load(reinterpret_cast<const vt*>(p));
+#pragma unroll
+    for (int i = 0; i < NP; ++i) v[i] = r[i];
+  }
+}
+template <typename T, int NP>
+__device__ inline void stn_nt(T* p, const T (&v)[NP]) {
+  if constexpr (NP == 1) {
+    __builtin_nontemporal_store(v[0], p);
+  } else {
+    typedef T vt __attribute__((ext_vector_type(NP)));
+    vt r;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) r[i] = v[i];
+    __builtin_nontemporal_store(r, reinterpret_cast<vt*>(p));
+  }
+}
+
 // ------------------------------------------------------------------ dual update of one position
 // z_new = relax(fenchel_prox_h(z + sigma K w)) for the directions a_first..2 of one position; kernels C
 // and D both go through these helpers, so the three-launch and the look-ahead steps produce the same bits.

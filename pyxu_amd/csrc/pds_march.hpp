@@ -25,7 +25,7 @@ struct PdsD {
   T sigma, lam, rho, omr;
 };
 
-template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL>
+template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT>
 __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T* __restrict__ w,
                                                               const T* __restrict__ z, const T* __restrict__ src,
                                                               T* __restrict__ zo, T* __restrict__ ao,
@@ -180,7 +180,10 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
           if (a < a_first) continue;
-          stn<T, NP>(zw + (int64_t)(a - a_first) * N + off, zn[a]);
+          if (NT)
+            stn_nt<T, NP>(zw + (int64_t)(a - a_first) * N + off, zn[a]);
+          else
+            stn<T, NP>(zw + (int64_t)(a - a_first) * N + off, zn[a]);
         }
       }
     } else {
@@ -215,14 +218,30 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
     T(&v)[NP] = r.v;
     if constexpr (PD3O) {
       T u[NP];
-      ldn<T, NP>(in + off, u);
+      if (NT)
+        ldn_nt<T, NP>(in + off, u);
+      else
+        ldn<T, NP>(in + off, u);
       const T one = T(1), mtau = -tau;
 #pragma unroll
       for (int k = 0; k < NP; ++k) v[k] = apply_prox<T>(prox, fma(mtau, kt[k], one * u[k]), pw);
-      if (mine) stn<T, NP>(aw + off, v);
+      if (mine) {
+        if (NT)
+          stn_nt<T, NP>(aw + off, v);
+        else
+          stn<T, NP>(aw + off, v);
+      }
     } else {
-      ldn<T, NP>(in + off, v);
-      if (mine) stn<T, NP>(aw + off, kt);
+      if (NT)
+        ldn_nt<T, NP>(in + off, v);
+      else
+        ldn<T, NP>(in + off, v);
+      if (mine) {
+        if (NT)
+          stn_nt<T, NP>(aw + off, kt);
+        else
+          stn<T, NP>(aw + off, kt);
+      }
     }
     return r;
   };
@@ -281,7 +300,10 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
         for (int t = 0; t < RING; ++t)
 #pragma unroll
           for (int k = 0; k < NP; ++k) acc[k] = fma(k0[t], rh[2 * R0 - t][k], acc[k]);
-        stn<T, NP>(qw + (int64_t)i * M, acc);
+        if (NT)
+          stn_nt<T, NP>(qw + (int64_t)i * M, acc);
+        else
+          stn<T, NP>(qw + (int64_t)i * M, acc);
       }
     }
   }
@@ -294,14 +316,23 @@ int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, cons
   // one position per thread by default (occupancy 7 against 4 with two: faster at 1024^3,
   // profiles/r03z_pds_march_ring_ab.txt); PXA_TUNE_PDS_MARCH bit 0 allows two (A/B)
   if (!(tuning(PXA_TUNE_PDS_MARCH) & 1)) np = 1;
+  // read-once / write-once streams (src, z_out, x_out or K^T z_out, Q) non-temporal so that the re-read
+  // neighbour rows of w and z stay in L2; PXA_TUNE_PDS_MARCH bit 1 turns that off (A/B)
+  const bool nt = (tuning(PXA_TUNE_PDS_MARCH) & 2) == 0;
   const int64_t blocks = (M + (int64_t)kAThreads * np - 1) / ((int64_t)kAThreads * np);
   dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pd.a.g.stack);
-  if (np == 2)
-    hipLaunchKernelGGL((pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL>), grid, dim3(kAThreads), 0, st, pd, (const T*)w,
-                       (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
+  if (np == 2 && nt)
+    hipLaunchKernelGGL((pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL, true>), grid, dim3(kAThreads), 0, st, pd,
+                       (const T*)w, (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
+  else if (np == 2)
+    hipLaunchKernelGGL((pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL, false>), grid, dim3(kAThreads), 0, st, pd,
+                       (const T*)w, (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
+  else if (nt)
+    hipLaunchKernelGGL((pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true>), grid, dim3(kAThreads), 0, st, pd,
+                       (const T*)w, (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
   else
-    hipLaunchKernelGGL((pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL>), grid, dim3(kAThreads), 0, st, pd, (const T*)w,
-                       (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
+    hipLaunchKernelGGL((pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, false>), grid, dim3(kAThreads), 0, st, pd,
+                       (const T*)w, (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
   return last_launch_status();
 }
 

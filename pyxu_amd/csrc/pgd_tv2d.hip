@@ -34,10 +34,18 @@
 // contiguous band of tiles so that halo re-reads of x / x_prev hit its own L2.
 #include "tile2d.hpp"
 
+// Measurement probes (s_memtime phase trace, skip probes, staggered starts: PXA_TUNE_PGD_DIAG /
+// PXA_TUNE_PGD_STAGGER) exist only in the probe build (`make -C pyxu_amd/csrc probe`, scripts/ that time
+// kernel phases); the production library compiles them out, so its kernel carries no probe branch.
+#ifndef PXA_PGD_PROBES
+#define PXA_PGD_PROBES 0
+#endif
+
 namespace pxa {
 namespace {
 
 using namespace tile2d;
+constexpr bool kProbes = PXA_PGD_PROBES != 0;
 
 
 template <typename T>
@@ -111,7 +119,7 @@ __device__ inline void win_issue(const PgdParams<T>& p, int ty0, int tx0, const 
       if (!EDGE) {
         const unsigned off = (unsigned)(gr * n1 + gc);
         ld_vec<T, V>(xs + off, w.xv[k]);
-        if (p.diag & 256) {  // timing probe only (WRONG results): one window array instead of two
+        if (kProbes && (p.diag & 256)) {  // timing probe only (WRONG results): one window array instead of two
 #pragma unroll
           for (int v = 0; v < V; ++v) w.pv[k][v] = w.xv[k][v];
         } else {
@@ -412,13 +420,13 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   }
   double part_d = 0.0, part_x = 0.0;
   const bool want_part = partials != nullptr;
-  const bool tracing = (p.diag & 32) != 0;
+  const bool tracing = kProbes && (p.diag & 32) != 0;
   unsigned long long* ts = reinterpret_cast<unsigned long long*>(smem + kGhOff<T, R> + kGhBytes<T, R>);
   auto tmark = [&](int pt) {
     if (tracing && (tid & 63) == 0) ts[(tid >> 6) * 8 + pt] = clock64();
   };
   tmark(0);
-  if (p.diag & 128) {  // timing probe only (WRONG results): no window loads, yk = 0
+  if (kProbes && (p.diag & 128)) {  // timing probe only (WRONG results): no window loads, yk = 0
     for (int i = tid; i < L::AR * L::AP; i += kThreads) A[i] = T(0);
   } else {
     load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
@@ -426,7 +434,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   tmark(1);
   __syncthreads();
   tmark(2);
-  const bool skip_passes = (p.diag & 64) != 0;  // timing probe only (WRONG results)
+  const bool skip_passes = kProbes && (p.diag & 64) != 0;  // timing probe only (WRONG results)
   if (!skip_passes) pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
   tmark(3);
   __syncthreads();
@@ -504,7 +512,7 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  if (p.stagger && blockIdx.x < p.round1) {
+  if (kProbes && p.stagger && blockIdx.x < p.round1) {
     const unsigned sel = (unsigned)p.stagger >> 8, b = blockIdx.x >> 3;  // b: index within the XCD
     const bool late = sel == 1 ? (b & 1u) : sel == 2 ? ((b >> 1) & 1u) : sel == 3 ? ((b >> 2) & 1u) : ((b >> 5) & 1u);
     if (late)
@@ -616,8 +624,8 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new);
   p.tv = lam != 0.0;
   p.prox = prox;
-  p.diag = tuning(PXA_TUNE_PGD_DIAG);
-  p.stagger = tuning(PXA_TUNE_PGD_STAGGER);
+  p.diag = kProbes ? tuning(PXA_TUNE_PGD_DIAG) : 0;
+  p.stagger = kProbes ? tuning(PXA_TUNE_PGD_STAGGER) : 0;
   p.round1 = 4u * 256u;
   int st;
   switch (R) {
@@ -644,6 +652,7 @@ extern "C" {
 int pxa_pgd_tv2d_last_kernel(void) { return g_last_pgd_kernel; }
 
 int pxa_pgd_tile_trace(uint64_t* host_out, int n) {
+  if (!kProbes) return PXA_ERR_UNSUPPORTED;  // the phase trace exists only in the probe build
   if (!host_out || n < 0 || n > kTraceWords) return PXA_ERR_ARG;
   if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tile_trace), (size_t)n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
     return PXA_ERR_UNSUPPORTED;

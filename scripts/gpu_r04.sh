@@ -47,6 +47,20 @@ if [ "$S" = "new" ]; then
   python3 scripts/pmc_traffic.py $P/k4fetch3d $P/k4write3d "pds_dual_kernel" pds_dual_kernel@1024x1024x1024 $P/traffic_k4.json $T || true
   grep -h "" $O/small_weights.jsonl 2>/dev/null || true
 fi
+if [ "$S" = "ab1" ]; then
+  step pdstests 600 $PT -m gpu tests/test_gpu_pds_fused.py tests/test_gpu_long_trajectories.py -k "pds or dual"
+  step ntab 600 python3 scripts/nt_ab_probe.py 1024 2
+  step gaptrace 300 rocprofv3 --kernel-trace -d $P/gap -o run --output-format csv -- python3 scripts/driver_gap_probe.py 20 5
+  python3 scripts/driver_gap_probe.py 20 5 > /dev/null 2>&1 || true
+  step k4fetch3d 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/k4fetch3d -o run --output-format csv -- python3 bench.py --only k4 --k4-which 3d
+  step k4write3d 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/k4write3d -o run --output-format csv -- python3 bench.py --only k4 --k4-which 3d
+  python3 scripts/pmc_traffic.py $P/k4fetch3d $P/k4write3d "pds_dual_kernel" pds_dual_kernel@1024x1024x1024 $P/traffic_k4.json $T || true
+  B3="python3 bench.py --only c3 --c3-steps 3"
+  step fetchc3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetchc3 -o run --output-format csv -- $B3
+  step writec3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writec3 -o run --output-format csv -- $B3
+  python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, true, false, true, true>" pds_march_kernel_pd3o@1024^3 $P/traffic_c3.json $T || true
+  python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, false, false, true, true>" pds_march_kernel_cv@1024^3 $P/traffic_c3.json $T || true
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
