@@ -389,7 +389,9 @@ int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int6
  * images, each (n0, n1), contiguous; image s uses data image (s % y_images) of hty (1 = one y shared
  * by a stack of initial points, stack = batch-as-axis images with their own data).  x_new must not
  * alias x or x_prev.  If `partials` is not NULL, each (tile, wavefront) slot writes (sum (x_new-x)^2,
- * sum x^2) for RelError into partials[2*slot..] (double) — pxa_pgd_tv2d_partials_count() gives the
+ * sum x^2) for RelError into partials[2*slot..] (double); with x_ref != NULL the statistics are taken against
+ * x_ref instead of x, i.e. (sum (x_new-x_ref)^2, sum x_ref^2): RelError at stop_rate > 1 compares with the
+ * iterate of the previous check (opt/stop.py:353-382) — pxa_pgd_tv2d_partials_count() gives the
  * number of slots (tiles x 4; the slots of one image are contiguous).  prox codes: 0 none, 1 positive
  * orthant, 2 l1 with weight prox_w.  pxa_pgd_tv2d_last_kernel() is 1 once the calling thread has
  * launched the tile kernel (0 before).
@@ -402,7 +404,8 @@ int pxa_pgd_tile_trace(uint64_t* host_out, int n);
 int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
                       const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
-                      const void* x_prev, const void* hty, void* x_new, double* partials, void* stream);
+                      const void* x_prev, const void* hty, void* x_new, double* partials, const void* x_ref,
+                      void* stream);
 
 
 /* ---------------------------------------------------------------------------------------------

@@ -23,10 +23,12 @@ def _torch():
     return torch
 
 
-def wait_event(ev, spin_s=1e-4):
-    """Wait for a recorded HIP event: poll it for up to `spin_s` seconds (a stop check usually waits a few
-    tens of microseconds, and a blocking hipEventSynchronize wakes the host up later than a poll notices
-    the event), then yield the GIL between polls so that a long wait does not starve other threads."""
+def wait_event(ev, spin_s=1e-3):
+    """Wait for a recorded HIP event: poll it for up to `spin_s` seconds, then yield between polls so that a
+    long wait does not starve other threads.  A stop check waits for the device queue the host has run ahead
+    by (stop_rate x the step time at most: ~0.25 ms at 20 PGD steps of 2048^2), and the step enqueued
+    behind the check covers only one step time after the event: a blocking hipEventSynchronize, or a
+    sleep(0) between polls, wakes the host up tens of microseconds late and leaves the device idle."""
     import time
 
     if ev.query():
@@ -779,8 +781,9 @@ def pgd_tv2d_args(stack, y_images, n0, n1, taps0, taps1, h0, h1, lam, mu, prox, 
 
 
 def pgd_tv2d_step(x, x_prev, hty, x_new, stack, y_images, n0, n1, taps0, taps1, h0, h1, lam, mu, a, tau, prox, prox_w, partials=None,
-                  pre=None):
-    """One fused PGD iteration (pxa_pgd_tv2d_step).  `pre`: pgd_tv2d_args(...) cached by the caller."""
+                  pre=None, x_ref=None):
+    """One fused PGD iteration (pxa_pgd_tv2d_step).  `pre`: pgd_tv2d_args(...) cached by the caller.  With
+    `partials`, the per-tile RelError statistics are taken against `x_ref` (None: against x)."""
     if pre is None:
         pre = pgd_tv2d_args(stack, y_images, n0, n1, taps0, taps1, h0, h1, lam, mu, prox, prox_w)
     ev = _TIMER.begin() if _TIMER is not None else None  # measurement hook (bench.py), normally None
@@ -788,7 +791,7 @@ def pgd_tv2d_step(x, x_prev, hty, x_new, stack, y_images, n0, n1, taps0, taps1, 
         lib.pxa_pgd_tv2d_step(
             dtcode(x), *pre, float(a), float(tau), int(prox), float(prox_w),
             x.data_ptr(), x_prev.data_ptr(), hty.data_ptr(), x_new.data_ptr(), ptr(partials) if partials is not None else None,
-            stream(),
+            x_ref.data_ptr() if x_ref is not None else None, stream(),
         ),
         "pxa_pgd_tv2d_step",
     )

@@ -81,7 +81,7 @@ EXPORTS = {
     "pxa_pgd_tv2d_step": (
         i32,
         [i32, i64, i64, i64, i64, i32, P_i32, P_f64, i32, P_i32, P_f64, f64, f64, f64, f64, f64, f64, i32, f64,
-         vp, vp, vp, vp, vp, vp],
+         vp, vp, vp, vp, vp, vp, vp],
     ),
     "pxa_fft": (i32, [i32, i32, P_i64, i32, P_int, i64, i32, vp, vp, vp]),
     "pxa_fft_workspace_bytes": (sz, [i32, i32, P_i64, i32, P_int, i64]),

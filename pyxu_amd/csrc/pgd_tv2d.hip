@@ -64,6 +64,7 @@ struct PgdParams {
   int diag;     // PXA_TUNE_PGD_DIAG (bit 5: s_memtime phase trace of a few workgroups)
   int stagger;  // PXA_TUNE_PGD_STAGGER (A/B probe: delayed start of some first-round workgroups)
   unsigned round1;  // workgroups resident at once (4 per CU)
+  const T* xref;    // RelError partials relative to this iterate (nullptr: relative to x)
 };
 
 // Round 3 also measured a variant that carried yk as solver state (the epilogue writing the next
@@ -380,7 +381,7 @@ __device__ inline void finish_vec(const PgdParams<T>& p, int gr, int gc, const T
   }
 }
 
-// RelError partials per wavefront: lane 0 of the wave writes its (sum (x_new - x)^2, sum x^2) to
+// RelError partials per wavefront: lane 0 of the wave writes its (sum (x_new - r)^2, sum r^2), r = x_ref or x, to
 // partials[2 slot .. 2 slot + 1], slot = tile * kPartWaves + wave (fixed-order shuffle fold, no barrier).
 constexpr int kPartWaves = kThreads / 64;
 
@@ -401,7 +402,7 @@ __device__ inline void wave_partials(double part_d, double part_x, double* parti
 template <typename T, int R, bool EDGE>
 __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
                                 const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
-                                T* __restrict__ xns, double* __restrict__ partials) {
+                                T* __restrict__ xns, double* __restrict__ partials, const T* __restrict__ xrs) {
   using L = Layout<T, R>;
   using S = Stage<T, R>;
   constexpr int CW = L::CW;
@@ -481,7 +482,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     }
   }
   // x (RelError partials only) is loaded once pass B's parked results are out of the registers
-  if (want_part) load_staged<T, R, EDGE>(p, ty0, tx0, xs, hb.x);
+  if (want_part) load_staged<T, R, EDGE>(p, ty0, tx0, xrs, hb.x);
   __syncthreads();
   tmark(6);
   {
@@ -537,14 +538,15 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
   const T* xps = xp + (int64_t)s * img;
   const T* bs = b + (int64_t)(s % (unsigned)p.y_images) * img;
   T* xns = xn + (int64_t)s * img;
+  const T* xrs = (p.xref != nullptr ? p.xref : x) + (int64_t)s * img;
   // interior: the whole A window lies inside the image (so no boundary rows / columns of G either),
   // rows are 16-B aligned and 32-bit offsets suffice -> no bounds tests
   const bool interior = p.vec_ok && img <= 0x7fffffff && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0 &&
                         tx0 - L::CA >= 0 && tx0 + TX + L::CA <= p.n1;
   if (interior)
-    pgd_tile<T, R, false>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
+    pgd_tile<T, R, false>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials, xrs);
   else
-    pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials);
+    pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials, xrs);
 }
 
 template <typename T, int R>
@@ -570,11 +572,11 @@ template <typename T>
 int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
               const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1, double lam,
               double mu, double a, double tau, int prox, double prox_w, const void* x, const void* x_prev,
-              const void* hty, void* x_new, double* partials, hipStream_t s) {
+              const void* hty, void* x_new, double* partials, const void* x_ref, hipStream_t s) {
   PXA_CHECK_ARG(stack >= 1 && n0 >= 1 && n1 >= 1 && y_images >= 1 && stack % y_images == 0);
   PXA_CHECK_ARG(n0 <= 0x7fffffff && n1 <= 0x7fffffff);
   PXA_CHECK_ARG(x && x_prev && hty && x_new);
-  PXA_CHECK_ARG(x_new != x && x_new != x_prev);
+  PXA_CHECK_ARG(x_new != x && x_new != x_prev && x_new != x_ref);
   PXA_CHECK_ARG(prox >= 0 && prox <= 2);
   PXA_CHECK_ARG(nt0 >= 1 && nt1 >= 1 && off0 && off1 && coef0 && coef1);
   int R = 1;  // TV needs a 1-pixel halo even for a 1-tap blur
@@ -621,7 +623,9 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.tau = (T)tau;
   p.pw = (T)prox_w;
   constexpr int V = kVecN<T>;
-  p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new);
+  p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new) &&
+             (x_ref == nullptr || aligned16(x_ref));
+  p.xref = (partials != nullptr && x_ref != nullptr && x_ref != x) ? (const T*)x_ref : nullptr;
   p.tv = lam != 0.0;
   p.prox = prox;
   p.diag = kProbes ? tuning(PXA_TUNE_PGD_DIAG) : 0;
@@ -667,10 +671,11 @@ int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1) {
 int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
                       const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
                       double lam, double mu, double a, double tau, int prox, double prox_w, const void* x,
-                      const void* x_prev, const void* hty, void* x_new, double* partials, void* stream) {
+                      const void* x_prev, const void* hty, void* x_new, double* partials, const void* x_ref,
+                      void* stream) {
   PXA_DISPATCH(dtype, T,
                return pgd_entry<T>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, a,
-                                   tau, prox, prox_w, x, x_prev, hty, x_new, partials, as_stream(stream)));
+                                   tau, prox, prox_w, x, x_prev, hty, x_new, partials, x_ref, as_stream(stream)));
 }
 
 }  // extern "C"

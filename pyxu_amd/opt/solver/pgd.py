@@ -100,6 +100,7 @@ class PGD(pxa.Solver):
             p["parts"] = _dev.empty_f64((2 * ntiles,), x0)
             p["tiles_per_row"] = ntiles // max(p["rows"], 1)
             self._spare = None
+            self._x_check = None  # the x of the last stop check (RelError partials against it)
             # the solver never writes a tensor it has published as x (outputs go to fresh or recycled
             # buffers nobody else references), so stop criteria may keep references instead of copies
             mst["__immutable__"] = frozenset({"x"})
@@ -138,16 +139,23 @@ class PGD(pxa.Solver):
                 out = _dev.empty_like(x)
             tau = mst["tau"]
             # RelError partials only for the launch right before a stop check (the engine advances idx
-            # before m_step: the next check runs at idx when idx % stop_rate == 0)
+            # before m_step: the next check runs at idx when idx % stop_rate == 0).  RelError compares with
+            # the iterate of the PREVIOUS check (opt/stop.py:353-382), which the criterion keeps: x itself at
+            # stop_rate 1, else the x this solver saw at that check (self._x_check, the same tensor object)
             ast = self._astate
-            want = (self._fused_relerr and ast.get("stop_rate") is not None
-                    and ast["idx"] % ast["stop_rate"] == 0)
+            sr = ast.get("stop_rate")
+            if sr is not None and (ast["idx"] - 1) % sr == 0:
+                self._x_check = x  # a check ran right before this step, on this x
+            want = self._fused_relerr and sr is not None and ast["idx"] % sr == 0
             parts = p["parts"] if want else None
+            xref = self._x_check if want else None
+            if xref is None:
+                xref = x
             _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
                                p["h0"], p["h1"], p["lam"], p["mu"], a, tau, p["prox"], tau * p["prox_scale"],
-                               partials=parts, pre=p["pre"])
+                               partials=parts, pre=p["pre"], x_ref=None if xref is x else xref)
             if want:  # (var, x_new, the x the statistics are relative to, partials, rows, tiles per row)
-                mst["__relerr__"] = ("x", out, x, parts, p["rows"], p["tiles_per_row"])
+                mst["__relerr__"] = ("x", out, xref, parts, p["rows"], p["tiles_per_row"])
             else:
                 mst.pop("__relerr__", None)
             mst["x_prev"], mst["x"] = x, out

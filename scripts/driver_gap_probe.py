@@ -66,7 +66,9 @@ def analyze(trace_dir, stamps):
         for r in csv.DictReader(open(fn)):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60]))
     rows.sort()
-    for rep in json.load(open(stamps)):
+    text = open(stamps).read()
+    reps, _ = json.JSONDecoder().raw_decode(text[text.index("["):])  # the JSON line may share the log
+    for rep in reps:
         t0, t1 = rep["t0"], rep["t1"]
         ks = [k for k in rows if t0 <= k[0] <= t1]
         print(f"rep {rep['rep']}: window {(t1 - t0) / 1e3:.1f} us, {len(ks)} kernels")
@@ -83,7 +85,11 @@ def analyze(trace_dir, stamps):
         for i, (a, b) in enumerate(rep["steps"]):
             if b - a > 30000:
                 print(f"  host step {i}: {(b - a) / 1e3:.1f} us at +{(a - t0) / 1e3:.1f} us")
-        print("  kernels:", ", ".join(f"{n.split('(')[0].split('<')[0]} {(e - s) / 1e3:.1f}" for s, e, n in ks[:4]), "...")
+        import re
+
+        for s, e, n in ks:
+            m = re.search(r"(\w+_kernel)", n)
+            print(f"    +{(s - t0) / 1e3:7.1f} us  {(e - s) / 1e3:5.1f} us  {m.group(1) if m else n[:40]}")
 
 
 if __name__ == "__main__":

@@ -61,6 +61,15 @@ if [ "$S" = "ab1" ]; then
   python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, true, false, true, true>" pds_march_kernel_pd3o@1024^3 $P/traffic_c3.json $T || true
   python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, false, false, true, true>" pds_march_kernel_cv@1024^3 $P/traffic_c3.json $T || true
 fi
+if [ "$S" = "gap" ]; then
+  step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_solver_engine.py tests/test_gpu_parity.py -k "pgd or relerr or speculative or async or trajectory"
+  step drv1 120 $DRV
+  step drv2 120 $DRV
+  step drv3 120 $DRV
+  step gaptrace 300 rocprofv3 --kernel-trace -d $P/gap -o run --output-format csv -- python3 scripts/driver_gap_probe.py 20 5
+  grep -h '^\[{' $O/gaptrace.log > $O/stamps.json || true
+  python3 scripts/driver_gap_probe.py --analyze $P/gap $O/stamps.json || true
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"

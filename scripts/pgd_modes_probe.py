@@ -26,7 +26,7 @@ def setup(n, stack):
 
 def launch(a, pre):
     _dev.lib.pxa_pgd_tv2d_step(0, *pre, 0.3, 0.5, 1, 0.0, a["x"].data_ptr(), a["xp"].data_ptr(), a["b"].data_ptr(),
-                               a["out"].data_ptr(), None, _dev.stream())
+                               a["out"].data_ptr(), None, None, _dev.stream())
 
 
 def window(a, pre, kern, n_launch, diag=0):

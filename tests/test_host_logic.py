@@ -48,7 +48,7 @@ def test_argument_validation_without_gpu():
     lib = pyxu_amd.lib
     assert lib.pxa_axpby(7, 10, 1.0, None, 0.0, None, None, None) == -2  # bad dtype
     assert lib.pxa_row_reduce(0, 99, 1, 4, 1, None, 1, 1, None) == -1  # bad op
-    assert lib.pxa_pgd_tv2d_step(0, 1, 1, 8, 8, 0, None, None, 0, None, None, 1, 1, 0, 1, 0, 1, 0, 0, 1, 2, 3, 4, None, None) == -1
+    assert lib.pxa_pgd_tv2d_step(0, 1, 1, 8, 8, 0, None, None, 0, None, None, 1, 1, 0, 1, 0, 1, 0, 0, 1, 2, 3, 4, None, None, None) == -1
 
 
 @pytest.mark.parametrize("name", golden_names("gaussian_"))
