@@ -67,7 +67,7 @@ def analyze(trace_dir, stamps):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60]))
     rows.sort()
     text = open(stamps).read()
-    reps, _ = json.JSONDecoder().raw_decode(text[text.index("["):])  # the JSON line may share the log
+    reps, _ = json.JSONDecoder().raw_decode(text[text.index("[{"):])  # the JSON line may share the log
     for rep in reps:
         t0, t1 = rep["t0"], rep["t1"]
         ks = [k for k in rows if t0 <= k[0] <= t1]
