@@ -190,9 +190,17 @@ int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p,
 /* RelError statistics from the fused PGD step's per-tile partials (pxa_pgd_tv2d_step[_y] with
  * `partials`): out[0 * rows + r] = sum (x_new - x)^2 and out[1 * rows + r] = sum x^2 over the per_row
  * consecutive tiles of stack row r, fixed summation order.  At stop_rate 1 the criterion's stored x_prev
- * IS the step's x, so this replaces the separate pass over x and x_prev (stop.py:353-382).  `out` may
- * be device or pinned (device-mapped) host memory. */
-int pxa_tile_partials_fold(int64_t rows, int64_t per_row, const double* partials, double* out, void* stream);
+ * IS the step's x, so this replaces the separate pass over x and x_prev (stop.py:353-382); at stop_rate > 1
+ * the step's partials were taken against the previous check's iterate (x_ref).  `out` may be device or
+ * pinned (device-mapped) host memory.  With `flags` != NULL (2 * rows words of pxa_host_alloc memory, like
+ * `out`), statistic q's flag is set to `seq` once out[q] is visible to the host (system-scope release): a
+ * stop check then polls the flags instead of waiting for a stream event. */
+int pxa_tile_partials_fold(int64_t rows, int64_t per_row, const double* partials, double* out, uint32_t* flags,
+                           uint32_t seq, void* stream);
+/* Host memory the device reads and writes coherently during a kernel (hipHostMalloc, coherent + mapped):
+ * the stop checks' statistics and completion flags.  The same pointer is valid on the device. */
+int pxa_host_alloc(size_t bytes, void** ptr);
+int pxa_host_free(void* ptr);
 /* RelError.stop in one pass (opt/stop.py:353-382, norm=2): out[0:rows] = sum (x - x_prev)^2 and
  * out[rows:2 rows] = sum x_prev^2 per row (same bits as pxa_row_reduce DIFFSQ / SUMSQ), and, when
  * x_copy is not NULL, x_copy = x (the `x.copy()` the criterion keeps, stop.py:381).  `out` may be

@@ -541,9 +541,53 @@ def tile_partials_fold(parts, rows, per_row, out):
     """RelError statistics from the fused PGD step's per-tile partials (pxa_tile_partials_fold):
     out (contiguous float64 (2, rows), device or pinned host) = per-row sum (x_new - x)^2, sum x^2."""
     assert out.is_contiguous() and out.numel() == 2 * rows
-    check(lib.pxa_tile_partials_fold(int(rows), int(per_row), parts.data_ptr(), out.data_ptr(), stream()),
+    check(lib.pxa_tile_partials_fold(int(rows), int(per_row), parts.data_ptr(), out.data_ptr(), None, 0, stream()),
           "pxa_tile_partials_fold")
     return out
+
+
+class HostFlagBuffer:
+    """Coherent host memory (pxa_host_alloc) for a stop check's statistics: `stats` (float64 (2, rows)) and one
+    completion flag per statistic (`flags`, uint32 (2 rows,)).  The device writes the statistics, then the
+    flags (system-scope release); the host polls the flags -- no stream event between the statistics and
+    the next kernel, and no event wake-up latency."""
+
+    def __init__(self, rows):
+        self.rows = int(rows)
+        nb = 16 * self.rows + 8 * self.rows  # 2 rows float64 + 2 rows uint32 (8-byte aligned tail)
+        p = ct.c_void_p()
+        check(lib.pxa_host_alloc(nb, ct.byref(p)), "pxa_host_alloc")
+        self._ptr = p.value
+        raw = (ct.c_uint8 * nb).from_address(self._ptr)
+        self.stats = np.frombuffer(raw, dtype=np.float64, count=2 * self.rows).reshape(2, self.rows)
+        self.flags = np.frombuffer(raw, dtype=np.uint32, count=2 * self.rows, offset=16 * self.rows)
+        self.flags[:] = 0
+        self.seq = 0
+        self._free = lib.pxa_host_free
+
+    def fold(self, parts, per_row):
+        """Enqueue pxa_tile_partials_fold into this buffer under a new sequence number; returns it."""
+        self.seq = (self.seq % 0xFFFFFFFE) + 1
+        check(lib.pxa_tile_partials_fold(self.rows, int(per_row), parts.data_ptr(), self._ptr,
+                                         self._ptr + 16 * self.rows, self.seq, stream()), "pxa_tile_partials_fold")
+        return self.seq
+
+    def wait(self, seq, spin_s=1e-3):
+        """Poll the flags until every statistic of check `seq` has landed (as wait_event)."""
+        import time
+
+        f = self.flags
+        if (f == seq).all():
+            return
+        t_end = time.perf_counter() + spin_s
+        while not (f == seq).all():
+            if time.perf_counter() > t_end:
+                time.sleep(0)
+
+    def __del__(self):
+        if getattr(self, "_ptr", None):
+            self._free(self._ptr)
+            self._ptr = None
 
 
 def row_reduce(op, x, y=None, out=None):

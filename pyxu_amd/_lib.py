@@ -47,7 +47,9 @@ EXPORTS = {
     "pxa_row_reduce_pow": (i32, [i32, i64, i64, f64, vp, vp, vp, vp, vp]),
     "pxa_relerr_stats_workspace_bytes": (sz, [i64, i64]),
     "pxa_relerr_stats": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp]),
-    "pxa_tile_partials_fold": (i32, [i64, i64, vp, vp, vp]),
+    "pxa_tile_partials_fold": (i32, [i64, i64, vp, vp, vp, ct.c_uint32, vp]),
+    "pxa_host_alloc": (i32, [sz, ct.POINTER(vp)]),
+    "pxa_host_free": (i32, [vp]),
     "pxa_cg_update_workspace_bytes": (sz, [i64]),
     "pxa_cg_update": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "pxa_stencil_axis": (i32, [i32, i64, i32, P_i64, i32, i32, P_i32, P_f64, i32, vp, i64, vp, i64, f64, vp]),

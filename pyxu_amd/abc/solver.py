@@ -404,12 +404,28 @@ class Solver:
                 ast["logger"].info(f"[{dt.datetime.now()}] Stopping Criterion satisfied -> END")
             self.writeback()
             return False
+        if err is None and ast["mode"] is not Mode.ASYNC:
+            # continue: the device has one step of work left, so the next launch is what matters now.  The
+            # check's history record is captured after it (_take_capture: before anything that can change the
+            # criterion's info(), i.e. the next check, and after the next launch otherwise).  ASYNC mode
+            # captures now: stats() may run on another thread.
+            ast["capture"] = (idx, _ml and log_on)
+            return True
         rec = (idx, ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, _ml and log_on)
         with ast["lock"]:
             ast["pending"].append(rec)
         if err is not None:
             raise err
         return True
+
+    def _take_capture(self):
+        """History record of a speculative check whose capture was deferred past the next launch."""
+        ast = self._astate
+        cap = ast.pop("capture", None)
+        if cap is not None:
+            rec = (cap[0], ast["stop_crit"].info(), dt.datetime.now(), pxrt.getPrecision().value, cap[1])
+            with ast["lock"]:
+                ast["pending"].append(rec)
 
     def _step(self) -> bool:
         ast = self._astate
@@ -419,6 +435,8 @@ class Solver:
         _mw = (ast["wb_rate"] is not None) and (idx % ast["wb_rate"] == 0)
 
         log_on = not ast.get("internal")
+        if "capture" in ast and (_ms or _mw):  # before this step's check can change the criterion's info()
+            self._take_capture()
         if ast["pending"] and (_mw or idx - ast["pending"][0][0] >= self._RECORD_LAG):
             self._flush_records()
 
@@ -453,6 +471,8 @@ class Solver:
             try:
                 self.m_step()
             finally:
+                if "capture" in ast:
+                    self._take_capture()
                 if _ms or (_ml and log_on):
                     rec = (idx, ast["stop_crit"].info() if _ms else None, dt.datetime.now(),
                            pxrt.getPrecision().value, _ml and log_on)
@@ -560,6 +580,8 @@ class Solver:
 
     def _flush_records(self):
         ast = self._astate
+        if "capture" in ast:
+            self._take_capture()
         if ast.get("pending"):
             with ast["lock"]:
                 items, ast["pending"] = ast["pending"], []

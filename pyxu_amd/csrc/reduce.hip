@@ -172,7 +172,8 @@ int launch_relerr(int64_t rows, int64_t n, const void* x, const void* p, void* x
 // slots of a 2048^2 image, every load a dependent round trip.)
 __global__ void __launch_bounds__(kBlock) tile_partials_fold_kernel(int64_t rows, int64_t per_row,
                                                                     const double* __restrict__ part,
-                                                                    double* __restrict__ out) {
+                                                                    double* __restrict__ out,
+                                                                    unsigned* __restrict__ flags, unsigned seq) {
   __shared__ double red[kBlock / kWave];
   const int64_t q = blockIdx.x;  // q = stat * rows + row
   const int64_t stat = q / rows, r = q - stat * rows;
@@ -188,6 +189,10 @@ __global__ void __launch_bounds__(kBlock) tile_partials_fold_kernel(int64_t rows
     double t = 0.0;
     for (int i = 0; i < kBlock / kWave; ++i) t += red[i];
     out[q] = t;
+    if (flags != nullptr) {  // completion flag of this statistic, ordered after its value system-wide
+      __threadfence_system();
+      __hip_atomic_store(flags + q, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -284,13 +289,22 @@ int pxa_row_reduce(int dtype, int op, int64_t rows, int64_t n, const void* x, co
 #undef PXA_RED_CASE
 }
 
-int pxa_tile_partials_fold(int64_t rows, int64_t per_row, const double* partials, double* out, void* stream) {
+int pxa_tile_partials_fold(int64_t rows, int64_t per_row, const double* partials, double* out, uint32_t* flags,
+                           uint32_t seq, void* stream) {
   PXA_CHECK_ARG(rows >= 1 && per_row >= 1 && partials != nullptr && out != nullptr);
   PXA_CHECK_ARG(2 * rows <= 0x7fffffff);
   hipLaunchKernelGGL(tile_partials_fold_kernel, dim3((unsigned)(2 * rows)), dim3(kBlock), 0, as_stream(stream), rows,
-                     per_row, partials, out);
+                     per_row, partials, out, (unsigned*)flags, (unsigned)seq);
   return last_launch_status();
 }
+
+int pxa_host_alloc(size_t bytes, void** ptr) {
+  PXA_CHECK_ARG(ptr != nullptr && bytes > 0);
+  *ptr = nullptr;
+  return (int)hipHostMalloc(ptr, bytes, hipHostMallocCoherent | hipHostMallocMapped);
+}
+
+int pxa_host_free(void* ptr) { return ptr ? (int)hipHostFree(ptr) : PXA_OK; }
 
 size_t pxa_relerr_stats_workspace_bytes(int64_t rows, int64_t n) { return 2 * pxa_row_reduce_workspace_bytes(rows, n); }
 

@@ -326,6 +326,24 @@ class RelError(pxa.StoppingCriterion):
         rows = x.numel() // x.shape[-1]
         if not (0 < rows <= 65535 and x.dtype == self._x_prev.dtype):
             return super().stop_async(state)
+        h = self._fused(state, x)
+        if h is not None:
+            # the step's own per-tile partials, folded straight into coherent host memory with a completion flag
+            # per statistic: no pass over x / x_prev, no copy, no stream event.  x is kept (a reference) now, so
+            # that the solver's next step, enqueued before the decision is read, may recycle the previous
+            # iterate's buffer
+            fb = getattr(self, "_flag_buf", None)
+            if fb is None or fb.rows != rows:
+                fb = self._flag_buf = _dev.HostFlagBuffer(rows)
+            seq = fb.fold(h[3], h[5])
+            self._x_prev = x
+            shape = x.shape[:-1]
+
+            def resolve_flags():
+                fb.wait(seq)
+                return self._decide(_finish(fb.stats.copy(), self._norm), shape)
+
+            return resolve_flags
         # one device / pinned-host statistics pair and one event per criterion, reused: a check is
         # resolved before the next one is issued
         buf = getattr(self, "_async_buf", None)
@@ -333,23 +351,13 @@ class RelError(pxa.StoppingCriterion):
             buf = (torch.empty((2, rows), dtype=torch.float64, pin_memory=True), torch.cuda.Event())
             self._async_buf = buf
         host, ev = buf
-        h = self._fused(state, x)
-        if h is not None:
-            # the step's own per-tile partials, folded straight into the pinned host buffer: no pass over
-            # x / x_prev, no copy.  x is kept (a reference) now, so that the solver's next step, enqueued
-            # before the decision is read, may recycle the previous iterate's buffer
-            _dev.tile_partials_fold(h[3], h[4], h[5], host)
+        # the final fold writes the statistics straight into the pinned host buffer (device-mapped): no device ->
+        # host copy launch between the statistics and the event
+        borrow = self._var in state.get("__immutable__", ()) if hasattr(state, "get") else False
+        x_copy = _dev.relerr_stats(x, self._x_prev, host, copy=not borrow)
+        if borrow:
             x_copy = x
-        else:
-            # the final fold writes the statistics straight into the pinned host buffer (device-mapped):
-            # no device -> host copy launch between the statistics and the event
-            borrow = self._var in state.get("__immutable__", ()) if hasattr(state, "get") else False
-            x_copy = _dev.relerr_stats(x, self._x_prev, host, copy=not borrow)
-            if borrow:
-                x_copy = x
         _dev.record_event(ev)
-        if h is not None:
-            self._x_prev = x_copy
         shape = x.shape[:-1]
 
         def resolve():

@@ -30,6 +30,25 @@ def run(steps, warmup):
     from pyxu_amd import _dev
 
     torch.cuda.set_device(0)
+    # host stamps inside the stop check (no change to the code path: wrappers around the same calls)
+    marks_in = []
+    orig_wait = _dev.wait_event
+
+    def wait_stamped(ev, *a, **k):
+        t = time.perf_counter_ns()
+        orig_wait(ev, *a, **k)
+        marks_in.append(("wait", t, time.perf_counter_ns()))
+
+    _dev.wait_event = wait_stamped
+    orig_spec = pxa.Solver._step_speculative
+
+    def spec_stamped(self, *a, **k):
+        t = time.perf_counter_ns()
+        r = orig_spec(self, *a, **k)
+        marks_in.append(("spec", t, time.perf_counter_ns()))
+        return r
+
+    pxa.Solver._step_speculative = spec_stamped
     f, g, _ = bench.build_problem(2048, 2048, seed=1234)
     sr = bench.auto_stop_rate(steps)
     out = []
@@ -55,7 +74,9 @@ def run(steps, warmup):
             t_launched = time.perf_counter_ns()
             torch.cuda.synchronize()
             t1 = time.perf_counter_ns()
-            out.append({"rep": rep, "t0": t0, "t1": t1, "t_launched": t_launched, "steps": marks})
+            out.append({"rep": rep, "t0": t0, "t1": t1, "t_launched": t_launched, "steps": marks,
+                        "inner": [m for m in marks_in if m[1] >= t0]})
+            marks_in.clear()
             del s, gen
     json.dump(out, sys.stdout)
 
@@ -85,6 +106,9 @@ def analyze(trace_dir, stamps):
         for i, (a, b) in enumerate(rep["steps"]):
             if b - a > 30000:
                 print(f"  host step {i}: {(b - a) / 1e3:.1f} us at +{(a - t0) / 1e3:.1f} us")
+        for tag, a, b in rep.get("inner", []):
+            print(f"  host {tag}: +{(a - t0) / 1e3:.1f} -> +{(b - t0) / 1e3:.1f} us")
+        print("  host step starts:", " ".join(f"{(a - t0) / 1e3:.1f}" for a, _ in rep["steps"]))
         import re
 
         for s, e, n in ks:
