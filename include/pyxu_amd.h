@@ -62,9 +62,8 @@ extern "C" {
                                   workgroups picked by `sel` in the first dispatch round by n x 1024 cycles */
 #define PXA_TUNE_PDS_EVENTS 5 /* measurement hook: > 0 makes pxa_pds_step record HIP events around each
                                  of its kernels (pxa_pds_kernel_ms) */
-#define PXA_TUNE_PDS_MARCH 7 /* A/B of the PDS dual-update kernels: bit 0 lets kernel D's threads own two
-                                positions (default one); bit 1 turns off the non-temporal policy of the
-                                read-once / write-once streams of kernels C and D (default on) */
+#define PXA_TUNE_PDS_MARCH 7 /* A/B of pxa_pds_step_la's kernel D: bit 0 lets a thread own two positions
+                                (default one) */
 #define PXA_TUNE_COUNT 8
 
 /* Row reductions (pxa_row_reduce). */
