@@ -70,6 +70,11 @@ if [ "$S" = "gap" ]; then
   grep -h '^\[{' $O/gaptrace.log > $O/stamps.json || true
   python3 scripts/driver_gap_probe.py --analyze $P/gap $O/stamps.json || true
 fi
+if [ "$S" = "c4prof" ]; then
+  step c4 300 python3 bench.py --only c4
+  step c4trace 300 rocprofv3 --kernel-trace --stats -d $P/c4 -o run --output-format csv -- python3 bench.py --only c4
+  python3 scripts/c4_timeline.py $P/c4 || true
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
