@@ -10,7 +10,8 @@ import threading
 
 __all__ = ["lib", "check", "BackendUnavailable", "LIB_PATH", "EXPORTS"]
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpyxu_amd.so")
+# PXA_LIB_PATH: the probe build of scripts/ (csrc/Makefile `probe`); the product loads the in-tree library
+LIB_PATH = os.environ.get("PXA_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpyxu_amd.so")
 
 i32, i64, f64, vp, sz = ct.c_int, ct.c_int64, ct.c_double, ct.c_void_p, ct.c_size_t
 P_i64 = ct.POINTER(ct.c_int64)
