@@ -183,6 +183,7 @@ def storage_exclusive(t) -> bool:
 
 TUNE_NORMAL_DIAG = 1  # PXA_TUNE_NORMAL_DIAG: pxa_dense_normal timing probes (wrong results)
 TUNE_DENSE_KERNEL = 2  # PXA_TUNE_DENSE_KERNEL: 0 LDS-staged MFMA GEMM (B >= 32), 1 the register-streamed kernel
+TUNE_DUAL_WGS = 4  # PXA_TUNE_DUAL_WGS: kernel C's target workgroup count (A/B; 0 = default)
 TUNE_PGD_DIAG = 3  # PXA_TUNE_PGD_DIAG: bit 5 = s_memtime phase trace of the PGD tile kernel
 TUNE_PGD_STAGGER = 6  # PXA_TUNE_PGD_STAGGER: (sel << 8) | n, delayed first-round workgroups (A/B probe)
 TUNE_PDS_EVENTS = 5  # PXA_TUNE_PDS_EVENTS: per-kernel HIP events inside pxa_pds_step (pds_kernel_ms)

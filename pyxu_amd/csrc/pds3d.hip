@@ -184,7 +184,8 @@ int run_c(const PdsGeom<T>& g, T sigma, T lam, T rho, T omr, bool pd3o, bool iso
   const bool vec = (g.n2 % V == 0) && aligned16(w) && aligned16(z) && aligned16(z_out);
   const int nv = vec ? V : 1;
   const int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
-  int cseg = (int)((4096 + blocks - 1) / blocks);
+  const int64_t target = tuning(PXA_TUNE_DUAL_WGS) > 0 ? tuning(PXA_TUNE_DUAL_WGS) : 4096;  // A/B knob
+  int cseg = (int)((target + blocks - 1) / blocks);
   if (cseg > g.n0) cseg = g.n0;
   if (cseg < 1) cseg = 1;
   pc.seg = (int)((g.n0 + cseg - 1) / cseg);

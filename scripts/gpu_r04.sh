@@ -71,6 +71,7 @@ if [ "$S" = "gap" ]; then
   python3 scripts/driver_gap_probe.py --analyze $P/gap $O/stamps.json || true
 fi
 if [ "$S" = "c4prof" ]; then
+  step k4wgs 300 python3 scripts/k4_wgs_probe.py 0,2048,8192
   step c4 300 python3 bench.py --only c4
   step c4trace 300 rocprofv3 --kernel-trace --stats -d $P/c4 -o run --output-format csv -- python3 bench.py --only c4
   python3 scripts/c4_timeline.py $P/c4 || true
