@@ -182,11 +182,13 @@ int pxa_row_reduce_pow(int dtype, int64_t rows, int64_t n, double p, const void*
 /* CG iteration tail after A p (opt/solver/cg.py:125-153), for `rows` stacked problems of n entries, in
  * three launches: alpha = (T)(rr / <p, A p>), x += alpha p, r -= alpha A p, rr' = ||r||^2,
  * beta = (T)(rr' / rr), p = r + beta p.  rr: this step's ||r||^2 per row (device double); rr_out (device,
- * != rr) and rr_host (pinned / device-mapped host memory, may be NULL) receive rr'.  All sums in double
+ * != rr) and rr_host (pinned / device-mapped host memory, may be NULL) receive rr'; with `flags` (rows words
+ * of pxa_host_alloc memory, rr_host then in that memory too) flag[row] is set to `seq` once rr_host[row] is
+ * visible to the host, so the stop check polls it instead of waiting for a stream event.  All sums in double
  * with a fixed partition and order.  `work`: pxa_cg_update_workspace_bytes(rows) bytes. */
 size_t pxa_cg_update_workspace_bytes(int64_t rows);
 int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
-                  double* rr_out, double* rr_host, void* work, void* stream);
+                  double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, void* stream);
 
 /* RelError statistics from the fused PGD step's per-tile partials (pxa_pgd_tv2d_step[_y] with
  * `partials`): out[0 * rows + r] = sum (x_new - x)^2 and out[1 * rows + r] = sum x^2 over the per_row

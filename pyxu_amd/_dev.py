@@ -531,11 +531,18 @@ def relerr_stats(x, x_prev, out, copy=True):
 
 def cg_update(x, r, p, ap, rr, rr_out, rr_host, work):
     """pxa_cg_update: the CG iteration tail after A p on (rows, n) x / r / p / A p (in place), from this
-    step's ||r||^2 `rr` (device float64 (rows,)); ||r'||^2 lands in rr_out (device) and rr_host (pinned)."""
+    step's ||r||^2 `rr` (device float64 (rows,)); ||r'||^2 lands in rr_out (device) and in rr_host: a
+    HostFlagBuffer(rows, rows, rows) (returns the publication's sequence number, which its wait() takes), a
+    pinned host tensor, or None."""
     rows, n = x.shape
+    seq, vp_, fp_ = 0, None, None
+    if isinstance(rr_host, HostFlagBuffer):
+        seq, vp_, fp_ = rr_host.next_seq(), rr_host.vptr, rr_host.fptr
+    elif rr_host is not None:
+        vp_ = rr_host.data_ptr()
     check(lib.pxa_cg_update(dtcode(x), rows, n, ptr(x), ptr(r), ptr(p), ptr(ap), rr.data_ptr(), rr_out.data_ptr(),
-                            rr_host.data_ptr() if rr_host is not None else None, work.data_ptr(), stream()),
-          "pxa_cg_update")
+                            vp_, fp_, seq, work.data_ptr(), stream()), "pxa_cg_update")
+    return seq
 
 
 def tile_partials_fold(parts, rows, per_row, out):
@@ -548,33 +555,45 @@ def tile_partials_fold(parts, rows, per_row, out):
 
 
 class HostFlagBuffer:
-    """Coherent host memory (pxa_host_alloc) for a stop check's statistics: `stats` (float64 (2, rows)) and one
-    completion flag per statistic (`flags`, uint32 (2 rows,)).  The device writes the statistics, then the
-    flags (system-scope release); the host polls the flags -- no stream event between the statistics and
-    the next kernel, and no event wake-up latency."""
+    """Coherent host memory (pxa_host_alloc) for statistics a kernel publishes to the host: `values`
+    (float64 (nvals,)) and one completion flag per value group (`flags`, uint32 (nflags,)).  The device writes
+    the values, then the flags (system-scope release); the host polls the flags -- no stream event between the
+    statistics and the next kernel, and no event wake-up latency.  Used by the fused RelError fold (2 rows
+    values, 2 rows flags: `stats` is the (2, rows) view) and by CG's ||r'||^2 (rows, rows)."""
 
-    def __init__(self, rows):
+    def __init__(self, rows, nvals=None, nflags=None):
         self.rows = int(rows)
-        nb = 16 * self.rows + 8 * self.rows  # 2 rows float64 + 2 rows uint32 (8-byte aligned tail)
+        nv = 2 * self.rows if nvals is None else int(nvals)
+        nf = nv if nflags is None else int(nflags)
+        nb = 8 * nv + 4 * nf + 4
         p = ct.c_void_p()
         check(lib.pxa_host_alloc(nb, ct.byref(p)), "pxa_host_alloc")
         self._ptr = p.value
         raw = (ct.c_uint8 * nb).from_address(self._ptr)
-        self.stats = np.frombuffer(raw, dtype=np.float64, count=2 * self.rows).reshape(2, self.rows)
-        self.flags = np.frombuffer(raw, dtype=np.uint32, count=2 * self.rows, offset=16 * self.rows)
+        self.values = np.frombuffer(raw, dtype=np.float64, count=nv)
+        self.flags = np.frombuffer(raw, dtype=np.uint32, count=nf, offset=8 * nv)
         self.flags[:] = 0
+        self.vptr, self.fptr = self._ptr, self._ptr + 8 * nv
         self.seq = 0
         self._free = lib.pxa_host_free
 
-    def fold(self, parts, per_row):
-        """Enqueue pxa_tile_partials_fold into this buffer under a new sequence number; returns it."""
+    @property
+    def stats(self):
+        return self.values.reshape(2, self.rows)
+
+    def next_seq(self):
         self.seq = (self.seq % 0xFFFFFFFE) + 1
-        check(lib.pxa_tile_partials_fold(self.rows, int(per_row), parts.data_ptr(), self._ptr,
-                                         self._ptr + 16 * self.rows, self.seq, stream()), "pxa_tile_partials_fold")
         return self.seq
 
+    def fold(self, parts, per_row):
+        """Enqueue pxa_tile_partials_fold into this buffer under a new sequence number; returns it."""
+        seq = self.next_seq()
+        check(lib.pxa_tile_partials_fold(self.rows, int(per_row), parts.data_ptr(), self.vptr, self.fptr, seq,
+                                         stream()), "pxa_tile_partials_fold")
+        return seq
+
     def wait(self, seq, spin_s=1e-3):
-        """Poll the flags until every statistic of check `seq` has landed (as wait_event)."""
+        """Poll the flags until every value of publication `seq` has landed (as wait_event)."""
         import time
 
         f = self.flags

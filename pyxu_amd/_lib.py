@@ -52,7 +52,7 @@ EXPORTS = {
     "pxa_host_alloc": (i32, [sz, ct.POINTER(vp)]),
     "pxa_host_free": (i32, [vp]),
     "pxa_cg_update_workspace_bytes": (sz, [i64]),
-    "pxa_cg_update": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "pxa_cg_update": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp, vp]),
     "pxa_stencil_axis": (i32, [i32, i64, i32, P_i64, i32, i32, P_i32, P_f64, i32, vp, i64, vp, i64, f64, vp]),
     "pxa_stencil_sep_workspace_bytes": (sz, [i32, i64, i32, P_i64, P_int]),
     "pxa_stencil_sep": (i32, [i32, i64, i32, P_i64, P_int, P_i32, P_f64, vp, i64, vp, i64, f64, vp, vp]),

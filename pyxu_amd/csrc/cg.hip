@@ -5,7 +5,8 @@
 //             float64 division then the cast of the host / row_ratio path), x += alpha p, r -= alpha A p,
 //             per-block partials of ||r'||^2
 //   cg_p      every block folds the ||r'||^2 partials, beta = (T)(rr' / rr), p = r + beta p; block 0 stores
-//             rr' for the next step (device) and into pinned host memory (the stop check's value)
+//             rr' for the next step (device) and into host memory (the stop check's value), then, with
+//             `flags`, a completion flag the host polls (coherent host memory, system-scope release)
 // One row of the stacked problem per grid.y.  All sums in double with a fixed partition and order, so the
 // results are deterministic run to run.  HBM-bound streaming (p, A p read twice; x, r, p written once).
 #include "common.hpp"
@@ -81,7 +82,8 @@ template <typename T>
 __global__ void __launch_bounds__(kBlock) cg_p_kernel(int64_t n, const double* __restrict__ rr,
                                                       const double* __restrict__ part_rr, const T* __restrict__ r,
                                                       T* __restrict__ p, double* __restrict__ rr_out,
-                                                      double* __restrict__ rr_host) {
+                                                      double* __restrict__ rr_host, unsigned* __restrict__ flags,
+                                                      unsigned seq) {
   const int64_t row = blockIdx.y;
   const double rn = fold(part_rr, row, gridDim.x);
   const T beta = (T)(rn / rr[row]);
@@ -93,6 +95,10 @@ __global__ void __launch_bounds__(kBlock) cg_p_kernel(int64_t n, const double* _
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     rr_out[row] = rn;
     if (rr_host) rr_host[row] = rn;
+    if (flags) {  // the stop check polls this flag instead of waiting for a stream event
+      __threadfence_system();
+      __hip_atomic_store(flags + row, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -106,7 +112,7 @@ extern "C" {
 size_t pxa_cg_update_workspace_bytes(int64_t rows) { return rows > 0 ? (size_t)rows * 2 * kCgBlocks * sizeof(double) : 0; }
 
 int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
-                  double* rr_out, double* rr_host, void* work, void* stream) {
+                  double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, void* stream) {
   PXA_CHECK_ARG(rows >= 1 && rows <= 65535 && n >= 1);
   PXA_CHECK_ARG(x && r && p && ap && rr && rr_out && work && rr_out != rr);
   hipStream_t st = as_stream(stream);
@@ -123,7 +129,7 @@ int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p,
     e = last_launch_status();
     if (e) return e;
     hipLaunchKernelGGL((cg_p_kernel<T>), grid, dim3(kBlock), 0, st, n, rr, part_rr, (const T*)r, (T*)p, rr_out,
-                       rr_host);
+                       rr_host, (unsigned*)flags, (unsigned)seq);
     return last_launch_status();
   });
 }

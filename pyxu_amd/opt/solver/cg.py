@@ -37,15 +37,16 @@ class _HostRows:
 
 
 class _KernelRows(_HostRows):
-    """A row statistic that a kernel writes into a device buffer AND straight into pinned host memory
-    (pxa_cg_update): no copy launch, one event."""
+    """A row statistic that a kernel writes into a device buffer AND straight into coherent host memory with a
+    completion flag (pxa_cg_update into a HostFlagBuffer): no copy launch, no stream event -- the host polls
+    the flag, and the next kernel (A p', launched ahead of the stop check) follows without a gap."""
 
-    def __init__(self, dev, host):
-        import torch
+    def __init__(self, dev, fb, seq):
+        self.dev, self._fb, self._seq = dev, fb, seq
 
-        self.dev, self._h = dev, host
-        self._ev = torch.cuda.Event()
-        _dev.record_event(self._ev)
+    def host(self):
+        self._fb.wait(self._seq)
+        return self._fb.values.copy()
 
 
 class CG(pxa.Solver):
@@ -172,8 +173,8 @@ class CG(pxa.Solver):
             # the whole tail in three launches (pxa_cg_update): alpha, x, r, ||r'||^2, beta, p; ||r'||^2 is
             # written straight into pinned host memory for the next stop check
             hr = self._rows_buffers(_rows2d(x).shape[0])
-            _dev.cg_update(_rows2d(x), _rows2d(r), _rows2d(p), _rows2d(Ap), rr.dev, hr[0], hr[1], self._cg_work)
-            hr = _KernelRows(hr[0], hr[1])
+            seq = _dev.cg_update(_rows2d(x), _rows2d(r), _rows2d(p), _rows2d(Ap), rr.dev, hr[0], hr[1], self._cg_work)
+            hr = _KernelRows(hr[0], hr[1], seq)
             self._rr = (hr, r)
             if self._astate.get("internal"):
                 mst[_ROWSTAT] = {"residual": (r, 2, hr)}
@@ -204,15 +205,15 @@ class CG(pxa.Solver):
         mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
 
     def _rows_buffers(self, rows):
-        """(device, pinned host) float64 (rows,) buffers for ||r'||^2, two sets used alternately (a step reads
-        the previous step's device value while its kernel writes the other), plus the update workspace."""
+        """(device float64 (rows,), host HostFlagBuffer) buffers for ||r'||^2, two sets used alternately (a step
+        reads the previous step's device value while its kernel writes the other), plus the update workspace."""
         import torch
 
         bufs = getattr(self, "_rr_bufs", None)
         if bufs is None or bufs[0][0].numel() != rows:
             dev = self._mstate["x"].device
             bufs = [(torch.empty((rows,), dtype=torch.float64, device=dev),
-                     torch.empty((rows,), dtype=torch.float64, pin_memory=True)) for _ in range(2)]
+                     _dev.HostFlagBuffer(rows, rows, rows)) for _ in range(2)]
             self._rr_bufs, self._rr_flip = bufs, 0
             self._cg_work = torch.empty((max(int(_dev.lib.pxa_cg_update_workspace_bytes(rows)) // 8, 1),),
                                         dtype=torch.float64, device=dev)

@@ -341,7 +341,7 @@ class RelError(pxa.StoppingCriterion):
 
             def resolve_flags():
                 fb.wait(seq)
-                return self._decide(_finish(fb.stats.copy(), self._norm), shape)
+                return self._decide(_finish(fb.stats.copy(), self._norm), shape)  # (2, rows) view
 
             return resolve_flags
         # one device / pinned-host statistics pair and one event per criterion, reused: a check is

@@ -47,3 +47,4 @@ with pxrt.Precision(pxrt.Width.SINGLE):
     torch.cuda.synchronize()
     pr.disable()
     pstats.Stats(pr).sort_stats("cumulative").print_stats(45)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(40)

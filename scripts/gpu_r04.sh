@@ -76,6 +76,13 @@ if [ "$S" = "c4prof" ]; then
   step c4trace 300 rocprofv3 --kernel-trace --stats -d $P/c4 -o run --output-format csv -- python3 bench.py --only c4
   python3 scripts/c4_timeline.py $P/c4 || true
 fi
+if [ "$S" = "c4b" ]; then
+  step cgtests 600 $PT -m gpu tests/test_gpu_dense_normal.py tests/test_gpu_parity.py tests/test_gpu_distributed.py -k "cg or admm or normal or sharded or dense"
+  step c4 300 python3 bench.py --only c4
+  step c4trace 300 rocprofv3 --kernel-trace --stats -d $P/c4b -o run --output-format csv -- python3 bench.py --only c4
+  python3 scripts/c4_timeline.py $P/c4b || true
+  step c4host 300 python3 scripts/c4_host_prof.py
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
