@@ -49,8 +49,10 @@ extern "C" {
 
 /* Kernel-selection knobs (pxa_tuning). */
 #define PXA_TUNE_PGD_KERNEL 0 /* reserved (kernel variants measured slower were removed; 0 = the tile kernel) */
-#define PXA_TUNE_NORMAL_DIAG 1 /* pxa_dense_normal timing probes (WRONG results, measurement only): 0 off,
-                                  1 no x loads, 2 no cross-wave reduction, 3 no LDS accumulator */
+#define PXA_TUNE_NORMAL_KERNEL 1 /* A/B of pxa_dense_normal: 0 paired workgroups (each row split in two column
+                                    halves, the half-dots exchanged), 1 one workgroup per row (results equal up
+                                    to summation order), 2 paired workgroups that compute their partner's
+                                    half-dot instead of waiting for it (the same bits as 0) */
 #define PXA_TUNE_DENSE_KERNEL 2 /* A/B of the fp32 MFMA dense path (pxa_dense_matmat, B >= 32): 0 the LDS-staged
                                    kernel, 1 the register-streamed kernel of rounds 1-3 (same results up to
                                    summation order) */

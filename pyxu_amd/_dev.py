@@ -181,7 +181,7 @@ def storage_exclusive(t) -> bool:
     return _USE_COUNT(t.untyped_storage()._cdata) <= 2
 
 
-TUNE_NORMAL_DIAG = 1  # PXA_TUNE_NORMAL_DIAG: pxa_dense_normal timing probes (wrong results)
+TUNE_NORMAL_KERNEL = 1  # PXA_TUNE_NORMAL_KERNEL: pxa_dense_normal A/B (0 paired workgroups, 1 one per row, 2 paired without the exchange)
 TUNE_DENSE_KERNEL = 2  # PXA_TUNE_DENSE_KERNEL: 0 LDS-staged MFMA GEMM (B >= 32), 1 the register-streamed kernel
 TUNE_DUAL_WGS = 4  # PXA_TUNE_DUAL_WGS: kernel C's target workgroup count (A/B; 0 = default)
 TUNE_PGD_DIAG = 3  # PXA_TUNE_PGD_DIAG: bit 5 = s_memtime phase trace of the PGD tile kernel

@@ -4,6 +4,7 @@
 // with 16 B/lane loads and keep B running sums per lane in registers (B processed in register
 // chunks of kBC).  apply: one wavefront per row of A; adjoint: workgroups own (row-chunk x
 // column-tile) panels, write partial sums, a second pass adds the chunks in a fixed order.
+#include <atomic>
 #include "common.hpp"
 
 namespace pxa {
@@ -532,13 +533,6 @@ constexpr int kNormG = 256;  // workgroups (fixed: the partition, hence the roun
 constexpr int kNormRegAcc = 7;  // accumulator vectors per thread kept in registers
 typedef float nf4 __attribute__((ext_vector_type(4)));
 
-// A row vector, read once: non-temporal (streaming) policy, so that the 8 MB of rows an XCD streams per
-// row-time do not evict x (256 KB, re-read by every row) from its 4 MB L2.
-__device__ inline float4 ld_stream(const float4* p) {
-  const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-
 template <int NV>
 struct NormPlan {
   static constexpr int NL = NV > kNormRegAcc ? NV - kNormRegAcc : 0;  // accumulator vectors in LDS
@@ -546,82 +540,125 @@ struct NormPlan {
   static constexpr size_t LDS = (size_t)NL * kNormThreads * 16 + 2 * (kNormThreads / 64) * sizeof(double);
 };
 
-// DIAG != 0: timing probes with a part of the work removed (wrong results; PXA_TUNE_NORMAL_DIAG only):
-// 1 no x loads (the dot uses the row itself), 2 no cross-wave reduction (t = the thread's own dot),
-// 3 no LDS accumulator traffic.
-template <int NV, bool FULL, int DIAG = 0>
+// DPP operand of one double (two 32-bit halves through the same lane permutation)
+template <int CTRL>
+__device__ inline double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum of a double over the 64 lanes of a wave, the same value in every lane, in a fixed order: within each
+// 16-lane row by DPP (quad butterfly, then row rotations by 4 and 8), then the four row sums read from
+// lanes 0, 16, 32, 48 and added in ascending order.  No LDS round trips (a __shfl_down ladder is six
+// ds_bpermute pairs in series).
+__device__ inline double wave_sum_f64(double d) {
+  d += dpp_f64<0xB1>(d);   // quad_perm [1,0,3,2]
+  d += dpp_f64<0x4E>(d);   // quad_perm [2,3,0,1]: every lane holds its quad's sum
+  d += dpp_f64<0x124>(d);  // row_ror 4
+  d += dpp_f64<0x128>(d);  // row_ror 8: lane 16 r holds row r's sum
+  double r[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    r[q] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(d), 16 * q),
+                            __builtin_amdgcn_readlane(__double2loint(d), 16 * q));
+  return ((r[0] + r[1]) + r[2]) + r[3];
+}
+
+// Sum over the 16 doubles the waves of a workgroup left in red[0..15]: lanes 0..15 of every wave read one
+// each, a DPP reduction within lane row 0 (fixed order), the total read from lane 0 -- the same bits in
+// every wave, one LDS read instead of sixteen in series.
+__device__ inline double block_sum16_f64(const double* red, int lane) {
+  double v = lane < 16 ? red[lane] : 0.0;
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x124>(v);
+  v += dpp_f64<0x128>(v);
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 0),
+                          __builtin_amdgcn_readlane(__double2loint(v), 0));
+}
+
+// 16-B buffer loads: the row / x base lives in a scalar resource, the per-vector offset k * 16 KB in a
+// scalar offset, the lane offset tid * 16 in ONE vector register shared by every load (global loads would
+// hold a 64-bit address per in-flight vector).  Rows are read once (non-temporal, aux 2), x is re-read
+// by every row (default policy: it stays in the XCD's L2).
+template <int AUX>
+__device__ inline float4 buf_ld16(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const nf4 v = __builtin_bit_cast(nf4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+constexpr int kNormXAhead = 3;  // x vectors loaded ahead of the next row (issued before its loads)
+
+template <int NV, bool FULL>
 __global__ void __launch_bounds__(kNormThreads) normal_rows_kernel(int64_t M, int N4, const float* __restrict__ A,
                                                                    const float* __restrict__ x,
                                                                    float* __restrict__ part) {
   using P = NormPlan<NV>;
+  constexpr int XA = NV < kNormXAhead ? NV : kNormXAhead;
   extern __shared__ __align__(16) unsigned char nsm[];
   float4* accl = reinterpret_cast<float4*>(nsm);  // [NL][kNormThreads]
   double* red = reinterpret_cast<double*>(nsm + (size_t)P::NL * kNormThreads * 16);  // 2 x 16 (parity)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t G = gridDim.x;
-  const float4* A4 = reinterpret_cast<const float4*>(A);
-  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const int voff = tid * 16;
+  const int row_bytes = N4 * 16;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, row_bytes, 0x00020000);
+  auto row_rsrc = [&](int64_t r) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(A + r * (int64_t)N4 * 4), (short)0, row_bytes, 0x00020000);
+  };
+  auto live = [&](int k) { return FULL || tid + k * kNormThreads < N4; };
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 row[NV];
   float4 accr[P::NR];
+  float4 xq[XA];
 #pragma unroll
-  for (int k = 0; k < P::NR; ++k) accr[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < P::NR; ++k) accr[k] = z4;
 #pragma unroll
-  for (int k = 0; k < P::NL; ++k) accl[k * kNormThreads + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < P::NL; ++k) accl[k * kNormThreads + tid] = z4;
   int64_t m = blockIdx.x;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (m < M) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int j = tid + k * kNormThreads;
-      row[k] = (FULL || j < N4) ? ld_stream(A4 + m * N4 + j) : z4;
-    }
+    for (int k = 0; k < XA; ++k) xq[k] = live(k) ? buf_ld16<0>(xr, voff, k * kNormThreads * 16) : z4;
+    const __amdgpu_buffer_rsrc_t ar = row_rsrc(m);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) row[k] = live(k) ? buf_ld16<2>(ar, voff, k * kNormThreads * 16) : z4;
   }
   int par = 0;
   for (; m < M; m += G) {
-    // phase 1: t = <A[m,:], x>.  x is re-read every row (L2 hits): kept live across rows it would take
-    // 4 NV more registers, so its address is laundered per row to stop the compiler from hoisting it.
-    int xo = 0;
-    asm volatile("" : "+s"(xo));
-    const float4* xr = x4 + xo;
+    // phase 1: t = <A[m,:], x>.  The first XA x vectors were loaded before this row (vector loads
+    // complete in issue order, so the dot of vector k < XA waits only for row vector k); the rest
+    // follow XA ahead of their use.
     double d = 0.0;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-      const int j = tid + k * kNormThreads;
-      const float4 xv = DIAG == 1 ? row[k] : ((FULL || j < N4) ? xr[j] : z4);
+      const float4 xv = xq[k % XA];
+      if (k + XA < NV) xq[k % XA] = live(k + XA) ? buf_ld16<0>(xr, voff, (k + XA) * kNormThreads * 16) : z4;
       float q = row[k].x * xv.x;
       q = fmaf(row[k].y, xv.y, q);
       q = fmaf(row[k].z, xv.z, q);
       q = fmaf(row[k].w, xv.w, q);
       d += (double)q;
     }
-    double tt = d;
-    if (DIAG != 2) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) d += __shfl_down(d, off, 64);
-      if (lane == 0) red[par * 16 + wave] = d;
-      __syncthreads();
-      tt = 0.0;
-#pragma unroll
-      for (int w = 0; w < kNormThreads / 64; ++w) tt += red[par * 16 + w];  // fixed order, same in every thread
-      par ^= 1;  // the next row writes the other half: no second barrier needed
-    }
-    const float t = (float)tt;
-    // phase 2: acc += t * A[m,:]; each register refilled with the next row right after its last use
+    d = wave_sum_f64(d);
+    if (lane == 0) red[par * 16 + wave] = d;
+    __syncthreads();
+    const float t = (float)block_sum16_f64(red + par * 16, lane);
+    par ^= 1;  // the next row writes the other half: no second barrier needed
+    // phase 2: acc += t * A[m,:]; the next row's first x vectors, then each register refilled with the
+    // next row right after its last use (the last row re-reads itself: cache hits, unconditional refills)
     const int64_t mn = m + G;
     const bool more = mn < M;  // uniform
-    // uniform row base (SGPR) + lane offset; the last row re-reads itself (cache hits) so that the
-    // refills are unconditional
-    const float4* an = A4 + (more ? mn : m) * (int64_t)N4;
+#pragma unroll
+    for (int k = 0; k < XA; ++k) xq[k] = live(k) ? buf_ld16<0>(xr, voff, k * kNormThreads * 16) : z4;
+    const __amdgpu_buffer_rsrc_t an = row_rsrc(more ? mn : m);
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-      const int j = tid + k * kNormThreads;
       if (k < P::NR) {
         accr[k].x = fmaf(row[k].x, t, accr[k].x);
         accr[k].y = fmaf(row[k].y, t, accr[k].y);
         accr[k].z = fmaf(row[k].z, t, accr[k].z);
         accr[k].w = fmaf(row[k].w, t, accr[k].w);
-      } else if (DIAG == 3) {
-        accr[k % P::NR].x = fmaf(row[k].x, t, accr[k % P::NR].x);
       } else {
         float4 a = accl[(k - P::NR) * kNormThreads + tid];
         a.x = fmaf(row[k].x, t, a.x);
@@ -630,7 +667,7 @@ __global__ void __launch_bounds__(kNormThreads) normal_rows_kernel(int64_t M, in
         a.w = fmaf(row[k].w, t, a.w);
         accl[(k - P::NR) * kNormThreads + tid] = a;
       }
-      row[k] = (FULL || j < N4) ? ld_stream(an + j) : z4;
+      row[k] = live(k) ? buf_ld16<2>(an, voff, k * kNormThreads * 16) : z4;
     }
   }
   float4* out = reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * N4 * 4);
@@ -639,6 +676,341 @@ __global__ void __launch_bounds__(kNormThreads) normal_rows_kernel(int64_t M, in
     const int j = tid + k * kNormThreads;
     if (FULL || j < N4) out[j] = k < P::NR ? accr[k] : accl[(k - P::NR) * kNormThreads + tid];
   }
+}
+
+// ---- workgroup groups: each row split in kParts column parts, one per workgroup of a group
+// Workgroup (group c, part h) owns the float4 columns [h P4, min((h + 1) P4, N4)) (P4 = ceil(N4 / kParts))
+// of rows c, c + C, c + 2C, ... (C = G / kParts groups).  A quarter row is 16 VGPRs per thread at
+// N = 65536, so a workgroup holds kBufs = 3 of them -- row i being reduced, rows i + 1 and i + 2 streaming
+// in -- plus its part of the A^T (A x) accumulator in registers and its part of x in LDS (64 KB).  Per row:
+// the part-dot (per-thread fp32 partials summed in double, DPP wave sum, fixed-order workgroup sum),
+// published to the group as two 64-bit words tagged with the launch's tag (relaxed agent-scope stores; each
+// word validates itself, no fences), the other parts polled through the scalar unit, t = (float)(((d0 + d1)
+// + d2) + d3) in the same order in every member, acc += t * row, the freed buffer refilled with row i + 3.
+// While row i is reduced and exchanged, rows i + 1 and i + 2 stream: the one-workgroup-per-row kernel had
+// nothing in flight during that time.
+// Progress never depends on the other members being resident: a workgroup that waits longer than
+// kGroupWaitTicks for a part computes that part-dot itself (the same threads, loads and summation order,
+// hence the same bits) and stops waiting for later rows.  Members are g, g ^ 8, g ^ 16, g ^ 24 -- one XCD
+// under round-robin dispatch, so the exchange stays in one L2; with fewer than 8 groups (M < 8) every
+// workgroup computes all parts itself.  Partials: C x N fp32 (a quarter of the one-workgroup kernel's).
+#ifndef PXA_PROBES
+#define PXA_PROBES 0
+#endif
+constexpr bool kGroupProbes = PXA_PROBES != 0;  // probe build: per-workgroup timing stats, store-flavour A/B
+constexpr int kParts = 4;
+constexpr int kBufs = 4;
+constexpr int kGroupWaitTicks = 5000;  // 50 us of the 100 MHz clock
+constexpr int kGroupScratch = 2048;    // LDS bytes below the x part
+
+template <int NVS>
+struct GroupPlan {
+  static constexpr size_t LDS = (size_t)NVS * kNormThreads * 16 + kGroupScratch;
+};
+
+struct GroupGeom {
+  int group, part, P4;
+};
+
+__device__ inline GroupGeom group_geom(int g, int G, int N4) {
+  GroupGeom q;
+  if ((G / kParts) % 8 == 0) {
+    q.part = (g >> 3) & (kParts - 1);
+    q.group = (g >> 5) * 8 + (g & 7);
+  } else {
+    q.part = g % kParts;
+    q.group = g / kParts;
+  }
+  q.P4 = (N4 + kParts - 1) / kParts;
+  return q;
+}
+
+// One thread's share of a part-dot: the fp32 fma chain of each of its vectors, summed in double over k
+// ascending.  The owner reads the row from registers and x from LDS; a workgroup computing another part's
+// dot reads both from memory -- the same values in the same order, hence the same bits.
+__device__ inline float dot4(float4 a, float4 b) {
+  float q = a.x * b.x;
+  q = fmaf(a.y, b.y, q);
+  q = fmaf(a.z, b.z, q);
+  return fmaf(a.w, b.w, q);
+}
+
+// The 8 words of one row's exchange ([part][2]), read through the scalar unit from the XCD's L2 (glc: no
+// scalar-cache hit), all requests in flight together.  A vector load would complete only after every vector
+// load issued before it -- the rows in flight -- so polling with one would undo the multiple buffering.
+__device__ inline void poll_row(const unsigned long long* p, unsigned long long (&w)[8]) {
+  asm volatile(
+      "s_load_dwordx4 %0, %4, 0x0 glc\n\t"
+      "s_load_dwordx4 %1, %4, 0x10 glc\n\t"
+      "s_load_dwordx4 %2, %4, 0x20 glc\n\t"
+      "s_load_dwordx4 %3, %4, 0x30 glc\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=s"(*reinterpret_cast<__attribute__((ext_vector_type(4))) unsigned*>(&w[0])),
+        "=s"(*reinterpret_cast<__attribute__((ext_vector_type(4))) unsigned*>(&w[2])),
+        "=s"(*reinterpret_cast<__attribute__((ext_vector_type(4))) unsigned*>(&w[4])),
+        "=s"(*reinterpret_cast<__attribute__((ext_vector_type(4))) unsigned*>(&w[6]))
+      : "s"(p)
+      : "memory");
+}
+
+// The lane index, recomputed where it is used: the asm keeps the compiler from hoisting it out of the row
+// loop into a register that would then be spilled (a spill reload waits for every load in flight).
+__device__ inline int lane_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+// Workgroup sum of the per-thread doubles d (wave DPP sum, then the fixed-order sum of the 16 wave
+// sums); red: 16 doubles of scratch, one barrier.
+__device__ inline double group_block_sum(double d, double* red) {
+  d = wave_sum_f64(d);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (lane_here() == 0) red[wave] = d;
+  __syncthreads();
+  return block_sum16_f64(red, lane_here());
+}
+
+template <int NVS, bool FULL>
+__global__ void __launch_bounds__(kNormThreads) normal_group_kernel(int64_t M, int N4, const float* __restrict__ A,
+                                                                    const float* __restrict__ x,
+                                                                    float* __restrict__ part,
+                                                                    unsigned long long* __restrict__ slots,
+                                                                    int rows_per_group, unsigned tag, int solo,
+                                                                    unsigned long long* __restrict__ stats, int flav) {
+  extern __shared__ __align__(16) unsigned char nsm[];
+  // LDS: scratch at the bottom (one base register + immediates): red[b][0, 16) the part-dot sums of buffer
+  // b's row, red[3 + b][0, 16) those of a part-dot computed here in another member's place, exch[b][part]
+  // the members' part-dots, arrived[b][part] whether they came; then this part of x, [NVS][kNormThreads]
+  double* red = reinterpret_cast<double*>(nsm);
+  double* exch = red + 6 * 16;
+  int* arrived = reinterpret_cast<int*>(exch + kBufs * kParts);
+  float4* xs = reinterpret_cast<float4*>(nsm + kGroupScratch);
+  const int tid = threadIdx.x;
+  const int G = gridDim.x, C = G / kParts;
+  const GroupGeom q = group_geom(blockIdx.x, G, N4);
+  const int c0 = q.part * q.P4;
+  auto width = [&](int h) { return N4 - h * q.P4 < q.P4 ? (N4 - h * q.P4 > 0 ? N4 - h * q.P4 : 0) : q.P4; };
+  const int W4 = width(q.part);
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const float4* A4 = reinterpret_cast<const float4*>(A);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto live = [&](int k, int w) { return FULL || tid + k * kNormThreads < w; };
+  const int voff = tid * 16;
+  auto rsrc = [&](const float4* base, int w) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, w * 16, 0x00020000);
+  };
+  {
+    const __amdgpu_buffer_rsrc_t xr = rsrc(x4 + c0, W4);
+#pragma unroll
+    for (int k = 0; k < NVS; ++k)
+      xs[k * kNormThreads + tid] = live(k, W4) ? buf_ld16<0>(xr, voff, k * kNormThreads * 16) : z4;
+  }
+  const int64_t R = M > q.group ? (M - q.group + C - 1) / C : 0;  // rows of this group
+  // four row buffers, four names (no dynamic indexing): when row i is reduced, row i - 1 waits for its
+  // members' part-dots and rows i + 1, i + 2 stream in
+  float4 b0[NVS], b1[NVS], b2[NVS], b3[NVS];
+  float4 acc[NVS];
+#pragma unroll
+  for (int k = 0; k < NVS; ++k) acc[k] = z4;
+  // a part row: unconditional loads (a branch around them would make the compiler's load counting wait for
+  // the rows in flight); outside the part the resource's range check returns zeros (the vector offset
+  // carries the whole offset, so that the check sees it)
+  auto load_row = [&](float4(&bb)[NVS], int64_t r) {
+    const __amdgpu_buffer_rsrc_t rr = rsrc(A4 + r * (int64_t)N4 + c0, W4);
+#pragma unroll
+    for (int k = 0; k < NVS; ++k)
+      bb[k] = FULL ? buf_ld16<2>(rr, voff, k * kNormThreads * 16) : buf_ld16<2>(rr, voff + k * kNormThreads * 16, 0);
+  };
+  // rows are taken as 1 + a multiple of 4 (the loop's shape); padding rows repeat the last row, their t unused
+  const int64_t last = q.group + (R > 0 ? R - 1 : 0) * (int64_t)C;
+  auto row_of = [&](int64_t i) { const int64_t r = q.group + i * C; return r < last ? r : last; };
+  const int64_t Rp = R > 0 ? (R + 2) / 4 * 4 + 1 : 0;  // >= R, = 1 mod 4
+  if (R > 0) {
+    load_row(b0, row_of(0));
+    load_row(b1, row_of(1));
+    load_row(b2, row_of(2));
+    load_row(b3, row_of(3));
+  }
+  __syncthreads();  // xs
+  // slots: [group][row][part][2 words]
+  unsigned long long* gs = slots + (int64_t)q.group * rows_per_group * kParts * 2;
+  const unsigned long long want = (unsigned long long)tag << 32;
+  // A member's part-dot that does not come in time sets `degraded` (the same in every thread: it is read
+  // from LDS after the barrier); from then on the poller looks once per row, the rows still go through the
+  // straight-line code below (only the refills as vector loads, so the compiler's load counting stays
+  // exact), and the workgroup redoes all its rows without the exchange afterwards.
+  int ticks = kGroupWaitTicks;
+  bool degraded = false;
+  double dm = 0.0;  // this workgroup's part-dot of the row just reduced
+  // tid 0: publish row i's part-dot
+  auto publish = [&](int64_t i, double v) {
+    unsigned long long* rs = gs + i * kParts * 2;
+    const unsigned long long hi = (unsigned)__double2hiint(v), lo = (unsigned)__double2loint(v);
+    // relaxed agent-scope 8-byte stores (write-through, sc1): the tagged words are visible to the members
+    // wherever they run.  Measured (scripts/normal_group_probe.py, r04k): 1.1 us of gather per row against
+    // 1.5 us with plain stores, whose line stays in the writer's L2 but reaches the pollers later.
+    if (kGroupProbes && (flav & 16)) {  // probe build A/B: plain stores
+      __hip_atomic_store(rs + q.part * 2, want | hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(rs + q.part * 2 + 1, want | lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      __hip_atomic_store(rs + q.part * 2, want | hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rs + q.part * 2 + 1, want | lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  // probe build: tid 0 sums its gather time and poll rounds, tid 64 its time from a step's start to the end
+  // of its dot (row arrival) and its barrier wait
+  unsigned long long st_gather = 0, st_polls = 0, st_dot = 0, st_bar = 0;
+  const unsigned long long st_t0 = kGroupProbes ? (unsigned long long)wall_clock64() : 0;
+  // tid 0: the members' part-dots of row i (own = v) into exch[e], arrived[e]
+  auto gather = [&](int64_t i, double v, int e) {
+    unsigned long long* rs = gs + i * kParts * 2;
+    int got = 1 << q.part;
+    double w[kParts];
+#pragma unroll
+    for (int h = 0; h < kParts; ++h) w[h] = v;
+    const uint64_t g0 = (uint64_t)wall_clock64();
+    const uint64_t until = g0 + (uint64_t)ticks;
+    for (;;) {
+      unsigned long long pw[8];
+      poll_row(rs, pw);
+      if (kGroupProbes) ++st_polls;
+#pragma unroll
+      for (int h = 0; h < kParts; ++h) {
+        if (got & (1 << h)) continue;
+        const unsigned long long w0 = pw[2 * h], w1 = pw[2 * h + 1];
+        if ((w0 >> 32) == tag && (w1 >> 32) == tag) {
+          w[h] = __hiloint2double((int)(unsigned)w0, (int)(unsigned)w1);
+          got |= 1 << h;
+        }
+      }
+      if (got == (1 << kParts) - 1 || (uint64_t)wall_clock64() > until) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int h = 0; h < kParts; ++h) exch[e * kParts + h] = w[h];
+    arrived[e] = got == (1 << kParts) - 1;
+    if (kGroupProbes) st_gather += (uint64_t)wall_clock64() - g0;
+  };
+  // after the barrier: t of the row gathered into exch[e]; acc += t * that row (not for a padding row)
+  auto finish = [&](float4(&bb)[NVS], int64_t i, int e) {
+    if (!arrived[e]) {
+      degraded = true;
+      ticks = 0;
+    }
+    double tot = exch[e * kParts];
+#pragma unroll
+    for (int h = 1; h < kParts; ++h) tot += exch[e * kParts + h];
+    const float t = (float)tot;
+    const bool real = i < R;
+#pragma unroll
+    for (int k = 0; k < NVS; ++k) {
+      acc[k].x = real ? fmaf(bb[k].x, t, acc[k].x) : acc[k].x;
+      acc[k].y = real ? fmaf(bb[k].y, t, acc[k].y) : acc[k].y;
+      acc[k].z = real ? fmaf(bb[k].z, t, acc[k].z) : acc[k].z;
+      acc[k].w = real ? fmaf(bb[k].w, t, acc[k].w) : acc[k].w;
+    }
+    // pin these FMAs before the refill that follows (the asm consumes acc; its memory clobber keeps the
+    // loads after it): the buffer's old and new values must not overlap, or the loop-carried buffers get
+    // copied at the back edge, and a copy waits for its load
+#pragma unroll
+    for (int k = 0; k < NVS; ++k) asm volatile("" : "+v"(acc[k].x), "+v"(acc[k].y), "+v"(acc[k].z), "+v"(acc[k].w)::"memory");
+  };
+  // Row i (buffer cur) is reduced; in the same barrier interval the poller gathers row i - 1's part-dots
+  // (published one row earlier, so normally already there); then row i - 1 (buffer prev) is accumulated and
+  // prev refilled with row i + 3.  One barrier per row.
+  auto step = [&](float4(&cur)[NVS], float4(&prev)[NVS], int64_t i) {
+    const uint64_t s0 = kGroupProbes && tid == 64 ? (uint64_t)wall_clock64() : 0;
+    double d = 0.0;
+#pragma unroll
+    for (int k = 0; k < NVS; ++k) d += (double)dot4(cur[k], xs[k * kNormThreads + tid]);
+    d = wave_sum_f64(d);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pi = (int)(i & 1), pe = (int)((i - 1) & 1);
+    if (lane_here() == 0) red[pi * 16 + wave] = d;
+    uint64_t s1 = 0;
+    if (kGroupProbes && tid == 64) {
+      s1 = (uint64_t)wall_clock64();
+      st_dot += s1 - s0;
+    }
+    if (tid == 0) gather(i - 1, dm, pe);
+    __syncthreads();
+    if (kGroupProbes && tid == 64) st_bar += (uint64_t)wall_clock64() - s1;
+    dm = block_sum16_f64(red + pi * 16, lane_here());
+    if (tid == 0) publish(i, dm);
+    finish(prev, i - 1, pe);
+    load_row(prev, row_of(i + 3));
+  };
+  if (!solo && R > 0) {
+    {  // row 0
+      double d = 0.0;
+#pragma unroll
+      for (int k = 0; k < NVS; ++k) d += (double)dot4(b0[k], xs[k * kNormThreads + tid]);
+      dm = group_block_sum(d, red);
+      if (tid == 0) publish(0, dm);
+    }
+    for (int64_t i = 1; i < Rp; i += 4) {
+      step(b1, b0, i);
+      step(b2, b1, i + 1);
+      step(b3, b2, i + 2);
+      step(b0, b3, i + 3);
+    }
+    // the last row (Rp - 1 = 0 mod 4: buffer b0)
+    if (tid == 0) gather(Rp - 1, dm, (int)((Rp - 1) & 1));
+    __syncthreads();
+    finish(b0, Rp - 1, (int)((Rp - 1) & 1));
+  }
+  if (solo || degraded) {
+    // every row without the exchange: each part-dot computed here from memory -- the same threads, values
+    // and summation order as its owner's, hence the same bits as the exchange gives
+#pragma unroll
+    for (int k = 0; k < NVS; ++k) acc[k] = z4;
+    for (int64_t i = 0; i < R; ++i) {
+      const int64_t row = q.group + i * C;
+      double tot = 0.0;
+#pragma unroll 1
+      for (int h = 0; h < kParts; ++h) {
+        const int wh = width(h);
+        const __amdgpu_buffer_rsrc_t ra = rsrc(A4 + row * (int64_t)N4 + h * q.P4, wh);
+        const __amdgpu_buffer_rsrc_t rx = rsrc(x4 + h * q.P4, wh);
+        double e = 0.0;
+#pragma unroll
+        for (int k = 0; k < NVS; ++k)
+          e += (double)dot4(live(k, wh) ? buf_ld16<2>(ra, voff, k * kNormThreads * 16) : z4,
+                            live(k, wh) ? buf_ld16<0>(rx, voff, k * kNormThreads * 16) : z4);
+        const double dh = group_block_sum(e, red + (3 + (h & 1)) * 16);  // consecutive sums alternate scratch
+        tot = h == 0 ? dh : tot + dh;
+      }
+      const float t = (float)tot;
+      const __amdgpu_buffer_rsrc_t ro = rsrc(A4 + row * (int64_t)N4 + c0, W4);
+#pragma unroll
+      for (int k = 0; k < NVS; ++k) {
+        const float4 a = live(k, W4) ? buf_ld16<2>(ro, voff, k * kNormThreads * 16) : z4;
+        acc[k].x = fmaf(a.x, t, acc[k].x);
+        acc[k].y = fmaf(a.y, t, acc[k].y);
+        acc[k].z = fmaf(a.z, t, acc[k].z);
+        acc[k].w = fmaf(a.w, t, acc[k].w);
+      }
+    }
+  }
+  if (kGroupProbes) {
+    if (tid == 0) {
+      stats[blockIdx.x * 8 + 0] = st_t0;
+      stats[blockIdx.x * 8 + 1] = (unsigned long long)wall_clock64();
+      stats[blockIdx.x * 8 + 2] = st_gather;
+      stats[blockIdx.x * 8 + 3] = st_polls;
+      stats[blockIdx.x * 8 + 4] = degraded ? 1 : 0;
+      stats[blockIdx.x * 8 + 5] = (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+    }
+    if (tid == 64) {
+      stats[blockIdx.x * 8 + 6] = st_dot;
+      stats[blockIdx.x * 8 + 7] = st_bar;
+    }
+  }
+  float4* out = reinterpret_cast<float4*>(part) + (int64_t)q.group * N4 + c0;
+#pragma unroll
+  for (int k = 0; k < NVS; ++k)
+    if (live(k, W4)) out[tid + k * kNormThreads] = acc[k];
 }
 
 // Fixed-order sum of the G workgroup partials in two launches with enough loads in flight: stage 1
@@ -683,8 +1055,46 @@ __global__ void __launch_bounds__(kBlock) normal_final_kernel(int N4, int slices
 }
 
 inline int normal_groups(int64_t M) { return (int)(M < kNormG ? M : kNormG); }
+// groups of the split kernel: a multiple of 8 (one XCD per group) when M allows, at most kNormG / kParts
+inline int normal_group_count(int64_t M) {
+  const int64_t cap = kNormG / kParts;
+  return (int)(M >= cap ? cap : M >= 8 ? M / 8 * 8 : M);
+}
 inline int normal_slices(int G) { return (G + kNormSlice - 1) / kNormSlice; }
-inline size_t normal_sums_offset(int G, int64_t N) { return ((size_t)G * (size_t)N * sizeof(float) + 255) / 256 * 256; }
+inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+inline size_t normal_sums_offset(int G, int64_t N) { return align256((size_t)G * (size_t)N * sizeof(float)); }
+// workspace: [partials (<= G x N fp32)][slice sums][pair exchange slots: P x rows per pair x 2 halves x 2 words]
+inline size_t normal_slots_offset(int64_t M, int64_t N) {
+  const int G = normal_groups(M);
+  return normal_sums_offset(G, N) + align256((size_t)normal_slices(G) * (size_t)N * sizeof(double));
+}
+inline int64_t normal_rows_per_group(int64_t M) {  // padded to 1 + a multiple of 4 (the kernel's row loop)
+  const int C = normal_group_count(M);
+  return ((M + C - 1) / C + 2) / 4 * 4 + 1;
+}
+inline size_t normal_stats_offset(int64_t M, int64_t N) {
+  return normal_slots_offset(M, N) + align256((size_t)normal_group_count(M) * (size_t)normal_rows_per_group(M) * kParts *
+                                              2 * sizeof(uint64_t));
+}
+// + 64 B per workgroup of probe-build stats
+inline size_t normal_workspace(int64_t M, int64_t N) {
+  return normal_stats_offset(M, N) + (size_t)kParts * normal_group_count(M) * 8 * sizeof(uint64_t);
+}
+
+// fixed-order sum of the `rows` partials (rows x N fp32 at work) and s * sum + d * x
+inline int normal_reduce(int rows, int64_t N, const float* x, float s, float d, float* Y, float* work, hipStream_t st) {
+  const int N4 = (int)(N / 4);
+  const int slices = normal_slices(rows);
+  double4* sums = reinterpret_cast<double4*>(reinterpret_cast<unsigned char*>(work) + normal_sums_offset(rows, N));
+  const unsigned cb = (unsigned)((N4 + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(normal_sum_kernel, dim3(cb, (unsigned)slices), dim3(kBlock), 0, st, N4, rows,
+                     reinterpret_cast<const float4*>(work), sums);
+  int e = last_launch_status();
+  if (e) return e;
+  hipLaunchKernelGGL(normal_final_kernel, dim3(cb), dim3(kBlock), 0, st, N4, slices, sums,
+                     reinterpret_cast<const float4*>(x), s, d, reinterpret_cast<float4*>(Y));
+  return last_launch_status();
+}
 
 template <int NV>
 int launch_normal(int64_t M, int64_t N, const float* A, const float* x, float s, float d, float* Y, float* work,
@@ -700,28 +1110,46 @@ int launch_normal(int64_t M, int64_t N, const float* A, const float* x, float s,
   }
   const int G = normal_groups(M);
   const int N4 = (int)(N / 4);
-  const int diag = NV == 16 ? tuning(PXA_TUNE_NORMAL_DIAG) : 0;
-  if (N4 == NV * kNormThreads && diag >= 1 && diag <= 3) {
-    auto kd = diag == 1 ? normal_rows_kernel<NV, true, 1> : diag == 2 ? normal_rows_kernel<NV, true, 2>
-                                                                       : normal_rows_kernel<NV, true, 3>;
-    (void)hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P::LDS);
-    hipLaunchKernelGGL(kd, dim3(G), dim3(kNormThreads), P::LDS, st, M, N4, A, x, work);
-  } else if (N4 == NV * kNormThreads)
+  if (N4 == NV * kNormThreads)
     hipLaunchKernelGGL((normal_rows_kernel<NV, true>), dim3(G), dim3(kNormThreads), P::LDS, st, M, N4, A, x, work);
   else
     hipLaunchKernelGGL((normal_rows_kernel<NV, false>), dim3(G), dim3(kNormThreads), P::LDS, st, M, N4, A, x, work);
-  int e = last_launch_status();
-  if (e) return e;
-  const int slices = normal_slices(G);
-  double4* sums = reinterpret_cast<double4*>(reinterpret_cast<unsigned char*>(work) + normal_sums_offset(G, N));
-  const unsigned cb = (unsigned)((N4 + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(normal_sum_kernel, dim3(cb, (unsigned)slices), dim3(kBlock), 0, st, N4, G,
-                     reinterpret_cast<const float4*>(work), sums);
-  e = last_launch_status();
-  if (e) return e;
-  hipLaunchKernelGGL(normal_final_kernel, dim3(cb), dim3(kBlock), 0, st, N4, slices, sums,
-                     reinterpret_cast<const float4*>(x), s, d, reinterpret_cast<float4*>(Y));
-  return last_launch_status();
+  const int e = last_launch_status();
+  return e ? e : normal_reduce(G, N, x, s, d, Y, work, st);
+}
+
+template <int NVS>
+int launch_normal_group(int64_t M, int64_t N, const float* A, const float* x, float s, float d, float* Y, float* work,
+                        bool solo, hipStream_t st) {
+  const size_t lds = GroupPlan<NVS>::LDS;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)normal_group_kernel<NVS, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)normal_group_kernel<NVS, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  static std::atomic<unsigned> launches{0};
+  // exchange tag: a fresh value per launch (slots of earlier launches never match), high byte 0xA5 so that
+  // small integers left in a reused workspace do not either
+  const unsigned tag = 0xA5000000u | (launches.fetch_add(1) & 0x00FFFFFFu);
+  const int C = normal_group_count(M);
+  const int N4 = (int)(N / 4);
+  const int P4 = (N4 + kParts - 1) / kParts;
+  auto* slots = reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(work) + normal_slots_offset(M, N));
+  const int rpg = (int)normal_rows_per_group(M);
+  solo = solo || C % 8 != 0;  // fewer than 8 groups: the members would not share an XCD
+  auto* stats = reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(work) + normal_stats_offset(M, N));
+  const int flav = kGroupProbes ? tuning(PXA_TUNE_NORMAL_KERNEL) : 0;
+  if (P4 * kParts == N4 && P4 == NVS * kNormThreads)
+    hipLaunchKernelGGL((normal_group_kernel<NVS, true>), dim3(kParts * C), dim3(kNormThreads), lds, st, M, N4, A, x,
+                       work, slots, rpg, tag, (int)solo, stats, flav);
+  else
+    hipLaunchKernelGGL((normal_group_kernel<NVS, false>), dim3(kParts * C), dim3(kNormThreads), lds, st, M, N4, A, x,
+                       work, slots, rpg, tag, (int)solo, stats, flav);
+  const int e = last_launch_status();
+  return e ? e : normal_reduce(C, N, x, s, d, Y, work, st);
 }
 
 }  // namespace
@@ -789,9 +1217,7 @@ int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, cons
 
 size_t pxa_dense_normal_workspace_bytes(int dtype, int64_t M, int64_t N, int64_t B) {
   if (dtype != PXA_F32 || B != 1 || N % 4 != 0 || N > kNormMaxN || M < 1) return 0;
-  const int G = normal_groups(M);
-  // G fp32 partials, then the slice sums (double4 per column group) at a 256-byte aligned offset
-  return normal_sums_offset(G, N) + (size_t)normal_slices(G) * (size_t)N * sizeof(double);
+  return normal_workspace(M, N);
 }
 
 int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, const void* X, double s, double d,
@@ -806,6 +1232,14 @@ int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, 
   const float* a = (const float*)A;
   const float* x = (const float*)X;
   const float fs = (float)s, fd = (float)d;
+  const int kern = tuning(PXA_TUNE_NORMAL_KERNEL) & 15;  // (probe build: bit 4 selects plain exchange stores)
+  if (kern != 1) {  // split rows (2: without the exchange, every part-dot computed by every member; same bits)
+    const int64_t nvs = ((N / 4 + kParts - 1) / kParts + kNormThreads - 1) / kNormThreads;  // vectors per part
+    const bool solo = kern == 2;
+    if (nvs <= 1) return launch_normal_group<1>(M, N, a, x, fs, fd, (float*)Y, (float*)work, solo, st);
+    if (nvs <= 2) return launch_normal_group<2>(M, N, a, x, fs, fd, (float*)Y, (float*)work, solo, st);
+    return launch_normal_group<4>(M, N, a, x, fs, fd, (float*)Y, (float*)work, solo, st);
+  }
   const int64_t nv = (N / 4 + kNormThreads - 1) / kNormThreads;  // vectors per thread
   if (nv <= 1) return launch_normal<1>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
   if (nv <= 2) return launch_normal<2>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);

@@ -37,15 +37,15 @@
 // Measurement probes (s_memtime phase trace, skip probes, staggered starts: PXA_TUNE_PGD_DIAG /
 // PXA_TUNE_PGD_STAGGER) exist only in the probe build (`make -C pyxu_amd/csrc probe`, scripts/ that time
 // kernel phases); the production library compiles them out, so its kernel carries no probe branch.
-#ifndef PXA_PGD_PROBES
-#define PXA_PGD_PROBES 0
+#ifndef PXA_PROBES
+#define PXA_PROBES 0
 #endif
 
 namespace pxa {
 namespace {
 
 using namespace tile2d;
-constexpr bool kProbes = PXA_PGD_PROBES != 0;
+constexpr bool kProbes = PXA_PROBES != 0;
 
 
 template <typename T>

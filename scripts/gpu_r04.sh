@@ -83,6 +83,19 @@ if [ "$S" = "c4b" ]; then
   python3 scripts/c4_timeline.py $P/c4b || true
   step c4host 300 python3 scripts/c4_host_prof.py
 fi
+if [ "$S" = "nab" ]; then
+  step cgtests 600 $PT -m gpu tests/test_gpu_dense_normal.py tests/test_gpu_parity.py tests/test_gpu_bench_shapes.py tests/test_gpu_distributed.py -k "cg or admm or normal or sharded or dense"
+  step nab 600 python3 scripts/normal_ab.py --all
+  step c4 300 python3 bench.py --only c4
+  step c4stamps 300 python3 scripts/c4_host_stamps.py
+fi
+if [ "$S" = "ngp" ]; then
+  export PXA_LIB_PATH=build/libpyxu_amd_probe.so
+  step ngp0 120 python3 scripts/normal_group_probe.py 0
+  step ngp16 120 python3 scripts/normal_group_probe.py 16
+  unset PXA_LIB_PATH
+  step nab 600 python3 scripts/normal_ab.py --all
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"

@@ -3,6 +3,8 @@ GPU tests of the one-pass normal operator (pxa_dense_normal) and of its use insi
   * the kernel against a float64 NumPy restatement of s * A^T (A x) + d * x (north_star fp32 tolerance
     1e-5 norm-wise), for every register/LDS split of the row (N = 256 .. 65536, full and ragged last
     vector blocks, M smaller and larger than the 256-workgroup partition), and bit-identical run to run;
+  * the row-split kernel (part-dots exchanged between four workgroups) against its no-exchange path bit for
+    bit, and against the one-workgroup-per-row kernel;
   * the operator-tree matcher on the operator ADMM builds (reference abc/operator.py:1273-1291,
     abc/arithmetic.py:1255-1264), and on trees it must reject;
   * ADMM / CG trajectories through the fused operator against the unfused operator and the oracle.
@@ -47,6 +49,35 @@ def test_dense_normal_vs_fp64(M, N):
     torch.cuda.synchronize()
     assert torch.equal(y1, y2)  # fixed partition and summation order
     assert rel_err(to_NUMPY(y1), _ref(A, x, 0.7, 1.3)) <= 1e-5
+
+
+@pytest.mark.parametrize("M,N", [(1, 4), (3, 16), (8, 1000), (100, 4100), (257, 65532), (771, 65536), (2048, 65536),
+                                 (8192, 65536)])
+def test_dense_normal_kernels_agree(M, N):
+    """The row-split kernel (PXA_TUNE_NORMAL_KERNEL 0: four workgroups per row, part-dots exchanged) against
+    the same kernel computing every part-dot itself (2: the path a workgroup takes when a member is late) BIT
+    FOR BIT, and both against the one-workgroup-per-row kernel (1) and float64 within the fp32 tolerance: group
+    counts below 8 (solo), ragged parts (N4 not a multiple of 4 x 1024), row counts that leave padding rows."""
+    rng = np.random.default_rng(M * 7 + N)
+    A = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float32)
+    x = rng.standard_normal(N).astype(np.float32)
+    Ad, xd = to_device(A), to_device(x)
+    out = {}
+    old = _dev.tuning(_dev.TUNE_NORMAL_KERNEL, 0)
+    try:
+        for mode in (0, 2, 1, 0):
+            _dev.tuning(_dev.TUNE_NORMAL_KERNEL, mode)
+            y = _dev.dense_normal(Ad, xd, 0.7, 1.3)
+            torch.cuda.synchronize()
+            if mode in out:
+                assert torch.equal(out[mode], y)  # run to run
+            out[mode] = y
+    finally:
+        _dev.tuning(_dev.TUNE_NORMAL_KERNEL, old)
+    assert torch.equal(out[0], out[2])
+    ref = _ref(A, x, 0.7, 1.3)
+    assert rel_err(to_NUMPY(out[0]), ref) <= 1e-5
+    assert rel_err(to_NUMPY(out[1]), ref) <= 1e-5
 
 
 def test_dense_normal_refuses_unsupported():
