@@ -49,10 +49,10 @@ extern "C" {
 
 /* Kernel-selection knobs (pxa_tuning). */
 #define PXA_TUNE_PGD_KERNEL 0 /* reserved (kernel variants measured slower were removed; 0 = the tile kernel) */
-#define PXA_TUNE_NORMAL_KERNEL 1 /* A/B of pxa_dense_normal: 0 paired workgroups (each row split in two column
-                                    halves, the half-dots exchanged), 1 one workgroup per row (results equal up
-                                    to summation order), 2 paired workgroups that compute their partner's
-                                    half-dot instead of waiting for it (the same bits as 0) */
+#define PXA_TUNE_NORMAL_KERNEL 1 /* A/B of pxa_dense_normal: 0 row-split kernel (each row in four column parts,
+                                    one workgroup each, part-dots exchanged), 1 one workgroup per row (results
+                                    equal up to summation order), 2 the row-split kernel computing every part-dot
+                                    in every member instead of exchanging (the same bits as 0) */
 #define PXA_TUNE_DENSE_KERNEL 2 /* A/B of the fp32 MFMA dense path (pxa_dense_matmat, B >= 32): 0 the LDS-staged
                                    kernel, 1 the register-streamed kernel of rounds 1-3 (same results up to
                                    summation order) */
@@ -310,7 +310,10 @@ int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, cons
  * QuadraticFunc.prox builds for ADMM's x-update (abc/operator.py:1273-1291 QuadraticFunc.prox,
  * opt/solver/pds.py:1645-1653, Q = K^T c K from abc/arithmetic.py ChainRule._quad_spec), i.e. the
  * K.apply -> K.adjoint -> AddRule chain of opt/solver/cg.py:130 (`Ap = self._A.apply(p)`).
- * Workgroup partials of A^T (A X) (fixed partition) are summed in a fixed order: deterministic.
+ * Each row is split in four column parts, one per workgroup of a group; the part-dots are exchanged
+ * inside the launch (a member that does not answer in time is replaced by computing its part here, with
+ * the same bits), t = ((d0 + d1) + d2) + d3 in every member.  Workgroup partials of A^T (A X) (fixed
+ * partition) are summed in a fixed order: deterministic.  The workspace also holds the exchange words.
  * pxa_dense_normal_workspace_bytes() returns 0 for unsupported cases, where pxa_dense_normal returns
  * PXA_ERR_UNSUPPORTED (the caller then composes pxa_dense_matmat calls). */
 size_t pxa_dense_normal_workspace_bytes(int dtype, int64_t M, int64_t N, int64_t B);
