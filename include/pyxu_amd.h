@@ -57,7 +57,7 @@ extern "C" {
                                    kernel, 1 the register-streamed kernel of rounds 1-3 (same results up to
                                    summation order) */
 #define PXA_TUNE_DUAL_WGS 4 /* A/B of the PDS dual-update kernel C: workgroups it aims for when it splits the
-                               axis-0 march into segments (0: 4096) */
+                               axis-0 march into segments (0: 2048) */
 #define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel, PROBE BUILD ONLY (make -C pyxu_amd/csrc probe; the production
                               library ignores it): bit 5 s_memtime phase trace (pxa_pgd_tile_trace); timing probes
                               with WRONG results: bit 6 skips passes A / B, bit 7 the window loads, bit 8 loads x only

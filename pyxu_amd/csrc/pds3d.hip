@@ -168,8 +168,8 @@ int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, co
 }
 
 // Kernel C over a whole (stack, n0, n1, n2) geometry: z_out = relax(fenchel_prox_h(z + sigma K w)).  The
-// march is split into axis-0 segments so that about 4096 workgroups are in flight (no halo: w(p + 1) is a
-// plain load).  pd3o selects the relaxation order: (1 - rho) z + rho z_t, else rho z_t + (1 - rho) z.
+// march is split into axis-0 segments so that about 2048 workgroups are in flight (no halo: w(p + 1) is a
+// plain load; at 1024^3 2048 took 5.0-5.1 ms against 5.1-5.7 ms at 4096, profiles/r04_k4_wgs.txt).  pd3o selects the relaxation order: (1 - rho) z + rho z_t, else rho z_t + (1 - rho) z.
 template <typename T>
 int run_c(const PdsGeom<T>& g, T sigma, T lam, T rho, T omr, bool pd3o, bool iso, const void* w, const void* z,
           void* z_out, hipStream_t st) {
@@ -184,7 +184,7 @@ int run_c(const PdsGeom<T>& g, T sigma, T lam, T rho, T omr, bool pd3o, bool iso
   const bool vec = (g.n2 % V == 0) && aligned16(w) && aligned16(z) && aligned16(z_out);
   const int nv = vec ? V : 1;
   const int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
-  const int64_t target = tuning(PXA_TUNE_DUAL_WGS) > 0 ? tuning(PXA_TUNE_DUAL_WGS) : 4096;  // A/B knob
+  const int64_t target = tuning(PXA_TUNE_DUAL_WGS) > 0 ? tuning(PXA_TUNE_DUAL_WGS) : 2048;  // A/B knob
   int cseg = (int)((target + blocks - 1) / blocks);
   if (cseg > g.n0) cseg = g.n0;
   if (cseg < 1) cseg = 1;

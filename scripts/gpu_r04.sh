@@ -97,8 +97,10 @@ if [ "$S" = "ngp" ]; then
   step nab 600 python3 scripts/normal_ab.py --all
 fi
 if [ "$S" = "full" ]; then
-  step pytest 1200 $PT tests -m gpu
-  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-  step bench 900 python bench.py --steps 20 --warmup 5
+  step pytest 1000 $PT tests -m gpu
+  step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$S" = "bench" ]; then
+  step bench 1000 python bench.py --steps 20 --warmup 5
 fi
 echo done
