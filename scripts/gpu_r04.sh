@@ -96,6 +96,15 @@ if [ "$S" = "ngp" ]; then
   unset PXA_LIB_PATH
   step nab 600 python3 scripts/normal_ab.py --all
 fi
+if [ "$S" = "pgdp" ]; then
+  export PXA_LIB_PATH=build/libpyxu_amd_probe.so
+  step stag 300 python3 scripts/pgd_modes_probe.py stagger
+  step modes 300 python3 scripts/pgd_modes_probe.py diag 2048
+  for d in 0 64 128 192; do
+    step pmc_lds_$d 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAVES -d $P/lds_$d -o run --output-format csv -- python3 scripts/pgd_modes_probe.py one $d
+  done
+  unset PXA_LIB_PATH
+fi
 if [ "$S" = "full" ]; then
   step pytest 1000 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"

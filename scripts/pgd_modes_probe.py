@@ -3,7 +3,8 @@ at n x n images (`stack` images of n x n with per-image data when given as n:sta
 with parts of its work skipped (PXA_TUNE_PGD_DIAG bits 6-8: WRONG results, timing only), which prices the
 window loads, the passes and the rest.  Each configuration is timed as windows of back-to-back launches between
 two HIP events (the bench's LaunchTimer convention), interleaved over 5 rounds; prints the median per launch.
-usage: python scripts/pgd_modes_probe.py diag [n[:stack] ...]"""
+usage: python scripts/pgd_modes_probe.py diag [n[:stack] ...] | stagger | one <diag>   (probe build:
+PXA_LIB_PATH=build/libpyxu_amd_probe.so)"""
 import sys
 
 import numpy as np
@@ -63,7 +64,36 @@ def diag_probe(sizes):
 
 
 
+def stagger_probe(n=2048):
+    """first-round workgroups picked by `sel` start n x 1024 cycles late (PXA_TUNE_PGD_STAGGER, probe build):
+    same results, only the phase of the four workgroups of a CU changes"""
+    a, pre = setup(n, 1)
+    cfg = [0] + [(sel << 8) | d for sel in (1, 2, 3, 4) for d in (4, 8, 12, 20)]
+    res = {c: [] for c in cfg}
+    for _ in range(5):
+        for c in cfg:
+            old = _dev.tuning(_dev.TUNE_PGD_STAGGER, c)
+            window(a, pre, 1, 3)
+            res[c].append(window(a, pre, 1, 40))
+            _dev.tuning(_dev.TUNE_PGD_STAGGER, old)
+    for c, v in res.items():
+        print(f"n={n} stagger sel={c >> 8} delay={c & 255}x1024 cyc {np.median(v):9.2f} us", flush=True)
+
+
+def one(diag, n=2048, launches=30):
+    """`launches` launches with PXA_TUNE_PGD_DIAG = diag (for rocprofv3 --pmc passes, one variant per run)"""
+    a, pre = setup(n, 1)
+    _dev.tuning(_dev.TUNE_PGD_DIAG, diag)
+    for _ in range(launches):
+        launch(a, pre)
+    torch.cuda.synchronize()
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "stagger":
+        return stagger_probe()
+    if len(sys.argv) > 2 and sys.argv[1] == "one":
+        return one(int(sys.argv[2]))
     return diag_probe([v for v in sys.argv[1:] if v != "diag"] or ["2048", "4096", "512:512"])
 
 
