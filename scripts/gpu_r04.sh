@@ -105,6 +105,12 @@ if [ "$S" = "pgdp" ]; then
   done
   unset PXA_LIB_PATH
 fi
+if [ "$S" = "timer" ]; then
+  for i in 1 2 3; do
+    step drvt$i 120 $DRV
+    step drvn$i 120 $DRV --no-kernel-timer
+  done
+fi
 if [ "$S" = "full" ]; then
   step pytest 1000 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
