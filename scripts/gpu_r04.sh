@@ -111,6 +111,13 @@ if [ "$S" = "timer" ]; then
     step drvn$i 120 $DRV --no-kernel-timer
   done
 fi
+if [ "$S" = "fft" ]; then
+  step ops 300 python3 scripts/bench_ops.py
+  step ffttrace 120 rocprofv3 --kernel-trace --stats -d $P/fft_trace -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048
+  step fftfetch 90 rocprofv3 --pmc FETCH_SIZE -d $P/fft_fetch -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+  step fftwrite 90 rocprofv3 --pmc WRITE_SIZE -d $P/fft_write -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+  step fftsq 90 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAVES -d $P/fft_sq -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+fi
 if [ "$S" = "full" ]; then
   step pytest 1000 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
