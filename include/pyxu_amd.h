@@ -68,7 +68,10 @@ extern "C" {
                                  of its kernels (pxa_pds_kernel_ms) */
 #define PXA_TUNE_PDS_MARCH 7 /* A/B of pxa_pds_step_la's kernel D: bit 0 lets a thread own two positions
                                 (default one) */
-#define PXA_TUNE_COUNT 8
+#define PXA_TUNE_FFT_KERNEL 8 /* A/B of the in-LDS FFT (pxa_fft, lines that fit one workgroup): 0 in-place register-staged
+                                 stages on padded lines with a twiddle table, 1 the ping-pong Stockham kernel of rounds
+                                 1-3 (results equal up to rounding) */
+#define PXA_TUNE_COUNT 9
 
 /* Row reductions (pxa_row_reduce). */
 #define PXA_RED_SUMSQ 0  /* sum x^2            : SquaredL2Norm.apply, norm(ord=2)^2   (norm.py:91-94) */

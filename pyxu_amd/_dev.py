@@ -207,13 +207,14 @@ def storage_exclusive(t) -> bool:
     return _USE_COUNT(t.untyped_storage()._cdata) <= 2
 
 
-TUNE_NORMAL_KERNEL = 1  # PXA_TUNE_NORMAL_KERNEL: pxa_dense_normal A/B (0 paired workgroups, 1 one per row, 2 paired without the exchange)
+TUNE_NORMAL_KERNEL = 1  # PXA_TUNE_NORMAL_KERNEL: pxa_dense_normal A/B (0 row-split, 1 one workgroup per row, 2 row-split without the exchange)
 TUNE_DENSE_KERNEL = 2  # PXA_TUNE_DENSE_KERNEL: 0 LDS-staged MFMA GEMM (B >= 32), 1 the register-streamed kernel
 TUNE_DUAL_WGS = 4  # PXA_TUNE_DUAL_WGS: kernel C's target workgroup count (A/B; 0 = default)
 TUNE_PGD_DIAG = 3  # PXA_TUNE_PGD_DIAG: bit 5 = s_memtime phase trace of the PGD tile kernel
 TUNE_PGD_STAGGER = 6  # PXA_TUNE_PGD_STAGGER: (sel << 8) | n, delayed first-round workgroups (A/B probe)
 TUNE_PDS_EVENTS = 5  # PXA_TUNE_PDS_EVENTS: per-kernel HIP events inside pxa_pds_step (pds_kernel_ms)
 TUNE_PDS_MARCH = 7  # PXA_TUNE_PDS_MARCH: kernel D A/B (bit 0: two positions per thread)
+TUNE_FFT_KERNEL = 8  # PXA_TUNE_FFT_KERNEL: 0 in-place register-staged FFT kernel, 1 the ping-pong Stockham kernel
 
 
 def tuning(key, value=-1):

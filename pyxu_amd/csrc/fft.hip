@@ -15,11 +15,19 @@
 // the stride-n2 axis, twiddles w_n^(k1 j2), n2-point DFTs stored transposed into a workspace, copied
 // back); other lengths by Bluestein's chirp-z (chirp, 2^k-point FFT convolution with the chirp filter,
 // chirp), so every length runs, as in the reference's scipy.fft.
+#include <map>
+#include <mutex>
+
 #include "common.hpp"
+
+#ifndef PXA_PROBES
+#define PXA_PROBES 0
+#endif
 
 namespace pxa {
 namespace {
 
+constexpr bool kFftProbes = PXA_PROBES != 0;
 constexpr int kFftThreads = 256;
 constexpr int kMaxStages = 24;
 constexpr size_t kFftLds = 64 * 1024;  // two LDS buffers of lines (2 workgroups per CU)
@@ -44,6 +52,24 @@ __device__ inline Cx<T> csub(Cx<T> a, Cx<T> b) {
 template <typename T, bool INV>
 __device__ inline Cx<T> mul_mi(Cx<T> a) {
   return INV ? Cx<T>{-a.im, a.re} : Cx<T>{a.im, -a.re};
+}
+// fp32: complex arithmetic on 2-vectors, so that it issues as packed fp32 (v_pk_add / v_pk_mul / v_pk_fma:
+// two lanes' worth of fp32 per instruction; the FFT kernels are VALU-bound at these counts)
+typedef float PkF32 __attribute__((ext_vector_type(2)));
+__device__ inline PkF32 pk(Cx<float> a) { return PkF32{a.re, a.im}; }
+__device__ inline Cx<float> unpk(PkF32 a) { return Cx<float>{a.x, a.y}; }
+template <>
+__device__ inline Cx<float> cadd(Cx<float> a, Cx<float> b) {
+  return unpk(pk(a) + pk(b));
+}
+template <>
+__device__ inline Cx<float> csub(Cx<float> a, Cx<float> b) {
+  return unpk(pk(a) - pk(b));
+}
+template <>
+__device__ inline Cx<float> cmul(Cx<float> a, Cx<float> b) {
+  const PkF32 t = PkF32{a.re, a.re} * pk(b);
+  return unpk(__builtin_elementwise_fma(PkF32{a.im, a.im}, PkF32{-b.im, b.re}, t));
 }
 
 __device__ inline void sc_pi(float x, float* s, float* c) { sincospif(x, s, c); }
@@ -127,6 +153,8 @@ struct FftPlan {
   int64_t n, inner, lines;  // axis length, stride of the axis (elements), number of lines
   int64_t tn1;              // 0: results back in place of the line; > 0: four-step transposed store (below)
   int lpb;                  // lines per workgroup
+  int pitch;                // fft_lds_kernel: LDS elements per line
+  int probe;                // fft_lds_kernel, probe build only: 16 skip stages, 32 skip loads, 64 skip stores
   int nst;
   int radix[kMaxStages];
 };
@@ -258,6 +286,266 @@ __global__ void __launch_bounds__(kFftThreads) fft_direct_kernel(FftPlan p, cons
   move_lines<T>(p, line, 1, dst, x, false);
 }
 
+// ---- in-place FFT of lines resident in LDS (PXA_TUNE_FFT_KERNEL 0, the default)
+// The ping-pong kernel above keeps two copies of its lines (so only 2 lines of 2048 fp32 per workgroup:
+// 16-B pieces of each row on a strided axis, 3.1x the compulsory HBM bytes, profiles/r04t_fft_pmc.txt),
+// writes each Stockham stage with stride R (8-way LDS bank conflicts at R = 8: 6.7 M extra cycles against
+// 2.8 M active) and evaluates a sincospi per butterfly.  This one: one copy of kLdsFftBytes of lines per
+// workgroup (8 lines of 2048 fp32: 64-B pieces of each row, adjacent line groups on one XCD so that the
+// rest of each 128-B line is an L2 hit), every stage in place -- all threads read their butterflies'
+// inputs into registers, barrier, write the outputs -- on swizzled lines (fft_padi: no bank conflicts),
+// twiddles w_n^m read from a table built once per length in double precision (exact to the rounding of T).
+// Power-of-two lengths.
+constexpr int kLdsFftThreads = 512;
+constexpr size_t kLdsFftBytes = 64 * 1024;  // line data per workgroup (+ pitch padding): two workgroups per CU
+
+template <typename T>
+struct LdsFft {
+  static constexpr int E = (int)(kLdsFftBytes / sizeof(Cx<T>));  // elements per workgroup: 16384 fp32, 8192 fp64
+  static constexpr int PER = E / kLdsFftThreads;                  // per thread and stage: 16 / 8
+};
+
+// Position m of a line at m ^ ((m >> 3) & 15) (a permutation within aligned blocks of 16), lines at a pitch
+// of n + 16 / min(L, 16): every Stockham stage's reads and writes and both load / store orders are free of
+// bank conflicts for the power-of-two lengths (checked with the MI355X_MICROARCH.md bank model)
+__host__ __device__ inline int fft_padi(int i) { return i ^ ((i >> 3) & 15); }
+__host__ __device__ inline int fft_pitch(int n, int L) { return n + 16 / (L < 16 ? L : 16); }
+
+// x / d and x % d for x, d < 2^16 by one multiply-high (m = floor((2^32 - 1) / d) + 1 is exact there)
+struct FastDiv {
+  unsigned d, m;
+  __device__ explicit FastDiv(unsigned dd) : d(dd), m(0xFFFFFFFFu / dd + 1u) {}
+  __device__ inline unsigned div(unsigned x) const { return d == 1u ? x : __umulhi(x, m); }
+};
+
+template <typename T, bool INV, int R>
+__device__ inline void dft_r(Cx<T>* v) {
+  if constexpr (R == 2) dft2<T, INV>(v);
+  else if constexpr (R == 4) dft4<T, INV>(v);
+  else if constexpr (R == 8) dft8<T, INV>(v);
+  else dft_odd<T, INV, R>(v);
+}
+
+// One radix-R Stockham stage over L padded lines (pitch P) in place: v[r] = x[j + r n / R],
+// twiddled by w_{ns R}^(r (j mod ns)) = tw[ns + (j mod ns)] ^ r, DFT_R, written to
+// (j div ns) ns R + (j mod ns) + r ns.  n / R = 2^lnr and ns = 2^lns (power-of-two lengths): indices by
+// shifts and masks.  A step that is a multiple of 128 leaves bits 0-6 alone, so fft_padi(x + r step) =
+// fft_padi(x) + r step there: one address per butterfly (the reads for n >= 128 R, the writes of the
+// stages with ns >= 128) instead of one swizzle per element.
+template <typename T, bool INV, int R>
+__device__ inline void lds_stage(Cx<T>* buf, int P, int lnr, int L, int lns, const Cx<T>* __restrict__ tw) {
+  constexpr int NB = (LdsFft<T>::PER + R - 1) / R;  // butterflies per thread
+  const int nr = 1 << lnr, ns = 1 << lns;
+  const int total = L << lnr;
+  Cx<T> v[NB][R];
+  Cx<T> w1[NB];  // w_{ns R}^k, loaded with the inputs: its latency overlaps the barrier
+  auto read = [&](auto lin) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int t = (int)threadIdx.x + b * kLdsFftThreads;
+      if (t < total) {
+        const int l = t >> lnr, j = t & (nr - 1);
+        const Cx<T>* s = buf + l * P;
+        if constexpr (lin()) {
+          const Cx<T>* s0 = s + fft_padi(j);
+#pragma unroll
+          for (int r = 0; r < R; ++r) v[b][r] = s0[r * nr];
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) v[b][r] = s[fft_padi(j + r * nr)];
+        }
+        if (ns > 1) w1[b] = tw[ns + (j & (ns - 1))];  // consecutive k: coalesced
+      }
+    }
+  };
+  if ((nr & 127) == 0) read(std::true_type{});
+  else read(std::false_type{});
+  __syncthreads();  // every input of the stage is in registers: the outputs may overwrite them
+  auto write = [&](auto lin) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int t = (int)threadIdx.x + b * kLdsFftThreads;
+      if (t < total) {
+        const int l = t >> lnr, j = t & (nr - 1);
+        const int k = j & (ns - 1);
+        if (ns > 1) {  // w^r by successive products (error ~ r ulp)
+          Cx<T> w0 = w1[b];
+          if (INV) w0.im = -w0.im;
+          Cx<T> w = w0;
+#pragma unroll
+          for (int r = 1; r < R; ++r) {
+            v[b][r] = cmul(v[b][r], w);
+            if (r + 1 < R) w = cmul(w, w0);
+          }
+        }
+        dft_r<T, INV, R>(v[b]);
+        Cx<T>* d = buf + l * P;
+        const int id = ((j - k) * R) + k;  // (j div ns) ns R + k
+        if constexpr (lin()) {
+          Cx<T>* d0 = d + fft_padi(id);
+#pragma unroll
+          for (int r = 0; r < R; ++r) d0[r << lns] = v[b][r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) d[fft_padi(id + (r << lns))] = v[b][r];
+        }
+      }
+    }
+  };
+  if ((ns & 127) == 0) write(std::true_type{});
+  else write(std::false_type{});
+  __syncthreads();
+}
+
+// XCD-aware group order (speed only): XCD g = blockIdx % 8 takes a contiguous band of line groups, so
+// that the groups sharing the 128-B lines of a strided axis meet in one L2
+__device__ inline unsigned fft_group(unsigned bid, unsigned nb) {
+  const unsigned q8 = nb >> 3, r8 = nb & 7u, g8 = bid & 7u;
+  return g8 * q8 + (g8 < r8 ? g8 : r8) + (bid >> 3);
+}
+
+// Power-of-two lengths (radices 8, 4, 2); the 3 / 5 / 7 butterflies held across the stage barrier would
+// spill here (fp64 radix 7: 62 VGPRs), so lengths with an odd factor keep the ping-pong kernel.
+template <typename T, bool INV>
+__global__ void __launch_bounds__(kLdsFftThreads, 4) fft_lds_kernel(FftPlan p, const Cx<T>* __restrict__ src, Cx<T>* dst,
+                                                                 const Cx<T>* __restrict__ tw) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  Cx<T>* buf = reinterpret_cast<Cx<T>*>(smem_raw);
+  const int n = (int)p.n;
+  const int P = p.pitch;
+  const int64_t line0 = (int64_t)fft_group(blockIdx.x, gridDim.x) * p.lpb;
+  const int L = (int)((p.lines - line0) < p.lpb ? (p.lines - line0) : p.lpb);
+  const int tot = L * n;
+  const int lgn = 31 - __builtin_clz((unsigned)n);
+  const FastDiv dl((unsigned)L);
+  // load: contiguous axis position-fastest (each line one run), strided axis line-fastest (adjacent lines
+  // adjacent in memory at each position); a thread's PER loads are all issued before the first LDS store.
+  // Line-fastest with L dividing the thread count: the thread keeps one line, so its global base is
+  // computed once (line_base / tstore_offset divide 64-bit integers)
+  constexpr int PER = LdsFft<T>::PER;
+  const bool fixed_line = kLdsFftThreads % L == 0;
+  const int l_fix = (int)threadIdx.x % L, m_fix = (int)threadIdx.x / L, m_step = kLdsFftThreads / L;
+  auto coords = [&](int k, bool line_fast, int& l, int& m) {
+    const int e = (int)threadIdx.x + k * kLdsFftThreads;
+    if (line_fast) {
+      if (fixed_line) {
+        l = l_fix;
+        m = m_fix + k * m_step;
+      } else {
+        m = (int)dl.div((unsigned)e);
+        l = e - m * L;
+      }
+    } else {
+      l = e >> lgn;
+      m = e & (n - 1);
+    }
+  };
+  const bool lf_in = p.inner != 1;
+  const bool lf_out = p.tn1 > 0 || p.inner != 1;
+  // fixed line: element m at in_base + m * inner, out_base + m * out_step
+  const int64_t in_base = lf_in && fixed_line ? line_base(line0 + l_fix, p.n, p.inner) : 0;
+  const int64_t out_step = p.tn1 > 0 ? p.tn1 * p.inner : p.inner;
+  const int64_t out_base = lf_out && fixed_line ? (p.tn1 > 0 ? tstore_offset(line0 + l_fix, 0, p)
+                                                               : line_base(line0 + l_fix, p.n, p.inner))
+                                                : 0;
+  // global offset g and LDS slot sl of this thread's element k in the load (OUT false) or store order;
+  // MODE 0 position-fastest, 1 line-fastest with a fixed line, 2 line-fastest (a template constant, so
+  // that each load / store loop is free of branches and its values stay in registers)
+  auto place = [&](int k, auto out, auto mode, int64_t& g, int& sl) {
+    int l, m;
+    coords(k, mode() != 0, l, m);
+    sl = l * P + fft_padi(m);
+    if constexpr (mode() == 0) g = (line0 + l) * n + m;
+    else if constexpr (mode() == 1) g = out() ? out_base + (int64_t)m * out_step : in_base + (int64_t)m * p.inner;
+    else if (out() && p.tn1 > 0) g = tstore_offset(line0 + l, m, p);
+    else g = line_base(line0 + l, p.n, p.inner) + (int64_t)m * p.inner;
+  };
+  // full workgroups (tot == E) without the per-element bound
+  auto load_lines = [&](auto full, auto mode) {
+    T vr[PER], vi[PER];  // (a Cx<double> array here is left in scratch memory)
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (full() || (int)threadIdx.x + k * kLdsFftThreads < tot) {
+        int64_t g;
+        int sl;
+        place(k, std::false_type{}, mode, g, sl);
+        const Cx<T> a = src[g];
+        vr[k] = a.re;
+        vi[k] = a.im;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (full() || (int)threadIdx.x + k * kLdsFftThreads < tot) {
+        int64_t g;
+        int sl;
+        place(k, std::false_type{}, mode, g, sl);
+        buf[sl] = Cx<T>{vr[k], vi[k]};
+      }
+    }
+  };
+  auto store_lines = [&](auto full, auto mode) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (full() || (int)threadIdx.x + k * kLdsFftThreads < tot) {
+        int64_t g;
+        int sl;
+        place(k, std::true_type{}, mode, g, sl);
+        dst[g] = buf[sl];
+      }
+    }
+  };
+  using M0 = std::integral_constant<int, 0>;
+  using M1 = std::integral_constant<int, 1>;
+  using M2 = std::integral_constant<int, 2>;
+  auto dispatch = [&](bool lf, auto fn) {
+    const bool full = tot == LdsFft<T>::E;
+    if (!lf) full ? fn(std::true_type{}, M0{}) : fn(std::false_type{}, M0{});
+    else if (fixed_line) full ? fn(std::true_type{}, M1{}) : fn(std::false_type{}, M1{});
+    else full ? fn(std::true_type{}, M2{}) : fn(std::false_type{}, M2{});
+  };
+  if (!(kFftProbes && (p.probe & 32))) dispatch(lf_in, load_lines);
+  __syncthreads();
+  int lns = 0;
+  for (int s = 0; s < (kFftProbes && (p.probe & 16) ? 0 : p.nst); ++s) {
+    const int R = p.radix[s];
+    int lg = lgn;
+    asm volatile("" : "+s"(lg));  // per stage: keeps the stages' thread-invariant LDS addresses out of registers
+    if (R == 8) lds_stage<T, INV, 8>(buf, P, lg - 3, L, lns, tw);
+    else if (R == 4) lds_stage<T, INV, 4>(buf, P, lg - 2, L, lns, tw);
+    else lds_stage<T, INV, 2>(buf, P, lg - 1, L, lns, tw);
+    lns += R == 8 ? 3 : R == 4 ? 2 : 1;
+  }
+  if (kFftProbes && (p.probe & 64)) return;
+  // store: the transposed four-step store and strided axes line-fastest, the contiguous axis position-fastest
+  dispatch(lf_out, store_lines);
+}
+
+// Stage twiddle tables of a power-of-two plan: the stage of span ns and radix R reads w_{ns R}^k, k < ns,
+// at tw[ns + k] (the spans are distinct powers of two, so the ranges [ns, 2 ns) do not overlap; n entries
+// in all).  exp(-2 pi i k / (ns R)) in double, then rounded to T.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) fft_twiddle_table_kernel(FftPlan p, Cx<T>* __restrict__ tw) {
+  const int64_t n = p.n;
+  for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (int64_t)gridDim.x * blockDim.x) {
+    if (m == 0) {
+      tw[0] = Cx<T>{T(1), T(0)};
+      continue;
+    }
+    int64_t ns = 1;
+    int R = 2;
+    for (int s = 0; s < p.nst; ++s) {  // the stage whose range [ns, 2 ns) holds m
+      R = p.radix[s];
+      if (m < 2 * ns) break;
+      ns *= R;
+    }
+    const int64_t k = m - ns;
+    double sn = 0.0, c = 1.0;
+    if (k >= 0 && k < ns) sincospi(2.0 * (double)k / (double)(ns * R), &sn, &c);
+    tw[m] = Cx<T>{(T)c, (T)(-sn)};
+  }
+}
+
 // out[i] = a[i] * b[i % nb] (b conjugated if CONJ): spectrum product of an FFT convolution
 template <typename T, bool CONJ>
 __global__ void __launch_bounds__(kBlock) cmul_kernel(int64_t n, int64_t nb, const Cx<T>* __restrict__ a,
@@ -351,6 +639,65 @@ int launch_stockham(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream
   return last_launch_status();
 }
 
+// Twiddle table of length n (device memory, built once per (n, T) and kept for the process).
+template <typename T>
+const Cx<T>* twiddle_table(const FftPlan& p, hipStream_t st) {
+  static std::mutex mu;
+  static std::map<int64_t, Cx<T>*> tables;
+  const int64_t n = p.n;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = tables.find(n);
+  if (it != tables.end()) return it->second;
+  Cx<T>* tw = nullptr;
+  if (hipMalloc((void**)&tw, (size_t)n * sizeof(Cx<T>)) != hipSuccess) return nullptr;
+  hipLaunchKernelGGL(fft_twiddle_table_kernel<T>, dim3(grid_for(n)), dim3(kBlock), 0, st, p, tw);
+  if (hipStreamSynchronize(st) != hipSuccess) return nullptr;  // once per length: usable from any stream
+  tables[n] = tw;
+  return tw;
+}
+
+template <typename T>
+bool lds_fft_fits(int64_t n) {  // powers of two (see fft_lds_kernel)
+  return n >= 2 && n <= LdsFft<T>::E && (n & (n - 1)) == 0 && (size_t)fft_pitch((int)n, 1) * sizeof(Cx<T>) <= kFftLdsMax;
+}
+
+template <typename T>
+int launch_lds_fft(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_t st) {
+  if (!factor(p.n, p)) return PXA_ERR_UNSUPPORTED;
+  const Cx<T>* tw = twiddle_table<T>(p, st);
+  if (tw == nullptr) return launch_stockham<T>(p, inv, src, dst, st);  // no memory for the table
+  int L = (int)(LdsFft<T>::E / p.n);
+  if (L > p.lines) L = (int)p.lines;
+  if (p.inner > 1 && L > p.inner) L = (int)p.inner;
+  if (L < 1) L = 1;
+  while (L > 1 && (size_t)L * fft_pitch((int)p.n, L) * sizeof(Cx<T>) > kFftLdsMax) L /= 2;  // short lines: pitch pad
+  p.lpb = L;
+  p.pitch = fft_pitch((int)p.n, L);
+  p.probe = kFftProbes ? (tuning(PXA_TUNE_FFT_KERNEL) & 0x70) : 0;
+  const int64_t blocks = (p.lines + L - 1) / L;
+  PXA_CHECK_ARG(blocks <= 0x7fffffff);
+  const size_t smem = (size_t)L * p.pitch * sizeof(Cx<T>);
+  if (smem > kFftLdsMax) return PXA_ERR_UNSUPPORTED;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fft_lds_kernel<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFftLdsMax);
+    (void)hipFuncSetAttribute((const void*)fft_lds_kernel<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFftLdsMax);
+    attr = true;
+  }
+  auto kern = inv ? fft_lds_kernel<T, true> : fft_lds_kernel<T, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLdsFftThreads), smem, st, p, src, dst, tw);
+  return last_launch_status();
+}
+
+// the in-LDS transform of one axis: the in-place kernel (default) or the ping-pong kernel (A/B)
+template <typename T>
+int launch_lines(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_t st) {
+  if ((tuning(PXA_TUNE_FFT_KERNEL) & 15) == 0 && lds_fft_fits<T>(p.n)) return launch_lds_fft<T>(p, inv, src, dst, st);
+  return launch_stockham<T>(p, inv, src, dst, st);
+}
+
 template <typename T>
 int launch_direct(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_t st) {
   PXA_CHECK_ARG(p.lines <= 0x7fffffff);
@@ -442,7 +789,7 @@ int fft_axis(int64_t n, int64_t inner, int64_t lines, bool inv, const Cx<T>* src
   p.inner = inner;
   p.lines = lines;
   p.tn1 = 0;
-  if (stockham_fits<T>(n)) return launch_stockham<T>(p, inv, src, dst, st);
+  if (stockham_fits<T>(n)) return launch_lines<T>(p, inv, src, dst, st);
   if (!smooth(n) && direct_fits<T>(n)) return launch_direct<T>(p, inv, src, dst, st);
   if (axis_work<T>(n, lines) < 0) return PXA_ERR_UNSUPPORTED;
   if (work == nullptr) return PXA_ERR_ARG;
@@ -453,7 +800,7 @@ int fft_axis(int64_t n, int64_t inner, int64_t lines, bool inv, const Cx<T>* src
     p1.n = n1;
     p1.inner = n2 * inner;
     p1.lines = total / n1;
-    int e = launch_stockham<T>(p1, inv, src, dst, st);
+    int e = launch_lines<T>(p1, inv, src, dst, st);
     if (e) return e;
     if (inv)
       hipLaunchKernelGGL((four_step_twiddle_kernel<T, true>), dim3(grid_for(total)), dim3(kBlock), 0, st, total, n1,
@@ -468,7 +815,7 @@ int fft_axis(int64_t n, int64_t inner, int64_t lines, bool inv, const Cx<T>* src
     p2.inner = inner;
     p2.lines = total / n2;
     p2.tn1 = n1;
-    e = launch_stockham<T>(p2, inv, dst, work, st);
+    e = launch_lines<T>(p2, inv, dst, work, st);
     if (e) return e;
     return (int)hipMemcpyAsync(dst, work, (size_t)total * sizeof(Cx<T>), hipMemcpyDeviceToDevice, st);
   }

@@ -111,6 +111,28 @@ if [ "$S" = "timer" ]; then
     step drvn$i 120 $DRV --no-kernel-timer
   done
 fi
+if [ "$S" = "fft3" ]; then
+  step ffttests 600 $PT -m gpu tests/test_gpu_fft.py tests/test_gpu_stencil_fft.py
+  step ffttrace 120 rocprofv3 --kernel-trace --stats -d $P/fft_trace -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048
+  step ffttrace4 120 rocprofv3 --kernel-trace --stats -d $P/fft_trace4 -o run --output-format csv -- python3 scripts/fft_probe.py 4096x4096
+  step ffttrace3 120 rocprofv3 --kernel-trace --stats -d $P/fft_trace3 -o run --output-format csv -- python3 scripts/fft_probe.py 256x256x256
+fi
+if [ "$S" = "fft2" ]; then
+  step ffttests 600 $PT -m gpu tests/test_gpu_fft.py tests/test_gpu_stencil_fft.py
+  step ops 300 python3 scripts/bench_ops.py
+  step ffttrace 120 rocprofv3 --kernel-trace --stats -d $P/fft_trace -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048
+  step fftfetch 90 rocprofv3 --pmc FETCH_SIZE -d $P/fft_fetch -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+  step fftwrite 90 rocprofv3 --pmc WRITE_SIZE -d $P/fft_write -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+  step fftsq 90 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAVES -d $P/fft_sq -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+fi
+if [ "$S" = "fft4" ]; then
+  step ffttests 600 $PT -m gpu tests/test_gpu_fft.py tests/test_gpu_stencil_fft.py
+  PXA_LIB_PATH=build/libpyxu_amd_probe.so step fftmodes 200 rocprofv3 --kernel-trace -d $P/fft_modes -o run --output-format csv -- python3 scripts/fft_modes_probe.py 2048x2048
+  step fftfetch 90 rocprofv3 --pmc FETCH_SIZE -d $P/fft_fetch -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+  step fftwrite 90 rocprofv3 --pmc WRITE_SIZE -d $P/fft_write -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+  step fftsq 90 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAVES -d $P/fft_sq -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+  step fftsq2 90 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES -d $P/fft_sq2 -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
+fi
 if [ "$S" = "fft" ]; then
   step ops 300 python3 scripts/bench_ops.py
   step ffttrace 120 rocprofv3 --kernel-trace --stats -d $P/fft_trace -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048

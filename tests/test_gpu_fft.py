@@ -92,3 +92,30 @@ def test_fft_adjoint_identity_and_gram():
         AtAx = to_NUMPY(op.adjoint(op.apply(to_device(x))))
         assert rel_err(AtAx, N * x) <= 1e-12
         assert rel_err(to_NUMPY(op.pinv(to_device(Ax), damp=0.0)), x) <= 1e-12
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("sh,axes", [((2048, 2048), (0, 1)), ((3, 64, 512), (0, 1, 2)), ((16384,), (0,)),
+                                     ((2, 256, 8), (1,)), ((4096, 3), (0,))])
+def test_fft_kernels_agree(sh, axes, dt):
+    """The in-place LDS kernel (PXA_TUNE_FFT_KERNEL 0: padded lines, twiddle table, power-of-two lengths) and
+    the ping-pong Stockham kernel (1) against NumPy, contiguous and strided axes, and four-step lengths."""
+    from pyxu_amd import _dev
+
+    rng = np.random.default_rng(len(sh) * 7 + sh[-1])
+    N = int(np.prod(sh))
+    x = rng.standard_normal(sh) + 1j * rng.standard_normal(sh)
+    ref = np.fft.fftn(x, axes=axes)
+    view = lambda c: np.stack([c.real, c.imag], axis=-1).reshape(2 * N).astype(dt)  # noqa: E731
+    out = {}
+    old = _dev.tuning(_dev.TUNE_FFT_KERNEL, 0)
+    try:
+        for mode in (0, 1):
+            _dev.tuning(_dev.TUNE_FFT_KERNEL, mode)
+            with pxrt.Precision(pxrt.Width.SINGLE if dt == np.float32 else pxrt.Width.DOUBLE):
+                op = pxo.FFT(arg_shape=sh, axes=axes)
+                out[mode] = to_NUMPY(op.apply(to_device(view(x))))
+    finally:
+        _dev.tuning(_dev.TUNE_FFT_KERNEL, old)
+    for mode in (0, 1):
+        assert rel_err(out[mode], view(ref)) <= TOL[dt], mode
