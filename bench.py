@@ -924,6 +924,7 @@ def main():
         if kern_ms is not None:
             roof = roofline(N * stack, kern_ms, bpp, f"{n0}x{n1}", mode=mode)
             roof["launches_timed"] = launches
+            roof["kernel_timer"] = "in_region" if args.kernel_timer_in_region else "post_region"
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
             v1, it1, dt1 = cpu_baseline(n0, n1, seed=1234, budget_s=args.cpu_seconds, threads=1)

@@ -140,6 +140,9 @@ if [ "$S" = "fft" ]; then
   step fftwrite 90 rocprofv3 --pmc WRITE_SIZE -d $P/fft_write -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
   step fftsq 90 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAVES -d $P/fft_sq -o run --output-format csv -- python3 scripts/fft_probe.py 2048x2048 10
 fi
+if [ "$S" = "k4off" ]; then
+  step k4off 300 python3 scripts/k4_offset_probe.py
+fi
 if [ "$S" = "full" ]; then
   step pytest 1000 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
