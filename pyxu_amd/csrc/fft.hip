@@ -68,8 +68,48 @@ __device__ inline Cx<float> csub(Cx<float> a, Cx<float> b) {
 }
 template <>
 __device__ inline Cx<float> cmul(Cx<float> a, Cx<float> b) {
-  const PkF32 t = PkF32{a.re, a.re} * pk(b);
-  return unpk(__builtin_elementwise_fma(PkF32{a.im, a.im}, PkF32{-b.im, b.re}, t));
+  // (ar br, ar bi), then + (-ai bi, ai br): the lane selects and the negation ride in the VOP3P modifiers
+  // (written out: the compiler materialises the swapped operand with moves)
+  PkF32 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(pk(a)), "v"(pk(b)));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(pk(a)), "v"(pk(b)), "v"(t));
+  return unpk(r);
+}
+// a + (-i) d (forward) / a + i d (inverse), and a - (-i) d / a - i d, in one packed add each
+template <typename T, bool INV>
+__device__ inline Cx<T> add_mi(Cx<T> a, Cx<T> d) {
+  return cadd(a, mul_mi<T, INV>(d));
+}
+template <typename T, bool INV>
+__device__ inline Cx<T> sub_mi(Cx<T> a, Cx<T> d) {
+  return csub(a, mul_mi<T, INV>(d));
+}
+__device__ inline PkF32 pk_add_swap_neg_hi(PkF32 a, PkF32 d) {  // (a.re + d.im, a.im - d.re)
+  PkF32 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(d));
+  return r;
+}
+__device__ inline PkF32 pk_add_swap_neg_lo(PkF32 a, PkF32 d) {  // (a.re - d.im, a.im + d.re)
+  PkF32 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(d));
+  return r;
+}
+template <>
+__device__ inline Cx<float> add_mi<float, false>(Cx<float> a, Cx<float> d) {
+  return unpk(pk_add_swap_neg_hi(pk(a), pk(d)));
+}
+template <>
+__device__ inline Cx<float> add_mi<float, true>(Cx<float> a, Cx<float> d) {
+  return unpk(pk_add_swap_neg_lo(pk(a), pk(d)));
+}
+template <>
+__device__ inline Cx<float> sub_mi<float, false>(Cx<float> a, Cx<float> d) {
+  return unpk(pk_add_swap_neg_lo(pk(a), pk(d)));
+}
+template <>
+__device__ inline Cx<float> sub_mi<float, true>(Cx<float> a, Cx<float> d) {
+  return unpk(pk_add_swap_neg_hi(pk(a), pk(d)));
 }
 
 __device__ inline void sc_pi(float x, float* s, float* c) { sincospif(x, s, c); }
@@ -92,11 +132,11 @@ __device__ inline void dft2(Cx<T>* v) {
 template <typename T, bool INV>
 __device__ inline void dft4(Cx<T>* v) {
   const Cx<T> t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
-  const Cx<T> t2 = cadd(v[1], v[3]), t3 = mul_mi<T, INV>(csub(v[1], v[3]));
+  const Cx<T> t2 = cadd(v[1], v[3]), d3 = csub(v[1], v[3]);
   v[0] = cadd(t0, t2);
   v[2] = csub(t0, t2);
-  v[1] = cadd(t1, t3);
-  v[3] = csub(t1, t3);
+  v[1] = add_mi<T, INV>(t1, d3);
+  v[3] = sub_mi<T, INV>(t1, d3);
 }
 template <typename T, bool INV>
 __device__ inline void dft8(Cx<T>* v) {
@@ -107,12 +147,15 @@ __device__ inline void dft8(Cx<T>* v) {
   // W8^k o_k, W8 = e^{-+ i pi / 4}
   const Cx<T> w1 = INV ? Cx<T>{h, h} : Cx<T>{h, -h};
   const Cx<T> w3 = INV ? Cx<T>{-h, h} : Cx<T>{-h, -h};
-  Cx<T> p[4] = {o[0], cmul(o[1], w1), mul_mi<T, INV>(o[2]), cmul(o[3], w3)};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    v[k] = cadd(e[k], p[k]);
-    v[k + 4] = csub(e[k], p[k]);
-  }
+  const Cx<T> p1 = cmul(o[1], w1), p3 = cmul(o[3], w3);
+  v[0] = cadd(e[0], o[0]);
+  v[4] = csub(e[0], o[0]);
+  v[1] = cadd(e[1], p1);
+  v[5] = csub(e[1], p1);
+  v[2] = add_mi<T, INV>(e[2], o[2]);
+  v[6] = sub_mi<T, INV>(e[2], o[2]);
+  v[3] = cadd(e[3], p3);
+  v[7] = csub(e[3], p3);
 }
 // e^{-+2 pi i m / R} for the odd radices, as literal constants (no sincos per butterfly)
 template <typename T, bool INV, int R>
@@ -154,7 +197,7 @@ struct FftPlan {
   int64_t tn1;              // 0: results back in place of the line; > 0: four-step transposed store (below)
   int lpb;                  // lines per workgroup
   int pitch;                // fft_lds_kernel: LDS elements per line
-  int probe;                // fft_lds_kernel, probe build only: 16 skip stages, 32 skip loads, 64 skip stores
+  int probe;                // fft_lds_kernel, probe build only: 16 skip stages, 32 skip loads, 64 skip stores, 128 no twiddle loads
   int nst;
   int radix[kMaxStages];
 };
@@ -290,19 +333,19 @@ __global__ void __launch_bounds__(kFftThreads) fft_direct_kernel(FftPlan p, cons
 // The ping-pong kernel above keeps two copies of its lines (so only 2 lines of 2048 fp32 per workgroup:
 // 16-B pieces of each row on a strided axis, 3.1x the compulsory HBM bytes, profiles/r04t_fft_pmc.txt),
 // writes each Stockham stage with stride R (8-way LDS bank conflicts at R = 8: 6.7 M extra cycles against
-// 2.8 M active) and evaluates a sincospi per butterfly.  This one: one copy of kLdsFftBytes of lines per
-// workgroup (8 lines of 2048 fp32: 64-B pieces of each row, adjacent line groups on one XCD so that the
-// rest of each 128-B line is an L2 hit), every stage in place -- all threads read their butterflies'
+// 2.8 M active) and evaluates a sincospi per butterfly.  This one: one copy of 64 or 128 KB of lines per
+// workgroup (4 / 8 lines of 2048 fp32: 32- / 64-B pieces of each row on a strided axis, adjacent line groups
+// on one XCD so that the rest of each 128-B line is an L2 hit), every stage in place -- all threads read their butterflies'
 // inputs into registers, barrier, write the outputs -- on swizzled lines (fft_padi: no bank conflicts),
 // twiddles w_n^m read from a table built once per length in double precision (exact to the rounding of T).
 // Power-of-two lengths.
-constexpr int kLdsFftThreads = 512;
-constexpr size_t kLdsFftBytes = 64 * 1024;  // line data per workgroup (+ pitch padding): two workgroups per CU
 
-template <typename T>
+// TH threads per workgroup and TH * 128 bytes of line data: 512 threads / 64 KB (two workgroups per CU) or
+// 1024 / 128 KB (one; twice the lines per workgroup, for strided axes and lines up to 16384 fp32)
+template <typename T, int TH>
 struct LdsFft {
-  static constexpr int E = (int)(kLdsFftBytes / sizeof(Cx<T>));  // elements per workgroup: 16384 fp32, 8192 fp64
-  static constexpr int PER = E / kLdsFftThreads;                  // per thread and stage: 16 / 8
+  static constexpr int E = (int)(TH * 128 / sizeof(Cx<T>));  // elements per workgroup: 8192 / 16384 fp32
+  static constexpr int PER = E / TH;                          // per thread and stage: 16 fp32, 8 fp64
 };
 
 // Position m of a line at m ^ ((m >> 3) & 15) (a permutation within aligned blocks of 16), lines at a pitch
@@ -332,9 +375,10 @@ __device__ inline void dft_r(Cx<T>* v) {
 // shifts and masks.  A step that is a multiple of 128 leaves bits 0-6 alone, so fft_padi(x + r step) =
 // fft_padi(x) + r step there: one address per butterfly (the reads for n >= 128 R, the writes of the
 // stages with ns >= 128) instead of one swizzle per element.
-template <typename T, bool INV, int R>
-__device__ inline void lds_stage(Cx<T>* buf, int P, int lnr, int L, int lns, const Cx<T>* __restrict__ tw) {
-  constexpr int NB = (LdsFft<T>::PER + R - 1) / R;  // butterflies per thread
+template <typename T, bool INV, int R, int TH>
+__device__ inline void lds_stage(Cx<T>* buf, int P, int lnr, int L, int lns, const Cx<T>* __restrict__ tw,
+                                 bool probe_tw = false) {
+  constexpr int NB = (LdsFft<T, TH>::PER + R - 1) / R;  // butterflies per thread
   const int nr = 1 << lnr, ns = 1 << lns;
   const int total = L << lnr;
   Cx<T> v[NB][R];
@@ -342,7 +386,7 @@ __device__ inline void lds_stage(Cx<T>* buf, int P, int lnr, int L, int lns, con
   auto read = [&](auto lin) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const int t = (int)threadIdx.x + b * kLdsFftThreads;
+      const int t = (int)threadIdx.x + b * TH;
       if (t < total) {
         const int l = t >> lnr, j = t & (nr - 1);
         const Cx<T>* s = buf + l * P;
@@ -355,6 +399,7 @@ __device__ inline void lds_stage(Cx<T>* buf, int P, int lnr, int L, int lns, con
           for (int r = 0; r < R; ++r) v[b][r] = s[fft_padi(j + r * nr)];
         }
         if (ns > 1) w1[b] = tw[ns + (j & (ns - 1))];  // consecutive k: coalesced
+        if (kFftProbes && probe_tw) w1[b] = Cx<T>{T(1), T(0)};  // timing probe only (WRONG results)
       }
     }
   };
@@ -364,7 +409,7 @@ __device__ inline void lds_stage(Cx<T>* buf, int P, int lnr, int L, int lns, con
   auto write = [&](auto lin) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const int t = (int)threadIdx.x + b * kLdsFftThreads;
+      const int t = (int)threadIdx.x + b * TH;
       if (t < total) {
         const int l = t >> lnr, j = t & (nr - 1);
         const int k = j & (ns - 1);
@@ -397,6 +442,20 @@ __device__ inline void lds_stage(Cx<T>* buf, int P, int lnr, int L, int lns, con
   __syncthreads();
 }
 
+// One complex element by a raw buffer access (voffset per thread, soffset uniform: no 64-bit address math)
+typedef unsigned FftU2 __attribute__((ext_vector_type(2)));
+typedef unsigned FftU4 __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ inline Cx<T> cx_buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (sizeof(Cx<T>) == 8) return __builtin_bit_cast(Cx<T>, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  else return __builtin_bit_cast(Cx<T>, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+template <typename T>
+__device__ inline void cx_buf_st(Cx<T> v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (sizeof(Cx<T>) == 8) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(FftU2, v), r, voff, soff, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(FftU4, v), r, voff, soff, 0);
+}
+
 // XCD-aware group order (speed only): XCD g = blockIdx % 8 takes a contiguous band of line groups, so
 // that the groups sharing the 128-B lines of a strided axis meet in one L2
 __device__ inline unsigned fft_group(unsigned bid, unsigned nb) {
@@ -406,8 +465,8 @@ __device__ inline unsigned fft_group(unsigned bid, unsigned nb) {
 
 // Power-of-two lengths (radices 8, 4, 2); the 3 / 5 / 7 butterflies held across the stage barrier would
 // spill here (fp64 radix 7: 62 VGPRs), so lengths with an odd factor keep the ping-pong kernel.
-template <typename T, bool INV>
-__global__ void __launch_bounds__(kLdsFftThreads, 4) fft_lds_kernel(FftPlan p, const Cx<T>* __restrict__ src, Cx<T>* dst,
+template <typename T, bool INV, int TH>
+__global__ void __launch_bounds__(TH, 4) fft_lds_kernel(FftPlan p, const Cx<T>* __restrict__ src, Cx<T>* dst,
                                                                  const Cx<T>* __restrict__ tw) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   Cx<T>* buf = reinterpret_cast<Cx<T>*>(smem_raw);
@@ -422,11 +481,11 @@ __global__ void __launch_bounds__(kLdsFftThreads, 4) fft_lds_kernel(FftPlan p, c
   // adjacent in memory at each position); a thread's PER loads are all issued before the first LDS store.
   // Line-fastest with L dividing the thread count: the thread keeps one line, so its global base is
   // computed once (line_base / tstore_offset divide 64-bit integers)
-  constexpr int PER = LdsFft<T>::PER;
-  const bool fixed_line = kLdsFftThreads % L == 0;
-  const int l_fix = (int)threadIdx.x % L, m_fix = (int)threadIdx.x / L, m_step = kLdsFftThreads / L;
+  constexpr int PER = LdsFft<T, TH>::PER;
+  const bool fixed_line = TH % L == 0;
+  const int l_fix = (int)threadIdx.x % L, m_fix = (int)threadIdx.x / L, m_step = TH / L;
   auto coords = [&](int k, bool line_fast, int& l, int& m) {
-    const int e = (int)threadIdx.x + k * kLdsFftThreads;
+    const int e = (int)threadIdx.x + k * TH;
     if (line_fast) {
       if (fixed_line) {
         l = l_fix;
@@ -465,7 +524,7 @@ __global__ void __launch_bounds__(kLdsFftThreads, 4) fft_lds_kernel(FftPlan p, c
     T vr[PER], vi[PER];  // (a Cx<double> array here is left in scratch memory)
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      if (full() || (int)threadIdx.x + k * kLdsFftThreads < tot) {
+      if (full() || (int)threadIdx.x + k * TH < tot) {
         int64_t g;
         int sl;
         place(k, std::false_type{}, mode, g, sl);
@@ -476,7 +535,7 @@ __global__ void __launch_bounds__(kLdsFftThreads, 4) fft_lds_kernel(FftPlan p, c
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      if (full() || (int)threadIdx.x + k * kLdsFftThreads < tot) {
+      if (full() || (int)threadIdx.x + k * TH < tot) {
         int64_t g;
         int sl;
         place(k, std::false_type{}, mode, g, sl);
@@ -487,7 +546,7 @@ __global__ void __launch_bounds__(kLdsFftThreads, 4) fft_lds_kernel(FftPlan p, c
   auto store_lines = [&](auto full, auto mode) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      if (full() || (int)threadIdx.x + k * kLdsFftThreads < tot) {
+      if (full() || (int)threadIdx.x + k * TH < tot) {
         int64_t g;
         int sl;
         place(k, std::true_type{}, mode, g, sl);
@@ -498,27 +557,78 @@ __global__ void __launch_bounds__(kLdsFftThreads, 4) fft_lds_kernel(FftPlan p, c
   using M0 = std::integral_constant<int, 0>;
   using M1 = std::integral_constant<int, 1>;
   using M2 = std::integral_constant<int, 2>;
+  const bool full = tot == LdsFft<T, TH>::E;
   auto dispatch = [&](bool lf, auto fn) {
-    const bool full = tot == LdsFft<T>::E;
     if (!lf) full ? fn(std::true_type{}, M0{}) : fn(std::false_type{}, M0{});
     else if (fixed_line) full ? fn(std::true_type{}, M1{}) : fn(std::false_type{}, M1{});
     else full ? fn(std::true_type{}, M2{}) : fn(std::false_type{}, M2{});
   };
-  if (!(kFftProbes && (p.probe & 32))) dispatch(lf_in, load_lines);
+  // Fast path (full groups; the contiguous axis, or line-fastest with the group's lines in one inner block,
+  // the axis' span < 2 GB and no transposed store): element k of a thread at group base + voffset (per
+  // thread) + k * sstep (uniform), its LDS slot at slot0 + a uniform step -- the generic path spends ~11
+  // VALU per element on 64-bit offsets and swizzles
+  const bool span_ok = p.n * p.inner * (int64_t)sizeof(Cx<T>) < ((int64_t)1 << 31);
+  auto fast_ok = [&](bool lf, bool out) {
+    return full && (!lf || (!(out && p.tn1 > 0) && fixed_line && p.inner % L == 0 && span_ok));
+  };
+  auto fast_lines = [&](auto out, auto lf, auto lin) {
+    Cx<T>* gb;
+    int voff, slot0, sstep;
+    const int tid = (int)threadIdx.x;
+    if constexpr (!lf()) {
+      gb = (out() ? dst : const_cast<Cx<T>*>(src)) + line0 * n;
+      voff = tid * (int)sizeof(Cx<T>);
+      sstep = TH * (int)sizeof(Cx<T>);
+      slot0 = (tid >> lgn) * P + fft_padi(tid & (n - 1));
+    } else {
+      gb = (out() ? dst : const_cast<Cx<T>*>(src)) + line_base(line0, p.n, p.inner);
+      voff = (l_fix + m_fix * (int)p.inner) * (int)sizeof(Cx<T>);
+      sstep = m_step * (int)p.inner * (int)sizeof(Cx<T>);
+      slot0 = l_fix * P + fft_padi(m_fix);
+    }
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(gb, (short)0, 0x7FFFFFFF, 0x00020000);
+    auto slot = [&](int k) {
+      if constexpr (!lf()) return slot0 + ((k * TH) >> lgn) * P + ((k * TH) & (n - 1));
+      else if constexpr (lin()) return slot0 + k * m_step;  // m_step a multiple of 128: the swizzle is linear
+      else return l_fix * P + fft_padi(m_fix + k * m_step);
+    };
+    if constexpr (!out()) {
+      T vr[PER], vi[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const Cx<T> a = cx_buf_ld<T>(rs, voff, k * sstep);
+        vr[k] = a.re;
+        vi[k] = a.im;
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) buf[slot(k)] = Cx<T>{vr[k], vi[k]};
+    } else {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) cx_buf_st<T>(buf[slot(k)], rs, voff, k * sstep);
+    }
+  };
+  auto run_lines = [&](auto out, bool lf, auto generic) {
+    if (!fast_ok(lf, out())) dispatch(lf, generic);
+    else if (!lf) fast_lines(out, std::false_type{}, std::false_type{});
+    else if ((m_step & 127) == 0) fast_lines(out, std::true_type{}, std::true_type{});
+    else fast_lines(out, std::true_type{}, std::false_type{});
+  };
+  if (!(kFftProbes && (p.probe & 32))) run_lines(std::false_type{}, lf_in, load_lines);
   __syncthreads();
   int lns = 0;
   for (int s = 0; s < (kFftProbes && (p.probe & 16) ? 0 : p.nst); ++s) {
     const int R = p.radix[s];
     int lg = lgn;
     asm volatile("" : "+s"(lg));  // per stage: keeps the stages' thread-invariant LDS addresses out of registers
-    if (R == 8) lds_stage<T, INV, 8>(buf, P, lg - 3, L, lns, tw);
-    else if (R == 4) lds_stage<T, INV, 4>(buf, P, lg - 2, L, lns, tw);
-    else lds_stage<T, INV, 2>(buf, P, lg - 1, L, lns, tw);
+    const bool ptw = kFftProbes && (p.probe & 128);  // probe: no twiddle loads
+    if (R == 8) lds_stage<T, INV, 8, TH>(buf, P, lg - 3, L, lns, tw, ptw);
+    else if (R == 4) lds_stage<T, INV, 4, TH>(buf, P, lg - 2, L, lns, tw, ptw);
+    else lds_stage<T, INV, 2, TH>(buf, P, lg - 1, L, lns, tw, ptw);
     lns += R == 8 ? 3 : R == 4 ? 2 : 1;
   }
   if (kFftProbes && (p.probe & 64)) return;
   // store: the transposed four-step store and strided axes line-fastest, the contiguous axis position-fastest
-  dispatch(lf_out, store_lines);
+  run_lines(std::true_type{}, lf_out, store_lines);
 }
 
 // Stage twiddle tables of a power-of-two plan: the stage of span ns and radix R reads w_{ns R}^k, k < ns,
@@ -658,7 +768,47 @@ const Cx<T>* twiddle_table(const FftPlan& p, hipStream_t st) {
 
 template <typename T>
 bool lds_fft_fits(int64_t n) {  // powers of two (see fft_lds_kernel)
-  return n >= 2 && n <= LdsFft<T>::E && (n & (n - 1)) == 0 && (size_t)fft_pitch((int)n, 1) * sizeof(Cx<T>) <= kFftLdsMax;
+  return n >= 2 && n <= LdsFft<T, 1024>::E && (n & (n - 1)) == 0 &&
+         (size_t)fft_pitch((int)n, 1) * sizeof(Cx<T>) <= kFftLdsMax;
+}
+
+// Workgroup size: 1024 threads / 128 KB for lines longer than 64 KB, and on strided axes whose 512-thread
+// group would hold only 1 or 2 lines (8- or 16-B row pieces: 4096^2 fp32 axis 0 170 -> 122 us); 512 / 64 KB
+// otherwise (2048^2 axis 0: equal, 23.0 vs 23.3 us; 256^3 axes 0 / 1: 82 / 74 us against 96 / 80 with 1024,
+// profiles/r04zf_fft_th.txt).  PXA_TUNE_FFT_KERNEL bit 256 forces 512, bit 512 forces 1024 (A/B).
+template <typename T>
+int lds_fft_threads(const FftPlan& p) {
+  const int64_t t = tuning(PXA_TUNE_FFT_KERNEL);
+  if (p.n > LdsFft<T, 512>::E || (t & 512)) return 1024;
+  if (t & 256) return 512;
+  return p.inner > 1 && 2 * p.n >= LdsFft<T, 512>::E ? 1024 : 512;
+}
+
+template <typename T, int TH>
+int launch_lds_fft_th(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, const Cx<T>* tw, hipStream_t st) {
+  int L = (int)(LdsFft<T, TH>::E / p.n);
+  if (L > p.lines) L = (int)p.lines;
+  if (p.inner > 1 && L > p.inner) L = (int)p.inner;
+  if (L < 1) L = 1;
+  while (L > 1 && (size_t)L * fft_pitch((int)p.n, L) * sizeof(Cx<T>) > kFftLdsMax) L /= 2;  // short lines: pitch pad
+  p.lpb = L;
+  p.pitch = fft_pitch((int)p.n, L);
+  p.probe = kFftProbes ? (tuning(PXA_TUNE_FFT_KERNEL) & 0xF0) : 0;
+  const int64_t blocks = (p.lines + L - 1) / L;
+  PXA_CHECK_ARG(blocks <= 0x7fffffff);
+  const size_t smem = (size_t)L * p.pitch * sizeof(Cx<T>);
+  if (smem > kFftLdsMax) return PXA_ERR_UNSUPPORTED;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fft_lds_kernel<T, false, TH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFftLdsMax);
+    (void)hipFuncSetAttribute((const void*)fft_lds_kernel<T, true, TH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFftLdsMax);
+    attr = true;
+  }
+  auto kern = inv ? fft_lds_kernel<T, true, TH> : fft_lds_kernel<T, false, TH>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(TH), smem, st, p, src, dst, tw);
+  return last_launch_status();
 }
 
 template <typename T>
@@ -666,29 +816,8 @@ int launch_lds_fft(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_
   if (!factor(p.n, p)) return PXA_ERR_UNSUPPORTED;
   const Cx<T>* tw = twiddle_table<T>(p, st);
   if (tw == nullptr) return launch_stockham<T>(p, inv, src, dst, st);  // no memory for the table
-  int L = (int)(LdsFft<T>::E / p.n);
-  if (L > p.lines) L = (int)p.lines;
-  if (p.inner > 1 && L > p.inner) L = (int)p.inner;
-  if (L < 1) L = 1;
-  while (L > 1 && (size_t)L * fft_pitch((int)p.n, L) * sizeof(Cx<T>) > kFftLdsMax) L /= 2;  // short lines: pitch pad
-  p.lpb = L;
-  p.pitch = fft_pitch((int)p.n, L);
-  p.probe = kFftProbes ? (tuning(PXA_TUNE_FFT_KERNEL) & 0x70) : 0;
-  const int64_t blocks = (p.lines + L - 1) / L;
-  PXA_CHECK_ARG(blocks <= 0x7fffffff);
-  const size_t smem = (size_t)L * p.pitch * sizeof(Cx<T>);
-  if (smem > kFftLdsMax) return PXA_ERR_UNSUPPORTED;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fft_lds_kernel<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kFftLdsMax);
-    (void)hipFuncSetAttribute((const void*)fft_lds_kernel<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kFftLdsMax);
-    attr = true;
-  }
-  auto kern = inv ? fft_lds_kernel<T, true> : fft_lds_kernel<T, false>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLdsFftThreads), smem, st, p, src, dst, tw);
-  return last_launch_status();
+  return lds_fft_threads<T>(p) == 1024 ? launch_lds_fft_th<T, 1024>(p, inv, src, dst, tw, st)
+                                       : launch_lds_fft_th<T, 512>(p, inv, src, dst, tw, st);
 }
 
 // the in-LDS transform of one axis: the in-place kernel (default) or the ping-pong kernel (A/B)
@@ -790,6 +919,9 @@ int fft_axis(int64_t n, int64_t inner, int64_t lines, bool inv, const Cx<T>* src
   p.lines = lines;
   p.tn1 = 0;
   if (stockham_fits<T>(n)) return launch_lines<T>(p, inv, src, dst, st);
+  // power-of-two lines up to 128 KB: one in-LDS pass instead of the four-step's three (its workspace, sized
+  // by axis_work regardless of the tuning knob, is then unused)
+  if ((tuning(PXA_TUNE_FFT_KERNEL) & 15) == 0 && lds_fft_fits<T>(n)) return launch_lines<T>(p, inv, src, dst, st);
   if (!smooth(n) && direct_fits<T>(n)) return launch_direct<T>(p, inv, src, dst, st);
   if (axis_work<T>(n, lines) < 0) return PXA_ERR_UNSUPPORTED;
   if (work == nullptr) return PXA_ERR_ARG;

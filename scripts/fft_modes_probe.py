@@ -1,6 +1,6 @@
 """Probe build only (PXA_LIB_PATH=build/libpyxu_amd_probe.so): FFT.apply 2048x2048 with parts of the in-LDS
-kernel skipped (PXA_TUNE_FFT_KERNEL bits 16 stages, 32 global loads, 64 global stores: WRONG results, timing
-only), HIP events over 20 launches after 3 warm-ups."""
+kernel skipped (PXA_TUNE_FFT_KERNEL bits 16 stages, 32 global loads, 64 global stores, 128 twiddle loads:
+WRONG results, timing only), HIP events over 20 launches after 3 warm-ups."""
 import os
 import sys
 
@@ -19,7 +19,7 @@ for spec in sys.argv[1:] or ["2048x2048"]:
     with pxrt.Precision(pxrt.Width.SINGLE):
         op = pxo.FFT(arg_shape=sh)
         x = torch.randn(2 * N, device="cuda", dtype=torch.float32)
-        for mode in (0, 16, 32, 64, 48, 80, 96, 112, 1):
+        for mode in (0, 16, 32, 64, 48, 80, 96, 112, 128, 224, 256, 512, 1):
             _dev.tuning(_dev.TUNE_FFT_KERNEL, mode)
             for _ in range(3):
                 op.apply(x)

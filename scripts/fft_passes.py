@@ -24,7 +24,7 @@ def launches(d):
 args = sys.argv[1:]
 if args and args[0] == "--chunks":
     k, d = int(args[1]), args[2]
-    rows = launches(d)
+    rows = [r for r in launches(d) if "twiddle" not in r[2]]
     per = int(args[3]) if len(args) > 3 else 2  # launches per apply
     for c in range(len(rows) // k):
         ch = rows[c * k:(c + 1) * k]

@@ -99,7 +99,8 @@ def test_fft_adjoint_identity_and_gram():
                                      ((2, 256, 8), (1,)), ((4096, 3), (0,))])
 def test_fft_kernels_agree(sh, axes, dt):
     """The in-place LDS kernel (PXA_TUNE_FFT_KERNEL 0: padded lines, twiddle table, power-of-two lengths) and
-    the ping-pong Stockham kernel (1) against NumPy, contiguous and strided axes, and four-step lengths."""
+    the ping-pong Stockham kernel (1) against NumPy, contiguous and strided axes, and four-step lengths; the LDS
+    kernel's 512- and 1024-thread workgroups (bits 256 / 512 force one) agree to the last bit."""
     from pyxu_amd import _dev
 
     rng = np.random.default_rng(len(sh) * 7 + sh[-1])
@@ -110,7 +111,7 @@ def test_fft_kernels_agree(sh, axes, dt):
     out = {}
     old = _dev.tuning(_dev.TUNE_FFT_KERNEL, 0)
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 256, 512):
             _dev.tuning(_dev.TUNE_FFT_KERNEL, mode)
             with pxrt.Precision(pxrt.Width.SINGLE if dt == np.float32 else pxrt.Width.DOUBLE):
                 op = pxo.FFT(arg_shape=sh, axes=axes)
@@ -119,3 +120,5 @@ def test_fft_kernels_agree(sh, axes, dt):
         _dev.tuning(_dev.TUNE_FFT_KERNEL, old)
     for mode in (0, 1):
         assert rel_err(out[mode], view(ref)) <= TOL[dt], mode
+    assert np.array_equal(out[256], out[512])  # same stages, same arithmetic: only the line grouping differs
+    assert rel_err(out[0], view(ref)) <= TOL[dt]
