@@ -157,6 +157,37 @@ __device__ inline void dft8(Cx<T>* v) {
   v[3] = cadd(e[3], p3);
   v[7] = csub(e[3], p3);
 }
+// 16-point DFT as 4 x 4: DFTs of the stride-4 subsequences, twiddles W16^(n1 k2), DFTs across (fp32 LDS stages)
+template <typename T, bool INV>
+__device__ inline void dft16(Cx<T>* v) {
+  Cx<T> a[4][4];
+#pragma unroll
+  for (int n1 = 0; n1 < 4; ++n1) {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) a[n1][n2] = v[4 * n2 + n1];
+    dft4<T, INV>(a[n1]);  // a[n1][k2] = sum_n2 x[4 n2 + n1] W4^(n2 k2)
+  }
+  const T c = T(0.92387953251128675613), sn = T(0.38268343236508977173), h = T(0.70710678118654752440);
+  const T sg = INV ? T(1) : T(-1);
+  // W16^m for m = n1 k2 in {1, 2, 3, 4, 6, 9}
+  const Cx<T> w1{c, sg * sn}, w2{h, sg * h}, w3{sn, sg * c}, w6{-h, sg * h}, w9{-c, sg * -sn};
+  a[1][1] = cmul(a[1][1], w1);
+  a[1][2] = cmul(a[1][2], w2);
+  a[1][3] = cmul(a[1][3], w3);
+  a[2][1] = cmul(a[2][1], w2);
+  a[2][2] = mul_mi<T, INV>(a[2][2]);
+  a[2][3] = cmul(a[2][3], w6);
+  a[3][1] = cmul(a[3][1], w3);
+  a[3][2] = cmul(a[3][2], w6);
+  a[3][3] = cmul(a[3][3], w9);
+#pragma unroll
+  for (int k2 = 0; k2 < 4; ++k2) {
+    Cx<T> b[4] = {a[0][k2], a[1][k2], a[2][k2], a[3][k2]};
+    dft4<T, INV>(b);  // X[k2 + 4 k1] = sum_n1 a[n1][k2] W4^(n1 k1)
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) v[k2 + 4 * k1] = b[k1];
+  }
+}
 // e^{-+2 pi i m / R} for the odd radices, as literal constants (no sincos per butterfly)
 template <typename T, bool INV, int R>
 __device__ inline Cx<T> root(int m) {
@@ -366,6 +397,7 @@ __device__ inline void dft_r(Cx<T>* v) {
   if constexpr (R == 2) dft2<T, INV>(v);
   else if constexpr (R == 4) dft4<T, INV>(v);
   else if constexpr (R == 8) dft8<T, INV>(v);
+  else if constexpr (R == 16) dft16<T, INV>(v);
   else dft_odd<T, INV, R>(v);
 }
 
@@ -413,15 +445,14 @@ __device__ inline void lds_stage(Cx<T>* buf, int P, int lnr, int L, int lns, con
       if (t < total) {
         const int l = t >> lnr, j = t & (nr - 1);
         const int k = j & (ns - 1);
-        if (ns > 1) {  // w^r by successive products (error ~ r ulp)
-          Cx<T> w0 = w1[b];
-          if (INV) w0.im = -w0.im;
-          Cx<T> w = w0;
+        if (ns > 1) {  // w^r: w^(2q) = (w^q)^2, w^(2q+1) = w^(2q) w -- a product chain of depth ~2 log2 r
+          Cx<T> wp[R];
+          wp[1] = w1[b];
+          if (INV) wp[1].im = -wp[1].im;
 #pragma unroll
-          for (int r = 1; r < R; ++r) {
-            v[b][r] = cmul(v[b][r], w);
-            if (r + 1 < R) w = cmul(w, w0);
-          }
+          for (int r = 2; r < R; ++r) wp[r] = (r & 1) ? cmul(wp[r - 1], wp[1]) : cmul(wp[r / 2], wp[r / 2]);
+#pragma unroll
+          for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], wp[r]);
         }
         dft_r<T, INV, R>(v[b]);
         Cx<T>* d = buf + l * P;
@@ -621,10 +652,12 @@ __global__ void __launch_bounds__(TH, 4) fft_lds_kernel(FftPlan p, const Cx<T>* 
     int lg = lgn;
     asm volatile("" : "+s"(lg));  // per stage: keeps the stages' thread-invariant LDS addresses out of registers
     const bool ptw = kFftProbes && (p.probe & 128);  // probe: no twiddle loads
-    if (R == 8) lds_stage<T, INV, 8, TH>(buf, P, lg - 3, L, lns, tw, ptw);
+    if (R == 16) {
+      if constexpr (sizeof(T) == 4) lds_stage<T, INV, 16, TH>(buf, P, lg - 4, L, lns, tw, ptw);
+    } else if (R == 8) lds_stage<T, INV, 8, TH>(buf, P, lg - 3, L, lns, tw, ptw);
     else if (R == 4) lds_stage<T, INV, 4, TH>(buf, P, lg - 2, L, lns, tw, ptw);
     else lds_stage<T, INV, 2, TH>(buf, P, lg - 1, L, lns, tw, ptw);
-    lns += R == 8 ? 3 : R == 4 ? 2 : 1;
+    lns += R == 16 ? 4 : R == 8 ? 3 : R == 4 ? 2 : 1;
   }
   if (kFftProbes && (p.probe & 64)) return;
   // store: the transposed four-step store and strided axes line-fastest, the contiguous axis position-fastest
@@ -671,6 +704,21 @@ __global__ void __launch_bounds__(kBlock) cmul_kernel(int64_t n, int64_t nb, con
 bool factor(int64_t n, FftPlan& p) {
   p.nst = 0;
   for (int r : {8, 4, 2, 3, 5, 7}) {
+    while (n % r == 0) {
+      if (p.nst == kMaxStages) return false;
+      p.radix[p.nst++] = r;
+      n /= r;
+    }
+  }
+  return n == 1;
+}
+
+// Radices of the in-LDS kernel (powers of two): 16 first for fp32 (16 values per thread: one radix-16
+// butterfly, three LDS round trips instead of four at 2048), 8 for fp64 (8 per thread); then 8 / 4 / 2
+template <typename T>
+bool factor_lds(int64_t n, FftPlan& p) {
+  p.nst = 0;
+  for (int r : {sizeof(T) == 4 ? 16 : 8, 8, 4, 2}) {
     while (n % r == 0) {
       if (p.nst == kMaxStages) return false;
       p.radix[p.nst++] = r;
@@ -813,7 +861,7 @@ int launch_lds_fft_th(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, const C
 
 template <typename T>
 int launch_lds_fft(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_t st) {
-  if (!factor(p.n, p)) return PXA_ERR_UNSUPPORTED;
+  if (!factor_lds<T>(p.n, p)) return PXA_ERR_UNSUPPORTED;
   const Cx<T>* tw = twiddle_table<T>(p, st);
   if (tw == nullptr) return launch_stockham<T>(p, inv, src, dst, st);  // no memory for the table
   return lds_fft_threads<T>(p) == 1024 ? launch_lds_fft_th<T, 1024>(p, inv, src, dst, tw, st)
