@@ -60,8 +60,8 @@ extern "C" {
                                axis-0 march into segments (0: 2048) */
 #define PXA_TUNE_PGD_DIAG 3 /* fused PGD tile kernel, PROBE BUILD ONLY (make -C pyxu_amd/csrc probe; the production
                               library ignores it): bit 5 s_memtime phase trace (pxa_pgd_tile_trace); timing probes
-                              with WRONG results: bit 6 skips passes A / B, bit 7 the window loads, bit 8 loads x only
-                              (scripts/pgd_modes_probe.py diag) */
+                              with WRONG results: bit 6 skips passes A / B, bit 7 the window loads, bit 8 loads x only,
+                              bit 9 the H^T y loads, bit 10 the x_new stores (scripts/pgd_modes_probe.py diag) */
 #define PXA_TUNE_PGD_STAGGER 6 /* fused PGD tile kernel A/B probe, PROBE BUILD ONLY: v = (sel << 8) | n delays the
                                   workgroups picked by `sel` in the first dispatch round by n x 1024 cycles */
 #define PXA_TUNE_PDS_EVENTS 5 /* measurement hook: > 0 makes pxa_pds_step record HIP events around each

@@ -143,6 +143,10 @@ fi
 if [ "$S" = "k4off" ]; then
   step k4off 300 python3 scripts/k4_offset_probe.py
 fi
+if [ "$S" = "pgdd" ]; then
+  export PXA_LIB_PATH=build/libpyxu_amd_probe.so
+  step modes 300 python3 scripts/pgd_modes_probe.py diag 2048 4096
+fi
 if [ "$S" = "full" ]; then
   step pytest 1000 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"

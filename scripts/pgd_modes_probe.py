@@ -1,6 +1,6 @@
 """Timing probe of the fused PGD launch (pxa_pgd_tv2d_step), fp32, Gaussian sigma=2 (R = 6), TV, PositiveOrthant,
 at n x n images (`stack` images of n x n with per-image data when given as n:stack): the tile kernel as it is and
-with parts of its work skipped (PXA_TUNE_PGD_DIAG bits 6-8: WRONG results, timing only), which prices the
+with parts of its work skipped (PXA_TUNE_PGD_DIAG bits 6-10: WRONG results, timing only), which prices the
 window loads, the passes and the rest.  Each configuration is timed as windows of back-to-back launches between
 two HIP events (the bench's LaunchTimer convention), interleaved over 5 rounds; prints the median per launch.
 usage: python scripts/pgd_modes_probe.py diag [n[:stack] ...] | stagger | one <diag>   (probe build:
@@ -48,7 +48,7 @@ def diag_probe(sizes):
         n, stack = (int(v) for v in (spec.split(":") + ["1"])[:2])
         a, pre = setup(n, stack)
         nl = max(5, int(2e6 / (n * n * stack) * 50) if n * n * stack < 2e7 else 10)
-        res = {d: [] for d in (0, 64, 128, 192, 256, 320)}
+        res = {d: [] for d in (0, 64, 128, 192, 256, 320, 512, 1024, 1536)}
         for d in res:
             window(a, pre, 1, 3, d)
         for _ in range(5):
@@ -56,7 +56,8 @@ def diag_probe(sizes):
                 res[d].append(window(a, pre, 1, nl, d))
         for d, v in res.items():
             lab = {0: "full", 64: "no passes", 128: "no window loads", 192: "neither", 256: "x window only",
-                   320: "x window, no passes"}[d]
+                   320: "x window, no passes", 512: "no H^T y loads", 1024: "no x_new stores",
+                   1536: "no H^T y, no x_new"}[d]
             print(f"n={n} stack={stack} tile kernel {lab:16s} {np.median(v):9.2f} us", flush=True)
         del a
 
