@@ -70,8 +70,12 @@ extern "C" {
                                 (default one) */
 #define PXA_TUNE_FFT_KERNEL 8 /* A/B of the in-LDS FFT (pxa_fft, lines that fit one workgroup): 0 in-place register-staged
                                  stages on padded lines with a twiddle table, 1 the ping-pong Stockham kernel of rounds
-                                 1-3 (results equal up to rounding) */
-#define PXA_TUNE_COUNT 9
+                                 1-3 (results equal up to rounding); bits 256 / 512 force 512- / 1024-thread
+                                 workgroups of the in-place kernel */
+#define PXA_TUNE_GRAD_KERNEL 9 /* A/B of pxa_gradient2 / pxa_gradient2_adjoint: 0 the axis-0 march (each input plane
+                                  loaded once, XCD-banded in-plane blocks), 1 the row kernel of rounds 1-3 (same
+                                  bits) */
+#define PXA_TUNE_COUNT 10
 
 /* Row reductions (pxa_row_reduce). */
 #define PXA_RED_SUMSQ 0  /* sum x^2            : SquaredL2Norm.apply, norm(ord=2)^2   (norm.py:91-94) */

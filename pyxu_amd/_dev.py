@@ -215,6 +215,7 @@ TUNE_PGD_STAGGER = 6  # PXA_TUNE_PGD_STAGGER: (sel << 8) | n, delayed first-roun
 TUNE_PDS_EVENTS = 5  # PXA_TUNE_PDS_EVENTS: per-kernel HIP events inside pxa_pds_step (pds_kernel_ms)
 TUNE_PDS_MARCH = 7  # PXA_TUNE_PDS_MARCH: kernel D A/B (bit 0: two positions per thread)
 TUNE_FFT_KERNEL = 8  # PXA_TUNE_FFT_KERNEL: 0 in-place register-staged FFT kernel, 1 the ping-pong Stockham kernel
+TUNE_GRAD_KERNEL = 9  # PXA_TUNE_GRAD_KERNEL: 0 axis-0 march gradient kernels, 1 the row kernels (same bits)
 
 
 def tuning(key, value=-1):

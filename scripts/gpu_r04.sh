@@ -147,6 +147,16 @@ if [ "$S" = "pgdd" ]; then
   export PXA_LIB_PATH=build/libpyxu_amd_probe.so
   step modes 300 python3 scripts/pgd_modes_probe.py diag 2048 4096
 fi
+if [ "$S" = "ops" ]; then
+  step ops 300 python3 scripts/bench_ops.py
+fi
+if [ "$S" = "grad" ]; then
+  step gradtests 300 $PT -m gpu tests/test_gpu_gradient_kernels.py
+  step gradab 300 python3 scripts/grad_ab.py
+  step gradtrace 120 rocprofv3 --kernel-trace --stats -d $P/grad_trace -o run --output-format csv -- python3 scripts/grad_probe.py 1024x1024x1024
+  step gradfetch 120 rocprofv3 --pmc FETCH_SIZE -d $P/grad_fetch -o run --output-format csv -- python3 scripts/grad_probe.py 1024x1024x1024 3
+  step gradwrite 120 rocprofv3 --pmc WRITE_SIZE -d $P/grad_write -o run --output-format csv -- python3 scripts/grad_probe.py 1024x1024x1024 3
+fi
 if [ "$S" = "full" ]; then
   step pytest 1000 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
