@@ -75,7 +75,9 @@ extern "C" {
 #define PXA_TUNE_GRAD_KERNEL 9 /* A/B of pxa_gradient2 / pxa_gradient2_adjoint: 0 the axis-0 march (each input plane
                                   loaded once, XCD-banded in-plane blocks), 1 the row kernel of rounds 1-3 (same
                                   bits) */
-#define PXA_TUNE_COUNT 10
+#define PXA_TUNE_STENCIL_ND 10 /* A/B of pxa_stencil_nd_box: 0 the LDS-tiled kernel where it applies, 1 always the
+                                   generic one-thread-per-output kernel (same sums) */
+#define PXA_TUNE_COUNT 11
 
 /* Row reductions (pxa_row_reduce). */
 #define PXA_RED_SUMSQ 0  /* sum x^2            : SquaredL2Norm.apply, norm(ord=2)^2   (norm.py:91-94) */
@@ -260,6 +262,15 @@ int pxa_stencil_sep(int dtype, int64_t stack, int ndim, const int64_t* shape, co
 int pxa_stencil_nd(int dtype, int64_t stack, int ndim, const int64_t* shape, int ntaps, const int32_t* offsets_dev,
                    const void* coefs_dev, int zero_partial, const void* x, int64_t x_stack_stride, void* y,
                    int64_t y_stack_stride, double beta, void* stream);
+
+/* pxa_stencil_nd with the tap offsets' range per axis given on the host (off_lo[a] <= every offset along axis a
+ * <= off_hi[a]): 2-D / 3-D stencils whose reach fits run LDS-tiled (the input box staged once per 16 x 64 output
+ * tile, four outputs per thread), same sums as pxa_stencil_nd (taps in list order, one fma each); others fall
+ * back to it.  Replaces the same reference call as pxa_stencil_nd (stencil.py:441-461, _stencil.py codegen). */
+int pxa_stencil_nd_box(int dtype, int64_t stack, int ndim, const int64_t* shape, int ntaps, const int32_t* offsets_dev,
+                       const void* coefs_dev, const int32_t* off_lo, const int32_t* off_hi, int zero_partial,
+                       const void* x, int64_t x_stack_stride, void* y, int64_t y_stack_stride, double beta,
+                       void* stream);
 
 /* Pad.apply (pad.py:235-306): y (stack, shape + lo + hi) from x (stack, shape); modes per axis. */
 int pxa_pad(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* pad_lo, const int64_t* pad_hi,

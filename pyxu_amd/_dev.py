@@ -216,6 +216,7 @@ TUNE_PDS_EVENTS = 5  # PXA_TUNE_PDS_EVENTS: per-kernel HIP events inside pxa_pds
 TUNE_PDS_MARCH = 7  # PXA_TUNE_PDS_MARCH: kernel D A/B (bit 0: two positions per thread)
 TUNE_FFT_KERNEL = 8  # PXA_TUNE_FFT_KERNEL: 0 in-place register-staged FFT kernel, 1 the ping-pong Stockham kernel
 TUNE_GRAD_KERNEL = 9  # PXA_TUNE_GRAD_KERNEL: 0 axis-0 march gradient kernels, 1 the row kernels (same bits)
+TUNE_STENCIL_ND = 10  # PXA_TUNE_STENCIL_ND: 0 LDS-tiled N-D stencil where it applies, 1 the generic kernel (same sums)
 
 
 def tuning(key, value=-1):
@@ -740,10 +741,24 @@ def stencil_sep(x, y, stack, shape, taps, beta=0.0, xs=None, ys=None, x_off=0, y
     return y
 
 
-def stencil_nd(x, y, stack, shape, offsets_dev, coefs_dev, zero_partial=False, beta=0.0, xs=None, ys=None, x_off=0, y_off=0):
+def stencil_nd(x, y, stack, shape, offsets_dev, coefs_dev, zero_partial=False, beta=0.0, xs=None, ys=None, x_off=0, y_off=0,
+               off_lo=None, off_hi=None):
+    """N-D stencil; with the tap offsets' per-axis range (off_lo / off_hi, host ints) pxa_stencil_nd_box, which
+    runs the LDS-tiled kernel where it applies."""
     N = int(np.prod(shape))
     ntaps = coefs_dev.numel()
     es = x.element_size()
+    if off_lo is not None and off_hi is not None:
+        lo, hi = (np.ascontiguousarray(v, dtype=np.int32) for v in (off_lo, off_hi))
+        check(
+            lib.pxa_stencil_nd_box(
+                dtcode(x), stack, len(shape), i64_array(shape), ntaps, ptr(offsets_dev), ptr(coefs_dev),
+                lo.ctypes.data, hi.ctypes.data, int(zero_partial), ptr(x) + x_off * es, N if xs is None else xs,
+                ptr(y) + y_off * es, N if ys is None else ys, float(beta), stream(),
+            ),
+            "pxa_stencil_nd_box",
+        )
+        return y
     check(
         lib.pxa_stencil_nd(
             dtcode(x), stack, len(shape), i64_array(shape), ntaps, ptr(offsets_dev), ptr(coefs_dev), int(zero_partial),

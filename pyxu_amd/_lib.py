@@ -57,6 +57,7 @@ EXPORTS = {
     "pxa_stencil_sep_workspace_bytes": (sz, [i32, i64, i32, P_i64, P_int]),
     "pxa_stencil_sep": (i32, [i32, i64, i32, P_i64, P_int, P_i32, P_f64, vp, i64, vp, i64, f64, vp, vp]),
     "pxa_stencil_nd": (i32, [i32, i64, i32, P_i64, i32, vp, vp, i32, vp, i64, vp, i64, f64, vp]),
+    "pxa_stencil_nd_box": (i32, [i32, i64, i32, P_i64, i32, vp, vp, vp, vp, i32, vp, i64, vp, i64, f64, vp]),
     "pxa_pad": (i32, [i32, i64, i32, P_i64, P_i64, P_i64, P_int, vp, vp, vp]),
     "pxa_pad_adjoint": (i32, [i32, i64, i32, P_i64, P_i64, P_i64, P_int, vp, vp, vp, vp]),
     "pxa_trim": (i32, [i32, i64, i32, P_i64, P_i64, P_i64, i32, vp, vp, vp]),

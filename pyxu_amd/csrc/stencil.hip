@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(kBlock) nd_kernel(int64_t stack, Geom g, int n
         idx += cc * g.st[d];
       }
       if (ok)
-        acc += coefs[q] * xr[idx];
+        acc = fma(coefs[q], xr[idx], acc);
       else if (ZERO_PARTIAL)
         inside = false;
     }
@@ -126,6 +126,142 @@ __global__ void __launch_bounds__(kBlock) nd_kernel(int64_t stack, Geom g, int n
     T* yp = y + s * ys + r;
     *yp = (beta == T(0)) ? acc : acc + beta * (*yp);
   }
+}
+
+// ------------------------------------------------------------------ N-D stencil, LDS-tiled (2-D / 3-D)
+// One 256-thread workgroup per (4 RPT) x 64 output tile of one plane: the input box the taps reach (every
+// plane of the axis-0 tap range for 3-D) is staged in LDS once, zero outside the array, and the tap table
+// (staged-box offset, coefficient) beside it; a thread owns RPT rows of one column and, per tap, reads its
+// RPT inputs at immediate offsets from one address (fixed pitch of 96 or 128: kernel widths up to 33 / 65).  Per output the taps are summed in list order with one fma each, so
+// the result is the generic kernel's (which walks the same list) -- 15 x 15 taps on 2048^2: 2.08 ms there.
+constexpr int kNdTX = 64;
+constexpr int kNdMaxTaps = 2048;  // tap table in LDS: (offset, coefficient) per tap
+
+struct BoxGeom {
+  int nd;                      // 2 or 3
+  int lo[3], hi[3];            // tap offset range per axis
+  int np, rows;                // staged planes (3-D: hi0 - lo0 + 1) and rows (TY + hi_y - lo_y)
+};
+
+// RPT output rows per thread (TY = 4 RPT rows per tile), PITCH floats per staged row
+template <typename T, bool ZP, int PITCH, int RPT>
+__global__ void __launch_bounds__(kBlock) nd_tile_kernel(int64_t stack, Geom g, BoxGeom b, int ntaps,
+                                                         const int32_t* __restrict__ offs,
+                                                         const T* __restrict__ coefs, const T* __restrict__ x,
+                                                         int64_t xs, T* __restrict__ y, int64_t ys, T beta) {
+  constexpr int TY = 4 * RPT;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int nt4 = (ntaps + 3) & ~3;
+  T* ctab = reinterpret_cast<T*>(smem_raw);          // coefficients
+  int* otab = reinterpret_cast<int*>(ctab + nt4);    // staged-box offsets
+  T* tile = reinterpret_cast<T*>(otab + nt4);
+  const int nd = b.nd;
+  const int ay = nd - 2, ax = nd - 1;
+  const int64_t ny = g.n[ay], nx = g.n[ax];
+  const int64_t n0 = nd == 3 ? g.n[0] : 1;
+  const int64_t sp = blockIdx.z;  // stack * n0 + plane
+  const int64_t s = sp / n0, p = sp - s * n0;
+  const int y0 = (int)blockIdx.y * TY, x0 = (int)blockIdx.x * kNdTX;
+  const T* xsb = x + s * xs;
+  const int cols = kNdTX + b.hi[ax] - b.lo[ax];
+  for (int q = threadIdx.x; q < ntaps; q += kBlock) {
+    const int32_t* o = offs + q * nd;
+    const int op = nd == 3 ? o[0] - b.lo[0] : 0;
+    otab[q] = (op * b.rows + (o[ay] - b.lo[ay])) * PITCH + (o[ax] - b.lo[ax]);
+    ctab[q] = coefs[q];
+  }
+  // stage the input box (zero outside the array)
+  const int box = b.np * b.rows * cols;
+  for (int i = threadIdx.x; i < box; i += kBlock) {
+    const int pl = i / (b.rows * cols), rem = i - pl * (b.rows * cols);
+    const int r = rem / cols, c = rem - r * cols;
+    const int64_t gp = nd == 3 ? p + b.lo[0] + pl : 0;
+    const int64_t gy = (int64_t)y0 + b.lo[ay] + r, gx = (int64_t)x0 + b.lo[ax] + c;
+    T v = T(0);
+    if (gp >= 0 && gp < n0 && gy >= 0 && gy < ny && gx >= 0 && gx < nx)
+      v = xsb[(nd == 3 ? gp * g.st[0] : 0) + gy * g.st[ay] + gx];
+    tile[(pl * b.rows + r) * PITCH + c] = v;
+  }
+  __syncthreads();
+  const int col = (int)threadIdx.x % kNdTX, r0 = ((int)threadIdx.x / kNdTX) * RPT;
+  const T* tb = tile + r0 * PITCH + col;
+  T acc[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) acc[i] = T(0);
+#pragma unroll 4
+  for (int q = 0; q < ntaps; ++q) {
+    const T cq = ctab[q];  // same address in every lane: broadcast
+    const T* t = tb + otab[q];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) acc[i] = fma(cq, t[i * PITCH], acc[i]);
+  }
+  const int64_t gx = (int64_t)x0 + col;
+  if (gx >= nx) return;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int64_t gy = (int64_t)y0 + r0 + i;
+    if (gy >= ny) continue;
+    T v = acc[i];
+    if (ZP) {  // every tap must lie inside the array
+      bool in = gy + b.lo[ay] >= 0 && gy + b.hi[ay] < ny && gx + b.lo[ax] >= 0 && gx + b.hi[ax] < nx;
+      if (nd == 3) in = in && p + b.lo[0] >= 0 && p + b.hi[0] < n0;
+      if (!in) v = T(0);
+    }
+    T* yp = y + s * ys + (nd == 3 ? p * g.st[0] : 0) + gy * g.st[ay] + gx;
+    *yp = (beta == T(0)) ? v : v + beta * (*yp);
+  }
+}
+
+// the tiled kernel when it applies (2-D / 3-D, <= 2048 taps, kernel width <= 65, staged box <= 96 KB);
+// false otherwise.  8 output rows per thread when the box fits, else 4.
+template <typename T>
+bool launch_nd_tile(int64_t stack, const Geom& g, int ntaps, const int32_t* offs, const T* coefs, const int32_t* lo,
+                    const int32_t* hi, int zero_partial, const T* x, int64_t xs, T* y, int64_t ys, T beta,
+                    hipStream_t st, int* status) {
+  if ((g.nd != 2 && g.nd != 3) || lo == nullptr || hi == nullptr || ntaps < 1 || ntaps > kNdMaxTaps) return false;
+  BoxGeom b;
+  b.nd = g.nd;
+  for (int a = 0; a < 3; ++a) b.lo[a] = b.hi[a] = 0;
+  for (int a = 0; a < g.nd; ++a) {
+    if (lo[a] > hi[a] || hi[a] - lo[a] > 64 || lo[a] < -65536 || hi[a] > 65536) return false;
+    b.lo[a] = lo[a];
+    b.hi[a] = hi[a];
+  }
+  const int ay = g.nd - 2, ax = g.nd - 1;
+  const int width = b.hi[ax] - b.lo[ax] + 1;
+  const int pitch = width <= 33 ? 96 : 128;
+  b.np = g.nd == 3 ? b.hi[0] - b.lo[0] + 1 : 1;
+  const size_t tabs = (size_t)((ntaps + 3) & ~3) * (sizeof(T) + sizeof(int));
+  auto smem_for = [&](int ty) { return tabs + (size_t)b.np * (ty + b.hi[ay] - b.lo[ay]) * pitch * sizeof(T); };
+  const int rpt = smem_for(32) <= 96 * 1024 ? 8 : 4;
+  const int ty = 4 * rpt;
+  b.rows = ty + b.hi[ay] - b.lo[ay];
+  const size_t smem = smem_for(ty);
+  if (smem > 96 * 1024) return false;
+  const int64_t n0 = g.nd == 3 ? g.n[0] : 1;
+  const int64_t tyn = (g.n[ay] + ty - 1) / ty, txn = (g.n[ax] + kNdTX - 1) / kNdTX;
+  if (tyn > 65535 || txn > 0x7fffffff || stack * n0 > 0x7fffffff) return false;
+  const dim3 grid((unsigned)txn, (unsigned)tyn, (unsigned)(stack * n0));
+  static bool attr = false;
+  if (!attr) {
+    const void* ks[] = {(const void*)nd_tile_kernel<T, false, 96, 8>, (const void*)nd_tile_kernel<T, true, 96, 8>,
+                        (const void*)nd_tile_kernel<T, false, 128, 8>, (const void*)nd_tile_kernel<T, true, 128, 8>,
+                        (const void*)nd_tile_kernel<T, false, 96, 4>, (const void*)nd_tile_kernel<T, true, 96, 4>,
+                        (const void*)nd_tile_kernel<T, false, 128, 4>, (const void*)nd_tile_kernel<T, true, 128, 4>};
+    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    attr = true;
+  }
+  using K = void (*)(int64_t, Geom, BoxGeom, int, const int32_t*, const T*, const T*, int64_t, T*, int64_t, T);
+  K kern;
+  if (rpt == 8)
+    kern = zero_partial ? (pitch == 96 ? nd_tile_kernel<T, true, 96, 8> : nd_tile_kernel<T, true, 128, 8>)
+                        : (pitch == 96 ? nd_tile_kernel<T, false, 96, 8> : nd_tile_kernel<T, false, 128, 8>);
+  else
+    kern = zero_partial ? (pitch == 96 ? nd_tile_kernel<T, true, 96, 4> : nd_tile_kernel<T, true, 128, 4>)
+                        : (pitch == 96 ? nd_tile_kernel<T, false, 96, 4> : nd_tile_kernel<T, false, 128, 4>);
+  hipLaunchKernelGGL(kern, grid, dim3(kBlock), smem, st, stack, g, b, ntaps, offs, coefs, x, xs, y, ys, beta);
+  *status = last_launch_status();
+  return true;
 }
 
 // ------------------------------------------------------------------ Pad / Pad^T / Trim
@@ -358,6 +494,28 @@ int pxa_stencil_nd(int dtype, int64_t stack, int ndim, const int64_t* shape, int
                          (T)beta);
     return last_launch_status();
   });
+}
+
+int pxa_stencil_nd_box(int dtype, int64_t stack, int ndim, const int64_t* shape, int ntaps, const int32_t* offsets_dev,
+                       const void* coefs_dev, const int32_t* off_lo, const int32_t* off_hi, int zero_partial,
+                       const void* x, int64_t x_stack_stride, void* y, int64_t y_stack_stride, double beta,
+                       void* stream) {
+  Geom g;
+  PXA_CHECK_ARG(make_geom(ndim, shape, g));
+  PXA_CHECK_ARG(ntaps >= 0 && stack >= 0);
+  PXA_CHECK_ARG(ntaps == 0 || (offsets_dev != nullptr && coefs_dev != nullptr));
+  if (stack == 0) return PXA_OK;
+  PXA_CHECK_ARG(x != nullptr && y != nullptr);
+  if ((tuning(PXA_TUNE_STENCIL_ND) & 1) == 0) {
+    PXA_DISPATCH(dtype, T, {
+      int status = PXA_OK;
+      if (launch_nd_tile<T>(stack, g, ntaps, offsets_dev, (const T*)coefs_dev, off_lo, off_hi, zero_partial,
+                            (const T*)x, x_stack_stride, (T*)y, y_stack_stride, (T)beta, as_stream(stream), &status))
+        return status;
+    });
+  }
+  return pxa_stencil_nd(dtype, stack, ndim, shape, ntaps, offsets_dev, coefs_dev, zero_partial, x, x_stack_stride, y,
+                        y_stack_stride, beta, stream);
 }
 
 int pxa_pad(int dtype, int64_t stack, int ndim, const int64_t* shape, const int64_t* pad_lo, const int64_t* pad_hi,

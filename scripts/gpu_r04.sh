@@ -157,6 +157,10 @@ if [ "$S" = "grad" ]; then
   step gradfetch 120 rocprofv3 --pmc FETCH_SIZE -d $P/grad_fetch -o run --output-format csv -- python3 scripts/grad_probe.py 1024x1024x1024 3
   step gradwrite 120 rocprofv3 --pmc WRITE_SIZE -d $P/grad_write -o run --output-format csv -- python3 scripts/grad_probe.py 1024x1024x1024 3
 fi
+if [ "$S" = "stnd" ]; then
+  step stndtests 300 $PT -m gpu tests/test_gpu_stencil_nd_tile.py tests/test_gpu_stencil_fft.py
+  step ops 300 python3 scripts/bench_ops.py
+fi
 if [ "$S" = "full" ]; then
   step pytest 1000 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
