@@ -75,8 +75,10 @@ extern "C" {
 #define PXA_TUNE_GRAD_KERNEL 9 /* A/B of pxa_gradient2 / pxa_gradient2_adjoint: 0 the axis-0 march (each input plane
                                   loaded once, XCD-banded in-plane blocks), 1 the row kernel of rounds 1-3 (same
                                   bits) */
-#define PXA_TUNE_STENCIL_ND 10 /* A/B of pxa_stencil_nd_box: 0 the LDS-tiled kernel where it applies, 1 always the
-                                   generic one-thread-per-output kernel (same sums) */
+#define PXA_TUNE_STENCIL_ND 10 /* A/B of the stencil kernels: bit 0 makes pxa_stencil_nd_box use the generic
+                                   one-thread-per-output kernel instead of the LDS-tiled one, bit 1 makes the
+                                   separable-axis passes (pxa_stencil_axis / _sep) use the scalar kernel instead of
+                                   the vector one (same sums either way) */
 #define PXA_TUNE_COUNT 11
 
 /* Row reductions (pxa_row_reduce). */

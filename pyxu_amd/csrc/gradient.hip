@@ -109,6 +109,11 @@ __device__ inline void stv_nt(T* p, const T (&v)[V]) {
   }
 }
 
+__device__ inline unsigned band_xcd(unsigned bid, unsigned nb) {  // XCD g = bid % 8 takes a contiguous band
+  const unsigned q8 = nb >> 3, r8 = nb & 7u, g8 = bid & 7u;
+  return g8 * q8 + (g8 < r8 ? g8 : r8) + (bid >> 3);
+}
+
 // values of x at i0 + e + o (e < V) along direction d, given the centre vector xc = x[i0 .. i0 + V) and the
 // item's coordinate ca along the direction's axis (non-last axes): |o| <= 1 on the last axis reuses xc and
 // loads one scalar, o == 0 is xc itself, other axes one vector load
@@ -151,7 +156,8 @@ template <typename T, int V, bool ADJ>
 __global__ void __launch_bounds__(kBlock) grad_rows_kernel(int64_t N, Dirs<T> dd, RowGeom g, const T* __restrict__ in,
                                                            T* __restrict__ out) {
   constexpr int U = 2;
-  for (int64_t base = blockIdx.x; base < g.items; base += (int64_t)U * gridDim.x) {
+  // XCD-banded: the workgroups of one XCD take consecutive items, so row + 1 is read from the same L2
+  for (int64_t base = band_xcd(blockIdx.x, gridDim.x); base < g.items; base += (int64_t)U * gridDim.x) {
     T res[U][ADJ ? 1 : PXA_MAX_DIM][V];
     int64_t s_[U], i0_[U];
     bool ok[U];
@@ -252,11 +258,6 @@ struct MarchGeom {
   int64_t mlen[PXA_MAX_DIM];     // its length
   int last[PXA_MAX_DIM];          // the direction differentiates the last axis
 };
-
-__device__ inline unsigned band_xcd(unsigned bid, unsigned nb) {  // XCD g = bid % 8 takes a contiguous band
-  const unsigned q8 = nb >> 3, r8 = nb & 7u, g8 = bid & 7u;
-  return g8 * q8 + (g8 < r8 ? g8 : r8) + (bid >> 3);
-}
 
 template <typename T, int V, bool ADJ, bool NT>
 __global__ void __launch_bounds__(kBlock) grad_march_kernel(int64_t N, Dirs<T> dd, MarchGeom g,

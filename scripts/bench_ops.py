@@ -67,6 +67,17 @@ def main():
                 ms = timed(lambda: op.apply(x), reps=5 if path == "direct" and N * k.size > 1e10 else 20)
                 out.append({"op": f"Stencil.apply[{path}]", "shape": sh, "kernel": list(K), "ms": round(ms, 4),
                             "gbs": round(8 * N / (ms * 1e-3) / 1e9, 1)})
+    with pxrt.Precision(pxrt.Width.SINGLE):  # separable Gaussian (13 taps per axis), constant and reflect modes
+        for sh in [(2048, 2048), (512, 512, 512)]:
+            N = int(np.prod(sh))
+            x = torch.randn(N, device="cuda", dtype=torch.float32, generator=g)
+            for mode in ("constant", "reflect"):
+                op = pxo.Gaussian(arg_shape=sh, sigma=2.0, truncate=3.0, mode=mode) if hasattr(pxo, "Gaussian") else None
+                if op is None:
+                    continue
+                ms = timed(lambda: op.apply(x), reps=5 if N > 1e8 else 20)
+                out.append({"op": f"Gaussian.apply[{mode}]", "shape": sh, "ms": round(ms, 4),
+                            "gbs_per_axis_pass": round(len(sh) * 8 * N / (ms * 1e-3) / 1e9, 1)})
     for line in out:
         line["shape"] = list(line["shape"])
         print(json.dumps(line), flush=True)

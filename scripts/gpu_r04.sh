@@ -158,7 +158,7 @@ if [ "$S" = "grad" ]; then
   step gradwrite 120 rocprofv3 --pmc WRITE_SIZE -d $P/grad_write -o run --output-format csv -- python3 scripts/grad_probe.py 1024x1024x1024 3
 fi
 if [ "$S" = "stnd" ]; then
-  step stndtests 300 $PT -m gpu tests/test_gpu_stencil_nd_tile.py tests/test_gpu_stencil_fft.py
+  step stndtests 300 $PT -m gpu tests/test_gpu_stencil_nd_tile.py tests/test_gpu_stencil_fft.py tests/test_gpu_filters.py tests/test_gpu_gradient_kernels.py
   step ops 300 python3 scripts/bench_ops.py
 fi
 if [ "$S" = "full" ]; then
