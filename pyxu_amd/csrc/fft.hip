@@ -228,6 +228,7 @@ struct FftPlan {
   int64_t tn1;              // 0: results back in place of the line; > 0: four-step transposed store (below)
   int lpb;                  // lines per workgroup
   int pitch;                // fft_lds_kernel: LDS elements per line
+  int no_fast;              // fft_lds_kernel: 1 = generic load / store paths only (PXA_TUNE_FFT_KERNEL bit 1024, A/B)
   int probe;                // fft_lds_kernel, probe build only: 16 skip stages, 32 skip loads, 64 skip stores, 128 no twiddle loads
   int nst;
   int radix[kMaxStages];
@@ -600,7 +601,7 @@ __global__ void __launch_bounds__(TH, 4) fft_lds_kernel(FftPlan p, const Cx<T>* 
   // VALU per element on 64-bit offsets and swizzles
   const bool span_ok = p.n * p.inner * (int64_t)sizeof(Cx<T>) < ((int64_t)1 << 31);
   auto fast_ok = [&](bool lf, bool out) {
-    return full && (!lf || (!(out && p.tn1 > 0) && fixed_line && p.inner % L == 0 && span_ok));
+    return !p.no_fast && full && (!lf || (!(out && p.tn1 > 0) && fixed_line && p.inner % L == 0 && span_ok));
   };
   auto fast_lines = [&](auto out, auto lf, auto lin) {
     Cx<T>* gb;
@@ -842,6 +843,7 @@ int launch_lds_fft_th(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, const C
   p.lpb = L;
   p.pitch = fft_pitch((int)p.n, L);
   p.probe = kFftProbes ? (tuning(PXA_TUNE_FFT_KERNEL) & 0xF0) : 0;
+  p.no_fast = (tuning(PXA_TUNE_FFT_KERNEL) & 1024) ? 1 : 0;
   const int64_t blocks = (p.lines + L - 1) / L;
   PXA_CHECK_ARG(blocks <= 0x7fffffff);
   const size_t smem = (size_t)L * p.pitch * sizeof(Cx<T>);

@@ -161,6 +161,13 @@ if [ "$S" = "stnd" ]; then
   step stndtests 300 $PT -m gpu tests/test_gpu_stencil_nd_tile.py tests/test_gpu_stencil_fft.py tests/test_gpu_filters.py tests/test_gpu_gradient_kernels.py
   step ops 300 python3 scripts/bench_ops.py
 fi
+if [ "$S" = "f64" ]; then
+  step f64a 120 python3 scripts/fft_f64_check.py 0
+  step f64b 120 python3 scripts/fft_f64_check.py 1024
+  step f64c 120 python3 scripts/fft_f64_check.py 256
+  step f64d 120 python3 scripts/fft_f64_check.py 1
+  step f64e 120 python3 scripts/fft_f64_check.py 0
+fi
 if [ "$S" = "full" ]; then
   step pytest 1000 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
