@@ -71,7 +71,8 @@ extern "C" {
 #define PXA_TUNE_FFT_KERNEL 8 /* A/B of the in-LDS FFT (pxa_fft, lines that fit one workgroup): 0 in-place register-staged
                                  stages on padded lines with a twiddle table, 1 the ping-pong Stockham kernel of rounds
                                  1-3 (results equal up to rounding); bits 256 / 512 force 512- / 1024-thread
-                                 workgroups of the in-place kernel */
+                                 workgroups of the in-place kernel, bit 1024 turns off its buffer-load fast path
+                                 (same bits) */
 #define PXA_TUNE_GRAD_KERNEL 9 /* A/B of pxa_gradient2 / pxa_gradient2_adjoint: 0 the axis-0 march (each input plane
                                   loaded once, XCD-banded in-plane blocks), 1 the row kernel of rounds 1-3 (same
                                   bits) */
