@@ -79,7 +79,8 @@ extern "C" {
 #define PXA_TUNE_STENCIL_ND 10 /* A/B of the stencil kernels: bit 0 makes pxa_stencil_nd_box use the generic
                                    one-thread-per-output kernel instead of the LDS-tiled one, bit 1 makes the
                                    separable-axis passes (pxa_stencil_axis / _sep) use the scalar kernel instead of
-                                   the vector one (same sums either way) */
+                                   the vector / LDS-tiled ones, bit 2 turns off the LDS-tiled off-last-axis pass
+                                   (same sums either way) */
 #define PXA_TUNE_COUNT 11
 
 /* Row reductions (pxa_row_reduce). */

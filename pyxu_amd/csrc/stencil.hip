@@ -144,6 +144,83 @@ __global__ void __launch_bounds__(kBlock) axis_vec_kernel(int64_t stack, Geom g,
   }
 }
 
+// LDS-tiled off-last-axis pass (round 4): a workgroup stages a (TA + reach) x 256-element block of rows
+// along the pass axis once (16-B vector loads, zero outside the axis) and each thread sums its vector column
+// for TA / 4 output rows from LDS (ds_read_b128 per tap): the vector kernel above re-reads every input row
+// once per tap from L2.  Same sums in the same tap order, one fma each.
+constexpr int kAxTA = 32, kAxTC = 256;  // output rows along the axis, elements along the inner dimension
+
+template <typename T, bool ZERO_PARTIAL>
+__global__ void __launch_bounds__(kBlock) axis_lds_kernel(int64_t sa, int64_t na, int64_t outer_per_stack,
+                                                          AxisTaps<T> tp, int omin, int reach,
+                                                          const T* __restrict__ x, int64_t xs, T* __restrict__ y,
+                                                          int64_t ys, T beta) {
+  constexpr int V = kVecN<T>;
+  constexpr int TCV = kAxTC / 4;  // vectors per staged row (fp32: 64; fp64 rows are 128 elements wide)
+  using VT = typename Vec4<T>::type;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  T* tile = reinterpret_cast<T*>(smem_raw);  // [row][TCV * V]
+  constexpr int W = TCV * V;
+  const int64_t oz = blockIdx.z;
+  const int64_t s = oz / outer_per_stack, o = oz - s * outer_per_stack;
+  const int64_t a0 = (int64_t)blockIdx.y * kAxTA;
+  const int64_t c0 = (int64_t)blockIdx.x * W;  // first inner element of the block
+  const int64_t base_x = s * xs + o * na * sa, base_y = s * ys + o * na * sa;
+  const int rows = kAxTA + reach;
+  for (int i = threadIdx.x; i < rows * TCV; i += kBlock) {
+    const int r = i / TCV, cv = i - r * TCV;
+    const int64_t ga = a0 + omin + r, gc = c0 + (int64_t)cv * V;
+    T v[V];
+    if (ga >= 0 && ga < na && gc < sa) {
+      *reinterpret_cast<VT*>(v) = *reinterpret_cast<const VT*>(x + base_x + ga * sa + gc);
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] = T(0);
+    }
+    *reinterpret_cast<VT*>(tile + r * W + cv * V) = *reinterpret_cast<const VT*>(v);
+  }
+  __syncthreads();
+  const int cv = (int)threadIdx.x % TCV, rg = (int)threadIdx.x / TCV;  // vector column, row group
+  constexpr int RG = kBlock / TCV, RPT = kAxTA / RG;                      // row groups, rows per thread
+  const int64_t gc = c0 + (int64_t)cv * V;
+  if (gc >= sa) return;
+#pragma unroll 1
+  for (int k = 0; k < RPT; ++k) {
+    const int i = rg * RPT + k;  // output row within the tile
+    const int64_t ga = a0 + i;
+    if (ga >= na) break;
+    T acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = T(0);
+    bool inside = true;
+    for (int q = 0; q < tp.n; ++q) {
+      const int o2 = tp.off[q];
+      const int64_t c = ga + o2;
+      if (c >= 0 && c < na) {
+        T v[V];
+        *reinterpret_cast<VT*>(v) = *reinterpret_cast<const VT*>(tile + (i + o2 - omin) * W + cv * V);
+        const T cq = tp.coef[q];
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = fma(cq, v[e], acc[e]);
+      } else if (ZERO_PARTIAL) {
+        inside = false;
+      }
+    }
+    if (ZERO_PARTIAL && !inside) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = T(0);
+    }
+    T* yp = y + base_y + ga * sa + gc;
+    if (beta != T(0)) {
+      T old[V];
+      *reinterpret_cast<VT*>(old) = *reinterpret_cast<const VT*>(yp);
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = acc[e] + beta * old[e];
+    }
+    *reinterpret_cast<VT*>(yp) = *reinterpret_cast<const VT*>(acc);
+  }
+}
+
 template <typename T>
 int launch_axis(int64_t stack, const Geom& g, int axis, int ntaps, const int32_t* offs, const double* coefs,
                 int zero_partial, const void* x, int64_t xs, void* y, int64_t ys, double beta, hipStream_t s) {
@@ -156,6 +233,32 @@ int launch_axis(int64_t stack, const Geom& g, int axis, int ntaps, const int32_t
   int64_t total = stack * g.size;
   constexpr int V = kVecN<T>;
   const bool last = axis == g.nd - 1;
+  // off-last-axis passes LDS-tiled (512^3 Gaussian 1.78 -> 1.48 ms; PXA_TUNE_STENCIL_ND bit 2 turns it off,
+  // bit 1 selects the scalar kernel for every pass)
+  if ((tuning(PXA_TUNE_STENCIL_ND) & 6) == 0 && !last && g.n[g.nd - 1] % V == 0 && xs % V == 0 && ys % V == 0 &&
+      aligned16(x) && aligned16(y) && ntaps > 0) {
+    int omin = 0, omax = 0;
+    for (int q = 0; q < ntaps; ++q) {
+      omin = q == 0 || offs[q] < omin ? offs[q] : omin;
+      omax = q == 0 || offs[q] > omax ? offs[q] : omax;
+    }
+    const int reach = omax - omin;
+    const int64_t sa = g.st[axis], na = g.n[axis];
+    const int64_t opv = g.size / (na * sa);
+    const int W = (kAxTC / 4) * V;
+    const size_t smem = (size_t)(kAxTA + reach) * W * sizeof(T);
+    const int64_t gx = (sa + W - 1) / W, gy = (na + kAxTA - 1) / kAxTA, gz = stack * opv;
+    if (smem <= 64 * 1024 && gy <= 65535 && gz <= 65535 && gx <= 0x7fffffff) {
+      const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
+      if (zero_partial)
+        hipLaunchKernelGGL((axis_lds_kernel<T, true>), grid, dim3(kBlock), smem, s, sa, na, opv, tp, omin, reach,
+                           (const T*)x, xs, (T*)y, ys, (T)beta);
+      else
+        hipLaunchKernelGGL((axis_lds_kernel<T, false>), grid, dim3(kBlock), smem, s, sa, na, opv, tp, omin, reach,
+                           (const T*)x, xs, (T*)y, ys, (T)beta);
+      return last_launch_status();
+    }
+  }
   if ((tuning(PXA_TUNE_STENCIL_ND) & 2) == 0 && g.n[g.nd - 1] % V == 0 && xs % V == 0 && ys % V == 0 &&
       aligned16(x) && aligned16(y)) {
     const int64_t items = total / V;

@@ -11,6 +11,7 @@ import torch
 
 import pyxu_amd.operator as pxo
 import pyxu_amd.runtime as pxrt
+from pyxu_amd import _dev
 
 
 def timed(fn, reps=20):
@@ -75,9 +76,12 @@ def main():
                 op = pxo.Gaussian(arg_shape=sh, sigma=2.0, truncate=3.0, mode=mode) if hasattr(pxo, "Gaussian") else None
                 if op is None:
                     continue
-                ms = timed(lambda: op.apply(x), reps=5 if N > 1e8 else 20)
-                out.append({"op": f"Gaussian.apply[{mode}]", "shape": sh, "ms": round(ms, 4),
-                            "gbs_per_axis_pass": round(len(sh) * 8 * N / (ms * 1e-3) / 1e9, 1)})
+                for knob in (0, 4):  # PXA_TUNE_STENCIL_ND bit 2 set: no LDS-tiled off-last-axis passes
+                    old = _dev.tuning(_dev.TUNE_STENCIL_ND, knob)
+                    ms = timed(lambda: op.apply(x), reps=5 if N > 1e8 else 20)
+                    _dev.tuning(_dev.TUNE_STENCIL_ND, old)
+                    out.append({"op": f"Gaussian.apply[{mode}]", "knob": knob, "shape": sh, "ms": round(ms, 4),
+                                "gbs_per_axis_pass": round(len(sh) * 8 * N / (ms * 1e-3) / 1e9, 1)})
     for line in out:
         line["shape"] = list(line["shape"])
         print(json.dumps(line), flush=True)

@@ -65,8 +65,9 @@ SEP_CASES = [((96, 130), 2.0, "constant"), ((64, 64), 1.5, "reflect"), ((20, 24,
 @pytest.mark.parametrize("stack", [1, 3])
 def test_separable_vector_pass_matches_scalar(shape, sigma, mode, dt, stack):
     """separable-axis passes (Gaussian: pxa_stencil_sep in constant mode, pxa_stencil_axis on the padded array
-    otherwise): the vector kernel (PXA_TUNE_STENCIL_ND bit 1 clear) against the scalar one, bit for bit; rows
-    whose length is not a multiple of the vector width take the scalar kernel either way"""
+    otherwise): the default (LDS-tiled off-last-axis passes, vector last-axis pass), the vector kernel alone
+    (PXA_TUNE_STENCIL_ND bit 2) and the scalar one (bit 1), bit for bit; rows whose length is not a multiple of the vector width take
+    the scalar kernel either way"""
     rng = np.random.default_rng(sum(shape) + stack)
     x = rng.standard_normal((stack, int(np.prod(shape))))
     width = pxrt.Width.SINGLE if dt == np.float32 else pxrt.Width.DOUBLE
@@ -74,8 +75,9 @@ def test_separable_vector_pass_matches_scalar(shape, sigma, mode, dt, stack):
         op = pxo.Gaussian(arg_shape=shape, sigma=sigma, truncate=3.0, mode=mode)
         xt = torch.tensor(x, dtype=torch.float32 if dt == np.float32 else torch.float64, device="cuda")
         for adjoint in (False, True):
-            a, b = run(op, xt, adjoint, 0), run(op, xt, adjoint, 2)
+            a, b, c = run(op, xt, adjoint, 0), run(op, xt, adjoint, 2), run(op, xt, adjoint, 4)
             assert np.array_equal(a, b), (adjoint, float(np.max(np.abs(a - b))))
+            assert np.array_equal(c, b), (adjoint, "vector", float(np.max(np.abs(c - b))))
         if mode == "constant":
             got = run(op, xt, False, 0)
             ref = np.stack([ndi.gaussian_filter(x[s].reshape(shape), sigma, mode="constant", cval=0.0, truncate=3.0)
