@@ -29,7 +29,9 @@ Sub-records on the same line (north_star):
         (--c3-three-launch: the three-launch step A / B / C; single GPU: replicas only at N > 1);
   "k4": SURVEY §8(d)'s "Gradient + prox" kernel alone (pxa_tv_dual_update) at 2048^2 and 1024^3;
   "dense_mfma": the dense LinOp's MFMA path (8192 x 65536 K, B = 64 / 128 right-hand sides) in TFLOP/s.
-Every sub-record carries a `cpu_baseline` (the oracle on the host's cores, bounded sample).
+The solver sub-records (c2_4096, c5, c4, and c3 per algorithm) carry a `cpu_baseline` (the oracle on the host's
+cores, bounded sample); the kernel-only records (k4, dense_mfma) carry rooflines instead, the oracle having no
+kernel-level equivalent of them.
 
 Roofline convention.  `frac` is the dominant kernel's time against ITS OWN compulsory bytes (every array
 it must read or write, once): the fused PGD launch reads x, x_prev, H^T y and writes x_new = 16 B/pixel.  `frac_survey` keeps SURVEY §8(d)'s 48 B/pixel figure for the same time; that model is not a
@@ -297,6 +299,54 @@ def cpu_baseline_c4(M, N, threads, steps=4, lam=0.01):
         if ctxm is not None:
             ctxm.restore_original_limits()
     return 1e3 * ((t2 - t1) - (t1 - t0)) / steps, used
+
+
+def cpu_baseline_c3(n, budget_s, seed=7, lam=0.01, sigma=2.0):
+    """C3 (PD3O / Condat-Vu, S = Gaussian(sigma) 3-D blur, K = Gradient, h = lam L1, g = None): the oracle's
+    pd3o / condat_vu (pds.py:722-761, 429-442 restated in NumPy, one thread) on an n^3 volume of the same
+    problem.  Every operator of the step is an O(voxels) stencil, so the per-voxel cost is size-independent and
+    the 1024^3 iteration time is voxels(1024^3) / (voxel-iterations/s of the sample).  Per algorithm: one
+    iteration (set-up + page-in), then as many as fit in `budget_s` (at least 1), timed as the difference.
+    Returns {algo: (voxel-iterations/s, timed iterations, seconds)}."""
+    import oracle as orc
+
+    sh = (n, n, n)
+    N = n ** 3
+    rng = np.random.default_rng(seed)
+    taps, c = orc.gaussian_taps(sigma, 3.0, np.float32)
+    K3, C3 = [taps] * 3, [c] * 3
+    x_gt = np.zeros(sh, np.float32)
+    for _ in range(12):  # piecewise-constant phantom, as bench_c3
+        lo = [int(rng.integers(0, n // 2)) for _ in sh]
+        hi = [v + int(rng.integers(n // 8 + 1, n // 2 + 1)) for v in lo]
+        x_gt[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] = float(rng.uniform(0.2, 1.0))
+    y = orc.stencil_apply(x_gt.reshape(-1), sh, K3, C3)
+    y = (y + (0.01 * rng.standard_normal(N)).astype(np.float32)).astype(np.float32)
+    blur = dict(arg_shape=sh, kernel=K3, center=C3)
+    grad_f = lambda v: orc.deblur_tv_grad(v, blur, y, 0.0, 1.0, dict(arg_shape=sh))
+    Kf = lambda v: orc.gradient_apply(v, arg_shape=sh)
+    KT = lambda v: orc.gradient_adjoint(v, arg_shape=sh)
+    lam32 = np.float32(lam)
+    fprox = lambda v, s_: orc.fenchel_prox(lambda a, t: orc.l1_prox(a, t * lam32), v, s_)
+    x0 = np.zeros(N, np.float32)
+    out = {}
+    for algo in ("pd3o", "cv"):
+        if algo == "pd3o":
+            tau, sig, _, rho = orc.pd3o_step_sizes(1.0, np.sqrt(12.0), np.float32)
+            run = lambda k: orc.pd3o(x0, grad_f, None, Kf, KT, fprox, tau, sig, rho, k)
+        else:
+            tau, sig, _, rho = orc.condat_vu_step_sizes(1.0, np.sqrt(12.0), np.float32)
+            run = lambda k: orc.condat_vu(x0, grad_f, None, Kf, KT, fprox, tau, sig, rho, k)
+        t0 = time.perf_counter()
+        run(1)
+        t1 = time.perf_counter() - t0
+        k = int(max(1, min(50, budget_s / max(t1, 1e-3))))
+        t0 = time.perf_counter()
+        run(1 + k)
+        dt = time.perf_counter() - t0 - t1
+        dt = dt if dt > 0 else time.perf_counter() - t0
+        out[algo] = (N * k / dt, k, dt)
+    return out
 
 
 # ----------------------------------------------------------------------------- timing helpers
@@ -787,6 +837,17 @@ def sub_cpu_baselines(sub, args):
             "value": round(v, 3), "unit": "image-iterations/s", "cores": th, "kind": "port",
             "sample": f"oracle PGD on {imgs} of the {args.c5_images} independent {args.c5_n}^2 images (one image per "
                       f"thread, {th} threads): {it} iterations each in {dt:.1f} s on {model}"}
+    if "c3" in sub and args.c3_cpu_n > 0:
+        n3 = args.c3_n
+        for algo, (vps, k, dt) in cpu_baseline_c3(args.c3_cpu_n, budget).items():
+            if algo in sub["c3"]:
+                sub["c3"][algo]["cpu_baseline"] = {
+                    "value": round(vps / n3 ** 3, 6), "unit": "iterations/s", "ms_per_step": round(1e3 * n3 ** 3 / vps, 1),
+                    "voxel_iterations_per_s": round(vps, 1), "cores": 1, "kind": "port",
+                    "sample": f"oracle {'pd3o' if algo == 'pd3o' else 'condat_vu'} (NumPy restatement of pds.py, one "
+                              f"thread) on a {args.c3_cpu_n}^3 volume of the same problem: {k} iterations in {dt:.1f} s; "
+                              f"{n3}^3 rate = voxel-iterations/s / {n3}^3 (every operator of the step is O(voxels)), "
+                              f"on {model}"}
     if "c4" in sub:
         ms, used = cpu_baseline_c4(args.c4_m, args.c4_n, th)
         per_outer = sub["c4"].get("cg_iters_per_outer") or 13.0
@@ -818,6 +879,7 @@ def main():
     ap.add_argument("--c3-n", type=int, default=1024, help="c3 record: volume edge (0 = skip)")
     ap.add_argument("--c3-steps", type=int, default=10)
     ap.add_argument("--c3-three-launch", action="store_true", help="C3 with the three-launch pxa_pds_step (A/B)")
+    ap.add_argument("--c3-cpu-n", type=int, default=160, help="c3 CPU baseline: oracle sample volume edge (0 = skip)")
     ap.add_argument("--c5-images", type=int, default=512)
     ap.add_argument("--c5-n", type=int, default=512)
     ap.add_argument("--c5-steps", type=int, default=20)

@@ -583,6 +583,29 @@ def tile_partials_fold(parts, rows, per_row, out):
     return out
 
 
+class FlagWaitError(RuntimeError):
+    """A HostFlagBuffer publication never landed although its stream is idle."""
+
+
+def wait_flags(flags, seq, spin_s, stream_idle):
+    """Host side of HostFlagBuffer.wait: busy-poll `flags` (uint32 array in coherent host memory) for
+    `spin_s` seconds, then poll with a yield, asking `stream_idle()` each round.  Once the stream reports idle
+    every write of the kernels before it has landed, so flags that still differ from `seq` after one more
+    look will never change: raise FlagWaitError (the wait used to spin forever there)."""
+    import time
+
+    if (flags == seq).all():
+        return
+    t_end = time.perf_counter() + spin_s
+    while not (flags == seq).all():
+        if time.perf_counter() > t_end:
+            if stream_idle() and not (flags == seq).all():
+                raise FlagWaitError(
+                    f"publication {seq} never landed (flags {np.unique(flags).tolist()[:4]}) and the stream is "
+                    "idle: the publishing kernel did not run, or the sequence number was overwritten")
+            time.sleep(0)
+
+
 class HostFlagBuffer:
     """Coherent host memory (pxa_host_alloc) for statistics a kernel publishes to the host: `values`
     (float64 (nvals,)) and one completion flag per value group (`flags`, uint32 (nflags,)).  The device writes
@@ -622,16 +645,11 @@ class HostFlagBuffer:
         return seq
 
     def wait(self, seq, spin_s=1e-3):
-        """Poll the flags until every value of publication `seq` has landed (as wait_event)."""
-        import time
-
-        f = self.flags
-        if (f == seq).all():
-            return
-        t_end = time.perf_counter() + spin_s
-        while not (f == seq).all():
-            if time.perf_counter() > t_end:
-                time.sleep(0)
+        """Poll the flags until every value of publication `seq` has landed (as wait_event).  Raises
+        instead of spinning forever when the stream has drained without publishing `seq` (an earlier
+        kernel faulted, the publishing kernel never ran, or `seq` was overwritten by a later publication);
+        an asynchronous device error surfaces through the stream query."""
+        wait_flags(self.flags, seq, spin_s, lambda: _torch().cuda.current_stream().query())
 
     def __del__(self):
         if getattr(self, "_ptr", None):

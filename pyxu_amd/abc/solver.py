@@ -156,13 +156,23 @@ class Solver:
 
     # ------------------------------------------------------------------ public API
     def fit(self, **kwargs):
-        self._fit_init(
-            mode=kwargs.pop("mode", Mode.BLOCK),
-            stop_crit=kwargs.pop("stop_crit", None),
-            track_objective=kwargs.pop("track_objective", False),
-        )
-        self.m_init(**kwargs)
-        self._fit_run()
+        from pyxu_amd import profile
+
+        profile.instrument(self)  # PXA_PROFILE roctx ranges / PXA_DEBUG_SYNC checks around m_step
+        prof = profile.enabled()
+        if prof:
+            profile.range_push(f"{type(self).__name__}.fit")
+        try:
+            self._fit_init(
+                mode=kwargs.pop("mode", Mode.BLOCK),
+                stop_crit=kwargs.pop("stop_crit", None),
+                track_objective=kwargs.pop("track_objective", False),
+            )
+            self.m_init(**kwargs)
+            self._fit_run()
+        finally:
+            if prof:
+                profile.range_pop()
 
     def m_init(self, **kwargs):
         raise NotImplementedError
@@ -299,6 +309,9 @@ class Solver:
         (QuadraticFunc.prox -> CG, operator.py:1273-1291), where the reference's per-fit temporary
         folder, log file, worker thread and final checkpoint are side effects nobody reads: they cost
         milliseconds per call against a sub-millisecond iteration on the device."""
+        from pyxu_amd import profile
+
+        profile.instrument(self)
         self._mstate.clear()
         if stop_crit is None:
             stop_crit = self.default_stop_crit()

@@ -1140,6 +1140,11 @@ int launch_normal_group(int64_t M, int64_t N, const float* A, const float* x, fl
   auto* slots = reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(work) + normal_slots_offset(M, N));
   const int rpg = (int)normal_rows_per_group(M);
   solo = solo || C % 8 != 0;  // fewer than 8 groups: the members would not share an XCD
+  // The tag is baked into the launch arguments: a graph replay would reuse it and accept the previous
+  // replay's part-dots from the slots.  Under stream capture every member computes its own parts (solo: no
+  // exchange, same bits).
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) solo = true;
   auto* stats = reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(work) + normal_stats_offset(M, N));
   const int flav = kGroupProbes ? tuning(PXA_TUNE_NORMAL_KERNEL) : 0;
   if (P4 * kParts == N4 && P4 == NVS * kNormThreads)

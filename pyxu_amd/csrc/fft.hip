@@ -15,8 +15,11 @@
 // the stride-n2 axis, twiddles w_n^(k1 j2), n2-point DFTs stored transposed into a workspace, copied
 // back); other lengths by Bluestein's chirp-z (chirp, 2^k-point FFT convolution with the chirp filter,
 // chirp), so every length runs, as in the reference's scipy.fft.
+#include <cmath>
 #include <map>
 #include <mutex>
+#include <utility>
+#include <vector>
 
 #include "common.hpp"
 
@@ -667,26 +670,21 @@ __global__ void __launch_bounds__(TH, 4) fft_lds_kernel(FftPlan p, const Cx<T>* 
 
 // Stage twiddle tables of a power-of-two plan: the stage of span ns and radix R reads w_{ns R}^k, k < ns,
 // at tw[ns + k] (the spans are distinct powers of two, so the ranges [ns, 2 ns) do not overlap; n entries
-// in all).  exp(-2 pi i k / (ns R)) in double, then rounded to T.
+// in all).  exp(-2 pi i k / (ns R)) in long double on the host, then rounded to T (correctly rounded for
+// fp32 and, but for ties at the 2^-64 level, for fp64).
 template <typename T>
-__global__ void __launch_bounds__(kBlock) fft_twiddle_table_kernel(FftPlan p, Cx<T>* __restrict__ tw) {
+void fill_twiddle_table(const FftPlan& p, std::vector<Cx<T>>& tw) {
   const int64_t n = p.n;
-  for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (int64_t)gridDim.x * blockDim.x) {
-    if (m == 0) {
-      tw[0] = Cx<T>{T(1), T(0)};
-      continue;
-    }
-    int64_t ns = 1;
-    int R = 2;
-    for (int s = 0; s < p.nst; ++s) {  // the stage whose range [ns, 2 ns) holds m
-      R = p.radix[s];
-      if (m < 2 * ns) break;
-      ns *= R;
-    }
-    const int64_t k = m - ns;
-    double sn = 0.0, c = 1.0;
-    if (k >= 0 && k < ns) sincospi(2.0 * (double)k / (double)(ns * R), &sn, &c);
-    tw[m] = Cx<T>{(T)c, (T)(-sn)};
+  tw.assign((size_t)n, Cx<T>{T(1), T(0)});
+  int64_t ns = 1;
+  for (int s = 0; s < p.nst; ++s) {
+    const int R = p.radix[s];
+    if (ns > 1)
+      for (int64_t k = 0; k < ns && ns + k < n; ++k) {
+        const long double a = 2.0L * 3.141592653589793238462643383279502884L * (long double)k / (long double)(ns * R);
+        tw[(size_t)(ns + k)] = Cx<T>{(T)cosl(a), (T)(-sinl(a))};
+      }
+    ns *= R;
   }
 }
 
@@ -798,20 +796,30 @@ int launch_stockham(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream
   return last_launch_status();
 }
 
-// Twiddle table of length n (device memory, built once per (n, T) and kept for the process).
+// Twiddle table of length n, in device memory of the current device: built once per (device, n, T) on the
+// host and uploaded with a synchronous hipMemcpy, then kept for the process (a few KB per length).  Keyed by
+// the device ordinal, so a process that drives several GPUs never passes one device's table to another; no
+// stream is touched (no hipStreamSynchronize that would break a stream capture in progress -- the first call
+// for a length must still happen outside a capture, since it allocates).
 template <typename T>
-const Cx<T>* twiddle_table(const FftPlan& p, hipStream_t st) {
+const Cx<T>* twiddle_table(const FftPlan& p) {
   static std::mutex mu;
-  static std::map<int64_t, Cx<T>*> tables;
-  const int64_t n = p.n;
+  static std::map<std::pair<int, int64_t>, Cx<T>*> tables;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const std::pair<int, int64_t> key{dev, p.n};
   std::lock_guard<std::mutex> lock(mu);
-  auto it = tables.find(n);
+  auto it = tables.find(key);
   if (it != tables.end()) return it->second;
+  std::vector<Cx<T>> host;
+  fill_twiddle_table<T>(p, host);
   Cx<T>* tw = nullptr;
-  if (hipMalloc((void**)&tw, (size_t)n * sizeof(Cx<T>)) != hipSuccess) return nullptr;
-  hipLaunchKernelGGL(fft_twiddle_table_kernel<T>, dim3(grid_for(n)), dim3(kBlock), 0, st, p, tw);
-  if (hipStreamSynchronize(st) != hipSuccess) return nullptr;  // once per length: usable from any stream
-  tables[n] = tw;
+  if (hipMalloc((void**)&tw, host.size() * sizeof(Cx<T>)) != hipSuccess) return nullptr;
+  if (hipMemcpy(tw, host.data(), host.size() * sizeof(Cx<T>), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(tw);
+    return nullptr;
+  }
+  tables[key] = tw;
   return tw;
 }
 
@@ -864,7 +872,7 @@ int launch_lds_fft_th(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, const C
 template <typename T>
 int launch_lds_fft(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_t st) {
   if (!factor_lds<T>(p.n, p)) return PXA_ERR_UNSUPPORTED;
-  const Cx<T>* tw = twiddle_table<T>(p, st);
+  const Cx<T>* tw = twiddle_table<T>(p);
   if (tw == nullptr) return launch_stockham<T>(p, inv, src, dst, st);  // no memory for the table
   return lds_fft_threads<T>(p) == 1024 ? launch_lds_fft_th<T, 1024>(p, inv, src, dst, tw, st)
                                        : launch_lds_fft_th<T, 512>(p, inv, src, dst, tw, st);

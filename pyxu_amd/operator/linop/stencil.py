@@ -174,9 +174,19 @@ class Stencil(pxa.SquareOp):
 
     # ------------------------------------------------------------------ FFT path (large N-D kernels)
     # Non-separable constant-mode kernels with at least this many taps go through the FFT.  None: 1280 for 2-D
-    # (the LDS-tiled direct kernel wins below: 2048^2 with 31 x 31 taps 0.30 ms direct, 0.40 ms FFT), 256 for
-    # 3-D and more (9 x 9 x 9 on 256^3: 2.9 ms direct, 1.8 ms FFT); set an int to override.
+    # tap boxes the LDS-tiled direct kernel takes (2048^2 with 31 x 31 taps 0.30 ms direct, 0.40 ms FFT), 256
+    # for other 2-D boxes (wider than 65 on an axis or more than 2048 taps: only the generic one-thread-per-output
+    # kernel would run them, 2.1 ms at 15 x 15 on 2048^2) and for 3-D and more (9 x 9 x 9 on 256^3: 2.9 ms
+    # direct, 1.8 ms FFT); set an int to override.
     FFT_MIN_TAPS = None
+    TILE_MAX_EXTENT, TILE_MAX_TAPS = 65, 2048  # the tiled kernel's envelope (csrc/stencil.hip launch_nd_tile)
+
+    @classmethod
+    def _fft_min_taps(cls, K):
+        if cls.FFT_MIN_TAPS is not None:
+            return cls.FFT_MIN_TAPS
+        tiled = max(K) <= cls.TILE_MAX_EXTENT and int(np.prod(K)) <= cls.TILE_MAX_TAPS
+        return 1280 if (len(K) == 2 and tiled) else 256
 
     @staticmethod
     def _smooth(n):
@@ -202,7 +212,7 @@ class Stencil(pxa.SquareOp):
         plan = None
         st = self._st_fw[0]
         K = st.kernel.shape
-        min_taps = self.FFT_MIN_TAPS if self.FFT_MIN_TAPS is not None else (1280 if len(K) == 2 else 256)
+        min_taps = self._fft_min_taps(K)
         if (not self._separable and all(m == "constant" for m in self._mode) and int(np.prod(K)) >= min_taps):
             L = tuple(self._smooth(n + k - 1) for n, k in zip(self._arg_shape, K))
             lim = 4096 if x.dtype == pxrt.Width.SINGLE.torch else 2048

@@ -1,0 +1,68 @@
+# usage: bash scripts/gpu_r05.sh <tag> <stage>
+# GPU calls of round 5.  Stages:
+#   new    the tests added / touched this round, the default bench line, a kernel trace of the headline
+#   full   the whole -m gpu suite, smoke, the default bench line
+#   prof   rocprofv3 kernel trace (--stats) of the headline + the PGD PMC passes (traffic, occupancy, waits)
+#   c3prof kernel-D / B PMC traffic passes at 1024^3 + the c3 record
+# Test failures (rc 1) do not stop the run; any other failure (fault, abort, timeout) ends it there.
+set -o pipefail
+T=${1:-r05}
+S=${2:-new}
+O=gpurun_out/$T
+mkdir -p $O
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>: run with a time limit; stop the script unless rc in {0, 1}
+  local name=$1 lim=$2; shift 2
+  echo "== $name"
+  timeout -k 10 $lim "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -3 $O/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+PT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+P=$O/prof
+mkdir -p $P
+DRV="python3 bench.py --steps 20 --warmup 5 --no-sub --cpu-seconds 0"
+export PXA_FAIL_DIR=$O/fail
+pmc_pgd() {  # the headline's PGD counters, one pass each (separate runs: FETCH / WRITE / SQ)
+  step pgdfetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/pgdfetch -o run --output-format csv -- $DRV
+  step pgdwrite 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/pgdwrite -o run --output-format csv -- $DRV
+  step pgdsq 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS --kernel-trace -d $P/pgdsq -o run --output-format csv -- $DRV
+  step pgdsq2 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES --kernel-trace -d $P/pgdsq2 -o run --output-format csv -- $DRV
+  python3 scripts/pmc_traffic.py $P/pgdfetch $P/pgdwrite "pgd_tv2d_kernel" pgd_tv2d_kernel@2048x2048 $P/traffic_pgd.json $T || true
+}
+if [ "$S" = "new" ]; then
+  step newtests 900 $PT -m gpu tests/test_gpu_c3_fullsize.py tests/test_gpu_fft.py tests/test_gpu_stencil_fft.py \
+       tests/test_gpu_dense_normal.py tests/test_gpu_solver_engine.py
+  step drv1 120 $DRV
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+  step bench 900 python bench.py --steps 20 --warmup 5
+fi
+if [ "$S" = "pgd" ]; then
+  step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py -k "pgd or c2 or c5 or smoke or trajectory"
+  step drv1 120 $DRV
+  step drv2 120 $DRV
+  step c5 300 python3 bench.py --only c5
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+fi
+if [ "$S" = "prof" ]; then
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+  pmc_pgd
+fi
+if [ "$S" = "c3prof" ]; then
+  step c3 300 python3 bench.py --only c3
+  B3="python3 bench.py --only c3 --c3-steps 3"
+  step fetchc3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetchc3 -o run --output-format csv -- $B3
+  step writec3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writec3 -o run --output-format csv -- $B3
+  python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, true, false, true, true>" pds_march_kernel_pd3o@1024^3 $P/traffic_c3.json $T || true
+  python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, false, false, true, true>" pds_march_kernel_cv@1024^3 $P/traffic_c3.json $T || true
+fi
+if [ "$S" = "full" ]; then
+  step pytest 1200 $PT tests -m gpu
+  step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$S" = "bench" ]; then
+  step bench 1000 python bench.py --steps 20 --warmup 5
+fi
+echo done

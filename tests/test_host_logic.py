@@ -544,3 +544,71 @@ def test_directional_lipschitz_chain_rule():
     assert abs(chain(w, 2, 2, 2, L_grad2) - 5.6568542494923815) < 1e-12
     # 1-D: the reference's square Sum loses the constant in the composition -> inf
     assert np.isinf(chain(np.ones((1, 1)), 1, 1, 1, 2.0))
+
+
+def test_flag_wait_raises_when_stream_idle_and_seq_never_published():
+    """HostFlagBuffer.wait must not spin forever on a sequence number that is never
+    published (faulted or missing kernel, overwritten seq) once the stream has drained."""
+    from pyxu_amd import _dev
+
+    flags = np.zeros(4, dtype=np.uint32)
+    flags[:] = 6
+    _dev.wait_flags(flags, 6, 1e-4, lambda: True)  # already published: returns at once
+    busy = iter([False, False, True])
+    with pytest.raises(_dev.FlagWaitError):
+        _dev.wait_flags(flags, 7, 1e-4, lambda: next(busy))
+    # a publication that lands while the stream is still busy is accepted
+    calls = {"n": 0}
+
+    def idle():
+        calls["n"] += 1
+        if calls["n"] == 3:
+            flags[:] = 8
+        return False
+
+    _dev.wait_flags(flags, 8, 1e-4, idle)
+    assert calls["n"] >= 3
+
+
+def test_stencil_fft_threshold_follows_tile_envelope():
+    """the 1280-tap 2-D FFT threshold holds only for tap boxes the LDS-tiled direct kernel takes
+    (both extents <= 65, <= 2048 taps); wider 2-D boxes (e.g. 5 x 101) keep 256, as do 3-D kernels."""
+    from pyxu_amd.operator.linop.stencil import Stencil
+
+    assert Stencil._fft_min_taps((31, 31)) == 1280
+    assert Stencil._fft_min_taps((65, 19)) == 1280
+    assert Stencil._fft_min_taps((5, 101)) == 256  # 505 taps: FFT, not the generic direct kernel
+    assert Stencil._fft_min_taps((45, 46)) == 256  # 2070 taps: beyond the tap table
+    assert Stencil._fft_min_taps((9, 9, 9)) == 256
+
+
+def test_profile_hooks_wrap_m_step(monkeypatch):
+    """PXA_PROFILE / PXA_DEBUG_SYNC: m_step runs inside a named range and is followed by a device
+    check; with neither flag the method is left alone (and a wrapper of an earlier fit is removed)."""
+    from pyxu_amd import profile
+
+    calls = []
+
+    class FakeSolver:
+        _astate = {"idx": 3}
+
+        def m_step(self):
+            calls.append("step")
+
+    monkeypatch.setattr(profile, "range_push", lambda n: calls.append(("push", n)))
+    monkeypatch.setattr(profile, "range_pop", lambda: calls.append("pop"))
+    monkeypatch.setattr(profile, "_check_device", lambda: calls.append("sync"))
+    s = FakeSolver()
+    monkeypatch.setenv("PXA_PROFILE", "1")
+    monkeypatch.setenv("PXA_DEBUG_SYNC", "1")
+    profile.instrument(s)
+    profile.instrument(s)  # idempotent
+    s.m_step()
+    assert calls == [("push", "FakeSolver.m_step[3]"), "step", "sync", "pop"]
+    monkeypatch.setenv("PXA_PROFILE", "0")
+    monkeypatch.setenv("PXA_DEBUG_SYNC", "0")
+    profile.instrument(s)
+    calls.clear()
+    s.m_step()
+    assert calls == ["step"]
+    assert profile._roctx().roctxRangePushA(b"x") >= 0 and profile._roctx().roctxRangePop() >= -1  # loads here
