@@ -6,6 +6,7 @@ Every function takes/returns torch-ROCm tensors resident on the current device, 
 a TypeError: this package has no CPU compute path.
 """
 import ctypes as ct
+import os
 
 import numpy as np
 
@@ -226,6 +227,15 @@ def tuning(key, value=-1):
     if r < 0:
         check(r, "pxa_tuning")
     return r
+
+
+def _tuning_from_env():
+    """PXA_TUNE="key=value[,key=value...]" (keys: the PXA_TUNE_* numbers) sets knobs at import, so that A/B
+    runs of bench.py / scripts need no code change."""
+    spec = os.environ.get("PXA_TUNE", "").strip()
+    for item in filter(None, (t.strip() for t in spec.split(","))):
+        k, _, v = item.partition("=")
+        tuning(int(k), int(v))
 
 
 def empty(shape, like):
@@ -1027,3 +1037,6 @@ def complex_mul(a, b, conj_b=False, out=None):
     check(lib.pxa_complex_mul(dtcode(a), a.numel() // 2, b.numel() // 2, ptr(a), ptr(b), int(bool(conj_b)), ptr(out),
                               stream()), "pxa_complex_mul")
     return out
+
+
+_tuning_from_env()

@@ -91,7 +91,7 @@ __device__ inline T tv_weight(T n2, T lam, T mu, T inv_mu) {
 template <>
 __device__ inline float tv_weight<float>(float n2, float lam, float mu, float inv_mu) {
   const float r = __builtin_amdgcn_rsqf(n2);  // 1/|v| (inf at 0), 1 ulp
-  return lam * (r < inv_mu ? r : inv_mu);
+  return lam * __builtin_fminf(r, inv_mu);      // one v_min_f32 (r is never NaN: n2 >= 0)
 }
 
 // ---- phase 0 of the tile kernel: yk = (x - x_prev) * a + x on the A window, zero outside the image.

@@ -182,11 +182,12 @@ class Stencil(pxa.SquareOp):
     TILE_MAX_EXTENT, TILE_MAX_TAPS = 65, 2048  # the tiled kernel's envelope (csrc/stencil.hip launch_nd_tile)
 
     @classmethod
-    def _fft_min_taps(cls, K):
-        if cls.FFT_MIN_TAPS is not None:
-            return cls.FFT_MIN_TAPS
+    def _default_fft_min_taps(cls, K):
         tiled = max(K) <= cls.TILE_MAX_EXTENT and int(np.prod(K)) <= cls.TILE_MAX_TAPS
         return 1280 if (len(K) == 2 and tiled) else 256
+
+    def _fft_min_taps(self, K):
+        return self.FFT_MIN_TAPS if self.FFT_MIN_TAPS is not None else self._default_fft_min_taps(K)
 
     @staticmethod
     def _smooth(n):

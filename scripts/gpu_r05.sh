@@ -39,6 +39,28 @@ if [ "$S" = "new" ]; then
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
   step bench 900 python bench.py --steps 20 --warmup 5
 fi
+if [ "$S" = "a" ]; then
+  step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_long_trajectories.py tests/test_gpu_small_weights.py -k "pgd or c2 or c5"
+  step drvnew 120 $DRV
+  PXA_TUNE=0=1 step drvold 120 $DRV
+  step drvnew2 120 $DRV
+  PXA_TUNE=0=1 step drvold2 120 $DRV
+  step c5new 300 python3 bench.py --only c5
+  PXA_TUNE=0=1 step c5old 300 python3 bench.py --only c5
+  step c4096new 300 python3 bench.py --only c2_4096
+  PXA_TUNE=0=1 step c4096old 300 python3 bench.py --only c2_4096
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+  step newtests 900 $PT -m gpu tests/test_gpu_c3_fullsize.py tests/test_gpu_fft.py tests/test_gpu_stencil_fft.py \
+       tests/test_gpu_dense_normal.py tests/test_gpu_solver_engine.py
+fi
+if [ "$S" = "b" ]; then
+  step newtests 900 $PT -m gpu tests/test_gpu_c3_fullsize.py tests/test_gpu_fft.py tests/test_gpu_stencil_fft.py \
+       tests/test_gpu_dense_normal.py tests/test_gpu_solver_engine.py tests/test_gpu_pgd_variants.py
+  step drv1 120 $DRV
+  step drv2 120 $DRV
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+  step bench 900 python bench.py --steps 20 --warmup 5
+fi
 if [ "$S" = "pgd" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py -k "pgd or c2 or c5 or smoke or trajectory"
   step drv1 120 $DRV

@@ -575,11 +575,11 @@ def test_stencil_fft_threshold_follows_tile_envelope():
     (both extents <= 65, <= 2048 taps); wider 2-D boxes (e.g. 5 x 101) keep 256, as do 3-D kernels."""
     from pyxu_amd.operator.linop.stencil import Stencil
 
-    assert Stencil._fft_min_taps((31, 31)) == 1280
-    assert Stencil._fft_min_taps((65, 19)) == 1280
-    assert Stencil._fft_min_taps((5, 101)) == 256  # 505 taps: FFT, not the generic direct kernel
-    assert Stencil._fft_min_taps((45, 46)) == 256  # 2070 taps: beyond the tap table
-    assert Stencil._fft_min_taps((9, 9, 9)) == 256
+    assert Stencil._default_fft_min_taps((31, 31)) == 1280
+    assert Stencil._default_fft_min_taps((65, 19)) == 1280
+    assert Stencil._default_fft_min_taps((5, 101)) == 256  # 505 taps: FFT, not the generic direct kernel
+    assert Stencil._default_fft_min_taps((45, 46)) == 256  # 2070 taps: beyond the tap table
+    assert Stencil._default_fft_min_taps((9, 9, 9)) == 256
 
 
 def test_profile_hooks_wrap_m_step(monkeypatch):
