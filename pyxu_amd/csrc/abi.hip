@@ -34,6 +34,28 @@ int pxa_tuning(int key, int value) {
 
 }  // extern "C"
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 namespace pxa {
 int tuning(int key) { return (key >= 0 && key < PXA_TUNE_COUNT) ? g_tuning[key] : 0; }
+
+int resident_grid(const void* kernel, int threads, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, int, size_t>, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const auto key = std::make_tuple(kernel, dev, threads, lds);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int cus = 0, per = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, lds);
+  int g = cus * (per > 0 ? per : 1) / 8 * 8;
+  if (g < 8) g = 8;
+  cache[key] = g;
+  return g;
+}
 }  // namespace pxa

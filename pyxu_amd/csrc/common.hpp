@@ -43,6 +43,11 @@ struct Vec4<double> {
 // Current value of a pxa_tuning() knob (abi.hip).
 int tuning(int key);
 
+// Workgroups of `kernel` resident on the current device at once (occupancy x CUs), rounded down to a multiple
+// of 8 so that workgroup w of a persistent grid stays on XCD w % 8 for every unit it takes (>= 8).  Cached per
+// (kernel, device, threads, LDS).
+int resident_grid(const void* kernel, int threads, size_t lds);
+
 // Elements per 16-byte vector.
 template <typename T>
 constexpr int kVecN = 16 / sizeof(T);

@@ -639,7 +639,19 @@ __global__ void __launch_bounds__(TH, 4) fft_lds_kernel(FftPlan p, const Cx<T>* 
       for (int k = 0; k < PER; ++k) buf[slot(k)] = Cx<T>{vr[k], vi[k]};
     } else {
 #pragma unroll
-      for (int k = 0; k < PER; ++k) cx_buf_st<T>(buf[slot(k)], rs, voff, k * sstep);
+      // 16-B stores (fp64) take their whole offset in voffset, soffset = 0.  A buffer store of more than 8
+      // bytes reads its data VGPRs after it issues; LLVM's hazard recognizer inserts the wait state before a
+      // VALU write of those VGPRs only when soffset is not a register (GCNHazardRecognizer::createsVALUHazard),
+      // but on gfx950 the hazard exists with an SGPR soffset too: the k-th store (soffset k * sstep in an SGPR)
+      // was followed at once by `v_add_u32 v0, ...` (the next LDS address) into its data register v0, and now
+      // and then the low dword of an fp64 result was that address (round-4 / r05b failure of
+      // test_fft_vs_numpy[(2048, 2048)-(0, 1)-float64-True]: 16 values in one row, low dwords 0xd940..0xdc30,
+      // high dwords exact; tests/test_gpu_fft.py::test_fft_f64_store_hazard_pattern).  8-B stores (fp32) have
+      // no such hazard and keep the SGPR offset.
+      for (int k = 0; k < PER; ++k) {
+        if constexpr (sizeof(Cx<T>) > 8) cx_buf_st<T>(buf[slot(k)], rs, voff + k * sstep, 0);
+        else cx_buf_st<T>(buf[slot(k)], rs, voff, k * sstep);
+      }
     }
   };
   auto run_lines = [&](auto out, bool lf, auto generic) {

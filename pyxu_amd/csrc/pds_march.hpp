@@ -25,11 +25,12 @@ struct PdsD {
   T sigma, lam, rho, omr;
 };
 
+// One work unit of kernel D: in-plane block `blk` (kAThreads * NP consecutive positions) of axis-0 segment `segi`
+// of volume `s`, marched over the segment's planes (+ the G0 halo planes).
 template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT>
-__global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T* __restrict__ w,
-                                                              const T* __restrict__ z, const T* __restrict__ src,
-                                                              T* __restrict__ zo, T* __restrict__ ao,
-                                                              T* __restrict__ q) {
+__device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict__ w, const T* __restrict__ z,
+                                           const T* __restrict__ src, T* __restrict__ zo, T* __restrict__ ao,
+                                           T* __restrict__ q, unsigned blk, int segi, int64_t s) {
   constexpr int RING = 2 * R0 + 1;
   // kernel arguments copied to registers (the lambdas capture by reference; see pds_axis0_kernel)
   const PdsGeom<T> g = p.a.g;
@@ -41,9 +42,8 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
   for (int t = 0; t < RING; ++t) k0[t] = p.a.k0[t];
   const int n0 = g.n0, n1 = g.n1, n2 = g.n2;
   const int64_t M = (int64_t)n1 * n2;
-  const int64_t j0 = ((int64_t)xcd_tile(blockIdx.x, gridDim.x) * kAThreads + threadIdx.x) * NP;
+  const int64_t j0 = ((int64_t)blk * kAThreads + threadIdx.x) * NP;
   if (j0 >= M) return;  // no barriers below
-  const int64_t s = blockIdx.z;
   const int64_t N = M * n0;
   const int row = (int)(j0 / n2), col = (int)(j0 - (int64_t)row * n2);
   const T* ws = w + s * N + j0;
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
   T* aw = ao + s * N + j0;
   T* qw = q + s * N + j0;
   const int seg = p.a.seg;
-  const int pb = blockIdx.y * seg;
+  const int pb = segi * seg;
   const int pe = pb + seg < n0 ? pb + seg : n0;
   const int a_first = 3 - g.D;
   const bool row_nb = row + 1 < n1, col_nb = col + NP < n2;
@@ -309,6 +309,27 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
   }
 }
 
+// Persistent over the work units (round 5): the grid is the resident capacity (a multiple of 8) and workgroup
+// w takes units w, w + G, w + 2 G, ...; units are numbered (volume, segment, in-plane block) with the block
+// fastest, and the block index is XCD-banded (tile2d::xcd_tile).  So at any time the resident workgroups of an
+// XCD march a contiguous band of rows of one segment, all started together: the row - 1 / row + 1 neighbours
+// of w and z that a workgroup reads are the rows its band neighbours read at about the same plane, i.e. L2
+// hits.  With one workgroup per unit (round 4, PXA_TUNE_PDS_MARCH bit 1) a workgroup dispatched when another
+// finished starts ~4 / (resident per XCD) of a march after its row neighbour -- ~10 planes at 1024^3, more than
+// the ~4.5 planes of the XCD's working set that its L2 holds -- and re-fetched half of those rows from HBM.
+template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT>
+__global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T* __restrict__ w,
+                                                              const T* __restrict__ z, const T* __restrict__ src,
+                                                              T* __restrict__ zo, T* __restrict__ ao,
+                                                              T* __restrict__ q, unsigned blocks, unsigned nseg,
+                                                              unsigned units) {
+  for (unsigned u = blockIdx.x; u < units; u += gridDim.x) {
+    const unsigned r = u % blocks, rest = u / blocks;
+    march_unit<T, R0, NP, PD3O, ISO, DUAL, NT>(p, w, z, src, zo, ao, q, xcd_tile(r, blocks), (int)(rest % nseg),
+                                               (int64_t)(rest / nseg));
+  }
+}
+
 // ------------------------------------------------------------------ host side
 template <typename T, int R0, bool PD3O, bool ISO, bool DUAL>
 int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, const void* z, const void* src, void* zo,
@@ -319,13 +340,17 @@ int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, cons
   // read-once / write-once streams (src, z_out, x_out or K^T z_out, Q) are non-temporal, so that the re-read
   // neighbour rows of w and z stay in L2 (C3 1024^3, r04b: fetch 29 -> 25.7 B/voxel, PD3O step 15.3 -> 14.4 ms)
   const int64_t blocks = (M + (int64_t)kAThreads * np - 1) / ((int64_t)kAThreads * np);
-  dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pd.a.g.stack);
-  if (np == 2)
-    hipLaunchKernelGGL((pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL, true>), grid, dim3(kAThreads), 0, st, pd,
-                       (const T*)w, (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
-  else
-    hipLaunchKernelGGL((pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true>), grid, dim3(kAThreads), 0, st, pd,
-                       (const T*)w, (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q);
+  const int64_t units = blocks * nseg * pd.a.g.stack;
+  PXA_CHECK_ARG(units <= 0x7fffffff);
+  auto kern = np == 2 ? pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL, true> : pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true>;
+  // grid: the resident capacity (PXA_TUNE_PDS_MARCH bit 1: one workgroup per unit, the round-4 launch)
+  unsigned grid = (unsigned)units;
+  if (!(tuning(PXA_TUNE_PDS_MARCH) & 2)) {
+    const unsigned cap = (unsigned)resident_grid((const void*)kern, kAThreads, 0);
+    if (grid > cap) grid = cap;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kAThreads), 0, st, pd, (const T*)w, (const T*)z, (const T*)src, (T*)zo,
+                     (T*)ao, (T*)q, (unsigned)blocks, (unsigned)nseg, (unsigned)units);
   return last_launch_status();
 }
 

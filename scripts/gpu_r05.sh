@@ -61,6 +61,17 @@ if [ "$S" = "b" ]; then
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
   step bench 900 python bench.py --steps 20 --warmup 5
 fi
+if [ "$S" = "c" ]; then
+  step tests 900 $PT -m gpu tests/test_gpu_fft.py tests/test_gpu_c3_fullsize.py tests/test_gpu_pds_fused.py tests/test_gpu_long_trajectories.py tests/test_gpu_bench_shapes.py
+  step c3new 300 python3 bench.py --only c3
+  PXA_TUNE=7=2 step c3old 300 python3 bench.py --only c3
+  step c3new2 300 python3 bench.py --only c3
+  B3="python3 bench.py --only c3 --c3-steps 3"
+  step fetchc3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetchc3 -o run --output-format csv -- $B3
+  step writec3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writec3 -o run --output-format csv -- $B3
+  python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, true, false, true, true>" pds_march_kernel_pd3o@1024^3 $P/traffic_c3.json $T || true
+  python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, false, false, true, true>" pds_march_kernel_cv@1024^3 $P/traffic_c3.json $T || true
+fi
 if [ "$S" = "pgd" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py -k "pgd or c2 or c5 or smoke or trajectory"
   step drv1 120 $DRV
