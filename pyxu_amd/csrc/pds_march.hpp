@@ -309,14 +309,14 @@ __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict
   }
 }
 
-// Persistent over the work units (round 5): the grid is the resident capacity (a multiple of 8) and workgroup
-// w takes units w, w + G, w + 2 G, ...; units are numbered (volume, segment, in-plane block) with the block
-// fastest, and the block index is XCD-banded (tile2d::xcd_tile).  So at any time the resident workgroups of an
-// XCD march a contiguous band of rows of one segment, all started together: the row - 1 / row + 1 neighbours
-// of w and z that a workgroup reads are the rows its band neighbours read at about the same plane, i.e. L2
-// hits.  With one workgroup per unit (round 4, PXA_TUNE_PDS_MARCH bit 1) a workgroup dispatched when another
-// finished starts ~4 / (resident per XCD) of a march after its row neighbour -- ~10 planes at 1024^3, more than
-// the ~4.5 planes of the XCD's working set that its L2 holds -- and re-fetched half of those rows from HBM.
+// Grid over the work units: one workgroup per unit by default; PXA_TUNE_PDS_MARCH bit 1 makes it persistent
+// (the resident capacity, a multiple of 8; workgroup w takes units w, w + G, ...).  Units are numbered (volume,
+// segment, in-plane block) with the block fastest and the block index XCD-banded (tile2d::xcd_tile), so in the
+// persistent form the resident workgroups of an XCD march a contiguous band of rows of one segment, started
+// together, and read each other's row - 1 / row + 1 neighbours of w and z from L2.  Measured at 1024^3 (round 5,
+// r05c): HBM fetch 25.7 -> 23.8 GiB per launch (1.29 -> 1.19 x compulsory), but kernel D 8.8 -> 11.0 ms (PD3O)
+// and 10.2 -> 12.0 ms (Condat-Vu): the marches running in lockstep cost more than the re-fetched rows, so the
+// default stays one workgroup per unit, dispatched as slots free up.
 template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT>
 __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T* __restrict__ w,
                                                               const T* __restrict__ z, const T* __restrict__ src,
@@ -343,9 +343,9 @@ int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, cons
   const int64_t units = blocks * nseg * pd.a.g.stack;
   PXA_CHECK_ARG(units <= 0x7fffffff);
   auto kern = np == 2 ? pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL, true> : pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true>;
-  // grid: the resident capacity (PXA_TUNE_PDS_MARCH bit 1: one workgroup per unit, the round-4 launch)
+  // grid: one workgroup per unit (PXA_TUNE_PDS_MARCH bit 1: the resident capacity, persistent; see above)
   unsigned grid = (unsigned)units;
-  if (!(tuning(PXA_TUNE_PDS_MARCH) & 2)) {
+  if (tuning(PXA_TUNE_PDS_MARCH) & 2) {
     const unsigned cap = (unsigned)resident_grid((const void*)kern, kAThreads, 0);
     if (grid > cap) grid = cap;
   }
