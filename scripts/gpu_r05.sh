@@ -72,6 +72,13 @@ if [ "$S" = "c" ]; then
   python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, true, false, true, true>" pds_march_kernel_pd3o@1024^3 $P/traffic_c3.json $T || true
   python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "pds_march_kernel<float, 6, 1, false, false, true, true>" pds_march_kernel_cv@1024^3 $P/traffic_c3.json $T || true
 fi
+if [ "$S" = "d" ]; then
+  step pdstests 600 $PT -m gpu tests/test_gpu_pds_fused.py -k "persistent or two_positions or lookahead_matches"
+  step sr1time 300 python3 scripts/host_time_pgd_sr1.py
+  step sr1prof 300 python3 scripts/prof_sr1.py
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+  pmc_pgd
+fi
 if [ "$S" = "pgd" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py -k "pgd or c2 or c5 or smoke or trajectory"
   step drv1 120 $DRV

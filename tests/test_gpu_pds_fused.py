@@ -285,3 +285,20 @@ def test_tv_dual_update_vs_oracle(dt, h_kind, sh, relax):
     zt = orc.fenchel_prox(hp, zin, sigma)
     ref = (d(1 - rho) * z + d(rho) * zt) if relax == 0 else (d(rho) * zt + d(1 - rho) * z)
     assert rel_err(out, ref) <= TOL[dt], rel_err(out, ref)
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+def test_pds_lookahead_persistent_grid_bit_exact(algo):
+    """Kernel D on a persistent grid (PXA_TUNE_PDS_MARCH bit 1: workgroups loop over the (segment, block) units)
+    gives the one-workgroup-per-unit launch's bits.  512 in-plane blocks x the automatic segments: more units
+    than resident workgroups, so the workgroups do loop."""
+    case = ((40, 256, 512), 2.0, "iso", "pos", np.float32, False)
+    x0 = np.random.default_rng(8).uniform(0, 1, int(np.prod(case[0]))).astype(np.float32)
+    a = _run(algo, case, 4, True, x0)
+    prev = _dev.tuning(_dev.TUNE_PDS_MARCH, 2)
+    try:
+        b = _run(algo, case, 4, True, x0)
+    finally:
+        _dev.tuning(_dev.TUNE_PDS_MARCH, prev)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
