@@ -436,6 +436,23 @@ int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int6
  * launched the tile kernel (0 before).
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
+/* Prepared form of pxa_pgd_tv2d_step for a solver's iterations (replaces the same call per PGD.m_step,
+ * opt/solver/pgd.py:173-191, and the RelError fold of its stop checks, opt/stop.py:353-382):
+ * pxa_pgd_tv2d_plan() folds the taps and builds the iteration-invariant parameters once (arguments as
+ * pxa_pgd_tv2d_step's, prox_w excluded) into an opaque handle; pxa_pgd_tv2d_plan_step() runs one iteration
+ * with the per-step a, tau, prox_w and arrays (as pxa_pgd_tv2d_step).  With rel_values != NULL (then partials
+ * and rel_flags too) the workgroup that finishes last also folds the partials into rel_values[(2, rows)],
+ * rows = stack / y_images, exactly as pxa_tile_partials_fold does (same bits), and sets rel_flags[q] = seq
+ * (2 * rows words; pxa_host_alloc memory) after its value, system-wide: a stop check then needs no fold
+ * launch.  A plan holds a device counter: launches of one plan must not run concurrently (one stream).
+ * pxa_pgd_tv2d_plan_free() releases it. */
+int pxa_pgd_tv2d_plan(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
+                      const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
+                      double lam, double mu, int prox, void** plan);
+int pxa_pgd_tv2d_plan_step(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
+                           const void* hty, void* x_new, double* partials, const void* x_ref, double* rel_values,
+                           uint32_t* rel_flags, uint32_t seq, void* stream);
+int pxa_pgd_tv2d_plan_free(void* plan);
 int pxa_pgd_tv2d_last_kernel(void);
 /* Diagnostics: s_memtime stamps of the tile kernel's last launch under PXA_TUNE_PGD_DIAG bit 5
  * (workgroups 0, 1, grid/2, grid-1; waves 0..3; 8 phase points; n <= 128 words). */

@@ -935,6 +935,42 @@ def pgd_tv2d_step(x, x_prev, hty, x_new, stack, y_images, n0, n1, taps0, taps1, 
     return x_new
 
 
+class PgdPlan:
+    """pxa_pgd_tv2d_plan: the fused PGD step's iteration-invariant parameters, prepared once per solve, and the
+    device counter of its last-workgroup RelError fold.  ``step`` is one iteration (pxa_pgd_tv2d_plan_step) with
+    the few per-step arguments, so a PGD step costs one short ctypes call."""
+
+    def __init__(self, like, stack, y_images, n0, n1, taps0, taps1, h0, h1, lam, mu, prox):
+        o0, k0 = taps0
+        o1, k1 = taps1
+        h = ct.c_void_p()
+        check(lib.pxa_pgd_tv2d_plan(dtcode(like), int(stack), int(y_images), int(n0), int(n1), len(o0), i32_array(o0),
+                                    f64_array(k0), len(o1), i32_array(o1), f64_array(k1), float(h0), float(h1),
+                                    float(lam), float(mu), int(prox), ct.byref(h)), "pxa_pgd_tv2d_plan")
+        self._h = h.value
+        self._fn = lib.pxa_pgd_tv2d_plan_step
+        self._free = lib.pxa_pgd_tv2d_plan_free
+
+    def step(self, x, x_prev, hty, x_new, a, tau, prox_w, partials=None, x_ref=None, sink=None, seq=0):
+        """One iteration; with `sink` (a HostFlagBuffer of (2, rows) values) the launch also folds its partials
+        there under publication `seq`."""
+        ev = _TIMER.begin() if _TIMER is not None else None  # measurement hook (bench.py), normally None
+        r = self._fn(self._h, float(a), float(tau), float(prox_w), x.data_ptr(), x_prev.data_ptr(), hty.data_ptr(),
+                     x_new.data_ptr(), partials.data_ptr() if partials is not None else None,
+                     x_ref.data_ptr() if x_ref is not None else None, sink.vptr if sink is not None else None,
+                     sink.fptr if sink is not None else None, int(seq), stream())
+        if r:
+            check(r, "pxa_pgd_tv2d_plan_step")
+        if ev is not None:
+            _TIMER.end(ev)
+        return x_new
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._free(self._h)
+            self._h = None
+
+
 _PDS_W = 17  # per-axis tap slots of pxa_pds_step (2 * 8 + 1)
 
 

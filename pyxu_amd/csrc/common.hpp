@@ -52,6 +52,27 @@ int resident_grid(const void* kernel, int threads, size_t lds);
 template <typename T>
 constexpr int kVecN = 16 / sizeof(T);
 
+// One RelError statistic of the fused PGD step's per-(tile, wavefront) partials, by a whole kBlock-thread
+// workgroup: thread t sums pr[2 k] for k = t, t + kBlock, ... in order, the wavefront folds by a shuffle-down
+// tree, then thread 0 adds the kBlock / 64 wave results in order (`red`: kBlock / 64 doubles of LDS).  The
+// result is valid in thread 0.  Shared by pxa_tile_partials_fold (reduce.hip) and the tile kernel's own
+// last-workgroup fold (pgd_tv2d.hip), so both give the same bits.
+__device__ inline double fold_tile_stat(const double* __restrict__ pr, int64_t per_row, double* red) {
+  double acc = 0.0;
+#pragma unroll 8
+  for (int64_t k = threadIdx.x; k < per_row; k += kBlock) acc += pr[2 * k];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = acc;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < kBlock / kWave; ++i) t += red[i];
+  __syncthreads();  // red may be reused by the next statistic
+  return t;
+}
+
 }  // namespace pxa
 
 // dtype dispatch: `code` is PXA_F32 / PXA_F64.

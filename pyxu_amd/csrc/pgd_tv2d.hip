@@ -65,6 +65,15 @@ struct PgdParams {
   int stagger;  // PXA_TUNE_PGD_STAGGER (A/B probe: delayed start of some first-round workgroups)
   unsigned round1;  // workgroups resident at once (4 per CU)
   const T* xref;    // RelError partials relative to this iterate (nullptr: relative to x)
+  // last-workgroup fold of the RelError partials (pxa_pgd_tv2d_plan_step with rel_values): the workgroup
+  // that finishes last folds them as pxa_tile_partials_fold does (same bits) into fold_vals (host-mapped,
+  // (2, fold_rows)) and sets fold_flags[q] = fold_seq; `counter` (device, 0 between launches) counts the
+  // finished workgroups.  fold_vals == nullptr: no fold.
+  double* fold_vals;
+  unsigned* fold_flags;
+  unsigned* counter;
+  unsigned fold_seq;
+  int64_t fold_rows, fold_per_row;
 };
 
 // Round 3 also measured a variant that carried yk as solver state (the epilogue writing the next
@@ -518,6 +527,35 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   }
 }
 
+// The RelError statistics of this launch, folded by the workgroup that finishes last (saves the fold launch
+// of a stop check: ~3.4 us of device time plus a launch gap per step at stop_rate 1).  Every wavefront's lane
+// 0 has written its (tile, wave) partials; a device-scope release fence, then one atomic count per workgroup;
+// the last one acquires, folds each (statistic, row) with fold_tile_stat in the order of
+// pxa_tile_partials_fold, stores the values and the completion flags (system scope, as that kernel does) and
+// resets the counter for the next launch.
+template <typename T>
+__device__ inline void tail_fold(const PgdParams<T>& p, const double* __restrict__ partials) {
+  __shared__ double red[kThreads / 64];
+  __shared__ unsigned last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(p.counter, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (int64_t q = 0; q < 2 * p.fold_rows; ++q) {
+    const int64_t stat = q / p.fold_rows, r = q - stat * p.fold_rows;
+    const double t = fold_tile_stat(partials + 2 * r * p.fold_per_row + stat, p.fold_per_row, red);
+    if (threadIdx.x == 0) p.fold_vals[q] = t;
+  }
+  if (threadIdx.x == 0) {
+    *p.counter = 0u;
+    __threadfence_system();
+    for (int64_t q = 0; q < 2 * p.fold_rows; ++q)
+      __hip_atomic_store(p.fold_flags + q, p.fold_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <typename T, int R>
 __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
                                                             const T* __restrict__ xp, const T* __restrict__ b,
@@ -558,6 +596,7 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
     pgd_tile<T, R, false>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials, xrs);
   else
     pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials, xrs);
+  if (p.fold_vals != nullptr) tail_fold<T>(p, partials);
 }
 
 template <typename T, int R>
@@ -579,22 +618,20 @@ int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void*
 
 thread_local int g_last_pgd_kernel = 0;  // pxa_pgd_tv2d_last_kernel
 
+// Iteration-invariant parameters (taps folded per offset, G = k (*) k, geometry, prox kind); `R` the blur reach.
 template <typename T>
-int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
-              const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1, double lam,
-              double mu, double a, double tau, int prox, double prox_w, const void* x, const void* x_prev,
-              const void* hty, void* x_new, double* partials, const void* x_ref, hipStream_t s) {
+int pgd_params(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
+               const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1, double lam,
+               double mu, int prox, PgdParams<T>& p, int& R) {
   PXA_CHECK_ARG(stack >= 1 && n0 >= 1 && n1 >= 1 && y_images >= 1 && stack % y_images == 0);
   PXA_CHECK_ARG(n0 <= 0x7fffffff && n1 <= 0x7fffffff);
-  PXA_CHECK_ARG(x && x_prev && hty && x_new);
-  PXA_CHECK_ARG(x_new != x && x_new != x_prev && x_new != x_ref);
   PXA_CHECK_ARG(prox >= 0 && prox <= 2);
   PXA_CHECK_ARG(nt0 >= 1 && nt1 >= 1 && off0 && off1 && coef0 && coef1);
-  int R = 1;  // TV needs a 1-pixel halo even for a 1-tap blur
+  R = 1;  // TV needs a 1-pixel halo even for a 1-tap blur
   for (int q = 0; q < nt0; ++q) R = abs(off0[q]) > R ? abs(off0[q]) : R;
   for (int q = 0; q < nt1; ++q) R = abs(off1[q]) > R ? abs(off1[q]) : R;
   if (R > kMaxR) return PXA_ERR_UNSUPPORTED;
-  PgdParams<T> p;
+  p = PgdParams<T>{};
   p.stack = stack;
   p.y_images = y_images;
   p.n0 = (int)n0;
@@ -630,18 +667,37 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   p.lam = (T)lam;
   p.mu = (T)mu;
   p.inv_mu = (T)(1.0 / mu);
+  p.tv = lam != 0.0;
+  p.prox = prox;
+  p.round1 = 4u * 256u;
+  return PXA_OK;
+}
+
+// One launch from prepared parameters: the per-step scalars and arrays, then the kernel of reach R.
+template <typename T>
+int pgd_run(PgdParams<T> p, int R, double a, double tau, double prox_w, const void* x, const void* x_prev,
+            const void* hty, void* x_new, double* partials, const void* x_ref, double* rel_values, uint32_t* rel_flags,
+            uint32_t seq, unsigned* counter, hipStream_t s) {
+  PXA_CHECK_ARG(x && x_prev && hty && x_new);
+  PXA_CHECK_ARG(x_new != x && x_new != x_prev && x_new != x_ref);
+  PXA_CHECK_ARG(rel_values == nullptr || (partials != nullptr && rel_flags != nullptr && counter != nullptr));
   p.a = (T)a;
   p.tau = (T)tau;
   p.pw = (T)prox_w;
   constexpr int V = kVecN<T>;
-  p.vec_ok = (n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new) &&
+  p.vec_ok = (p.n1 % V == 0) && aligned16(x) && aligned16(x_prev) && aligned16(hty) && aligned16(x_new) &&
              (x_ref == nullptr || aligned16(x_ref));
   p.xref = (partials != nullptr && x_ref != nullptr && x_ref != x) ? (const T*)x_ref : nullptr;
-  p.tv = lam != 0.0;
-  p.prox = prox;
   p.diag = kProbes ? tuning(PXA_TUNE_PGD_DIAG) : 0;
   p.stagger = kProbes ? tuning(PXA_TUNE_PGD_STAGGER) : 0;
-  p.round1 = 4u * 256u;
+  p.fold_vals = rel_values;
+  p.fold_flags = (unsigned*)rel_flags;
+  p.fold_seq = (unsigned)seq;
+  p.counter = counter;
+  // rows of the RelError statistics = rows of the solver state: y_images images each (batch-as-axis); the
+  // slots of one image, hence of one row, are contiguous
+  p.fold_rows = p.stack / p.y_images;
+  p.fold_per_row = (int64_t)p.ntiles * (kThreads / 64) / p.fold_rows;
   int st;
   switch (R) {
     case 1: st = launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s); break;
@@ -656,6 +712,28 @@ int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, 
   if (st == PXA_OK) g_last_pgd_kernel = 1;
   return st;
 }
+
+template <typename T>
+int pgd_entry(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
+              const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1, double lam,
+              double mu, double a, double tau, int prox, double prox_w, const void* x, const void* x_prev,
+              const void* hty, void* x_new, double* partials, const void* x_ref, hipStream_t s) {
+  PgdParams<T> p;
+  int R = 1;
+  const int e = pgd_params<T>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, prox, p, R);
+  if (e != PXA_OK) return e;
+  return pgd_run<T>(p, R, a, tau, prox_w, x, x_prev, hty, x_new, partials, x_ref, nullptr, nullptr, 0, nullptr, s);
+}
+
+// pxa_pgd_tv2d_plan: the prepared parameters of one problem (both precisions' storage, one used) and the
+// device counter of the last-workgroup fold
+struct PgdPlan {
+  int dtype;
+  int R;
+  PgdParams<float> pf;
+  PgdParams<double> pd;
+  unsigned* counter;
+};
 
 }  // namespace
 }  // namespace pxa
@@ -677,6 +755,50 @@ int pxa_pgd_tile_trace(uint64_t* host_out, int n) {
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1) {
   int64_t t = stack * ((n0 + TY - 1) / TY) * ((n1 + TX - 1) / TX) * kPartWaves;
   return (int)t;
+}
+
+int pxa_pgd_tv2d_plan(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,
+                      const double* coef0, int nt1, const int32_t* off1, const double* coef1, double h0, double h1,
+                      double lam, double mu, int prox, void** plan) {
+  PXA_CHECK_ARG(plan != nullptr);
+  *plan = nullptr;
+  PgdPlan* pl = new PgdPlan();
+  pl->dtype = dtype;
+  int e = PXA_ERR_DTYPE;
+  if (dtype == PXA_F32)
+    e = pgd_params<float>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, prox, pl->pf, pl->R);
+  else if (dtype == PXA_F64)
+    e = pgd_params<double>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, prox, pl->pd, pl->R);
+  if (e == PXA_OK) {
+    e = (int)hipMalloc((void**)&pl->counter, sizeof(unsigned));
+    if (e == PXA_OK) e = (int)hipMemset(pl->counter, 0, sizeof(unsigned));
+  }
+  if (e != PXA_OK) {
+    delete pl;
+    return e;
+  }
+  *plan = pl;
+  return PXA_OK;
+}
+
+int pxa_pgd_tv2d_plan_step(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
+                           const void* hty, void* x_new, double* partials, const void* x_ref, double* rel_values,
+                           uint32_t* rel_flags, uint32_t seq, void* stream) {
+  PXA_CHECK_ARG(plan != nullptr);
+  const PgdPlan* pl = (const PgdPlan*)plan;
+  if (pl->dtype == PXA_F32)
+    return pgd_run<float>(pl->pf, pl->R, a, tau, prox_w, x, x_prev, hty, x_new, partials, x_ref, rel_values, rel_flags,
+                          seq, pl->counter, as_stream(stream));
+  return pgd_run<double>(pl->pd, pl->R, a, tau, prox_w, x, x_prev, hty, x_new, partials, x_ref, rel_values, rel_flags, seq,
+                         pl->counter, as_stream(stream));
+}
+
+int pxa_pgd_tv2d_plan_free(void* plan) {
+  if (plan == nullptr) return PXA_OK;
+  PgdPlan* pl = (PgdPlan*)plan;
+  if (pl->counter) (void)hipFree(pl->counter);
+  delete pl;
+  return PXA_OK;
 }
 
 int pxa_pgd_tv2d_step(int dtype, int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0, const int32_t* off0,

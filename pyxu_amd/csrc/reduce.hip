@@ -177,17 +177,8 @@ __global__ void __launch_bounds__(kBlock) tile_partials_fold_kernel(int64_t rows
   __shared__ double red[kBlock / kWave];
   const int64_t q = blockIdx.x;  // q = stat * rows + row
   const int64_t stat = q / rows, r = q - stat * rows;
-  const double* pr = part + 2 * r * per_row + stat;
-  double acc = 0.0;
-#pragma unroll 8
-  for (int64_t k = threadIdx.x; k < per_row; k += kBlock) acc += pr[2 * k];
-  acc = wave_reduce<PXA_RED_SUMSQ>(acc);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) red[w] = acc;
-  __syncthreads();
+  const double t = fold_tile_stat(part + 2 * r * per_row + stat, per_row, red);
   if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int i = 0; i < kBlock / kWave; ++i) t += red[i];
     out[q] = t;
     if (flags != nullptr) {  // completion flag of this statistic, ordered after its value system-wide
       __threadfence_system();

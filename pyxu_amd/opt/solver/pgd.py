@@ -93,8 +93,8 @@ class PGD(pxa.Solver):
             # the fused kernel evaluates H^T (H yk - y) as (H^T H) yk - H^T y: H^T y is iteration-invariant
             p["hty"] = _dev.copy(p["H"].adjoint(y))
             p["stack"] = p["rows"] * p["B"]
-            p["pre"] = _dev.pgd_tv2d_args(p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"], p["h1"],
-                                          p["lam"], p["mu"], p["prox"], p["prox_scale"])
+            p["plan"] = _dev.PgdPlan(x0, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"], p["h1"],
+                                     p["lam"], p["mu"], p["prox"])
             # per-tile RelError partials of the launch that precedes a stop check (pxa_tile_partials_fold)
             ntiles = int(_dev.lib.pxa_pgd_tv2d_partials_count(p["stack"], p["n0"], p["n1"]))
             p["parts"] = _dev.empty_f64((2 * ntiles,), x0)
@@ -151,11 +151,15 @@ class PGD(pxa.Solver):
             xref = self._x_check if want else None
             if xref is None:
                 xref = x
-            _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"],
-                               p["h0"], p["h1"], p["lam"], p["mu"], a, tau, p["prox"], tau * p["prox_scale"],
-                               partials=parts, pre=p["pre"], x_ref=None if xref is x else xref)
-            if want:  # (var, x_new, the x the statistics are relative to, partials, rows, tiles per row)
-                mst["__relerr__"] = ("x", out, xref, parts, p["rows"], p["tiles_per_row"])
+            # the stop criterion's host buffer for this launch's folded statistics, if it offered one
+            sink = mst.pop("__relerr_sink__", None) if want else None
+            sink = sink[1] if sink is not None and sink[0] == "x" else None
+            seq = sink.next_seq() if sink is not None else 0
+            p["plan"].step(x, xp, p["hty"], out, a, tau, tau * p["prox_scale"], partials=parts,
+                           x_ref=None if xref is x else xref, sink=sink, seq=seq)
+            if want:  # (var, x_new, the x the statistics are relative to, partials, rows, tiles per row, folded)
+                mst["__relerr__"] = ("x", out, xref, parts, p["rows"], p["tiles_per_row"],
+                                     (sink, seq) if sink is not None else None)
             else:
                 mst.pop("__relerr__", None)
             mst["x_prev"], mst["x"] = x, out

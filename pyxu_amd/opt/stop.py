@@ -331,11 +331,20 @@ class RelError(pxa.StoppingCriterion):
             # the step's own per-tile partials, folded straight into coherent host memory with a completion flag
             # per statistic: no pass over x / x_prev, no copy, no stream event.  x is kept (a reference) now, so
             # that the solver's next step, enqueued before the decision is read, may recycle the previous
-            # iterate's buffer
-            fb = getattr(self, "_flag_buf", None)
-            if fb is None or fb.rows != rows:
-                fb = self._flag_buf = _dev.HostFlagBuffer(rows)
-            seq = fb.fold(h[3], h[5])
+            # iterate's buffer.  Two buffers, alternately: this check reads one while the launch behind it
+            # (enqueued before the decision) may fold into the other -- the solver finds that one as the
+            # "__relerr_sink__" of its state, and then the fold is part of its launch (h[6] = (buffer, seq))
+            bufs = getattr(self, "_flag_bufs", None)
+            if bufs is None or bufs[0].rows != rows:
+                bufs = self._flag_bufs = (_dev.HostFlagBuffer(rows), _dev.HostFlagBuffer(rows))
+            folded = h[6] if len(h) > 6 else None
+            if folded is not None and folded[0] in bufs:
+                fb, seq = folded
+            else:
+                fb = bufs[0]
+                seq = fb.fold(h[3], h[5])
+            if hasattr(state, "__setitem__"):
+                state["__relerr_sink__"] = (self._var, bufs[1] if fb is bufs[0] else bufs[0])
             self._x_prev = x
             shape = x.shape[:-1]
 

@@ -79,6 +79,14 @@ if [ "$S" = "d" ]; then
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
   pmc_pgd
 fi
+if [ "$S" = "e" ]; then
+  step tests 900 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_solver_engine.py tests/test_gpu_parity.py tests/test_gpu_bench_shapes.py tests/test_gpu_long_trajectories.py tests/test_gpu_small_weights.py tests/test_gpu_distributed.py
+  step sr1time 300 python3 scripts/host_time_pgd_sr1.py
+  step sr1prof 300 python3 scripts/prof_sr1.py
+  step drv1 120 $DRV
+  step drv2 120 $DRV
+  step bench 900 python bench.py --steps 20 --warmup 5
+fi
 if [ "$S" = "pgd" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py -k "pgd or c2 or c5 or smoke or trajectory"
   step drv1 120 $DRV

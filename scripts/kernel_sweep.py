@@ -37,7 +37,7 @@ def time_it(s, reps=100):
 
     def step():
         _dev.pgd_tv2d_step(x, xp, p["hty"], out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
-                           p["h1"], p["lam"], p["mu"], 0.5, s._mstate["tau"], p["prox"], 0.0, pre=p["pre"])
+                           p["h1"], p["lam"], p["mu"], 0.5, s._mstate["tau"], p["prox"], 0.0)
 
     for _ in range(5):
         step()

@@ -67,8 +67,7 @@ def _launch(s, x, xp, hty, a, parts=None):
     p, m = s._plan, s._mstate
     out = _dev.empty_like(x)
     _dev.pgd_tv2d_step(x, xp, hty, out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
-                       p["h1"], p["lam"], p["mu"], a, m["tau"], p["prox"], m["tau"] * p["prox_scale"], partials=parts,
-                       pre=p["pre"])
+                       p["h1"], p["lam"], p["mu"], a, m["tau"], p["prox"], m["tau"] * p["prox_scale"], partials=parts)
     assert int(lib.pxa_pgd_tv2d_last_kernel()) == 1
     return out
 
@@ -158,6 +157,35 @@ def test_fused_relerr_matches_separate_pass(stack, rows, stop_rate):
         v1, v2 = h1[k].astype(np.float64), h2[k].astype(np.float64)
         assert np.allclose(v1, v2, rtol=1e-6, atol=0), k
     assert c1 <= 1 and c2 >= len(h2) - 2
+
+
+@pytest.mark.parametrize("case", [((2048, 2048), 1, 1), ((128, 192), 6, 2), ((40, 36), 2, 2)],
+                         ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}")
+def test_in_kernel_fold_matches_fold_kernel(case):
+    """pxa_pgd_tv2d_plan_step with a RelError sink: the workgroup that finishes last folds the partials into the
+    host buffer with its completion flags -- the same bits as pxa_tile_partials_fold on the same partials, the
+    same x_new as a launch without the fold, and the device counter is reset for the next launch (two launches
+    in a row both publish)."""
+    sh, stack, y_images = case
+    s = _plan(sh, stack, y_images, 2.0, "pos")
+    m, p = s._mstate, s._plan
+    x, xp, hty = m["x"], m["x_prev"], p["hty"]
+    rows = stack // y_images
+    per_row = int(lib.pxa_pgd_tv2d_partials_count(p["stack"], p["n0"], p["n1"])) // rows
+    sink = _dev.HostFlagBuffer(rows)
+    for rep in range(2):
+        parts = _parts(s)
+        seq = sink.next_seq()
+        out = _dev.empty_like(x)
+        p["plan"].step(x, xp, hty, out, 0.37, m["tau"], m["tau"] * p["prox_scale"], partials=parts, sink=sink, seq=seq)
+        sink.wait(seq)
+        got = sink.values.copy()
+        ref = _dev.empty_f64((2, rows), x)
+        _dev.tile_partials_fold(parts, rows, per_row, ref)
+        plain = _launch(s, x, xp, hty, 0.37)
+        torch.cuda.synchronize()
+        assert np.array_equal(got, to_NUMPY(ref).reshape(-1)), rep
+        assert np.array_equal(to_NUMPY(out), to_NUMPY(plain)), rep
 
 
 def test_wide_blur_warns_and_runs_generic_path():
