@@ -6,6 +6,7 @@ scalars cross to the host — the single device->host sync of a stop check (stop
 """
 import datetime as dt
 import numbers
+import os
 
 import numpy as np
 
@@ -208,6 +209,9 @@ class AbsError(pxa.StoppingCriterion):
 
     # hook: combine a device row statistic across shards (identity on one process)
     _reduce = None
+    # offer the fused PGD step a host buffer to fold its statistics into (pxa_pgd_tv2d_plan_step's last-workgroup
+    # fold): off until its flag latency is understood (r05e: ~200 us per check against 3.4 us for the fold launch)
+    _offer_sink = os.environ.get("PXA_RELERR_SINK", "0") == "1"
 
     def info(self):
         if self._val.size == 1:
@@ -312,6 +316,9 @@ class RelError(pxa.StoppingCriterion):
 
     # hook: combine a device row statistic across shards (identity on one process)
     _reduce = None
+    # offer the fused PGD step a host buffer to fold its statistics into (pxa_pgd_tv2d_plan_step's last-workgroup
+    # fold): off until its flag latency is understood (r05e: ~200 us per check against 3.4 us for the fold launch)
+    _offer_sink = os.environ.get("PXA_RELERR_SINK", "0") == "1"
 
     def stop_async(self, state):
         """stop() in two phases: the statistics (written by the device into pinned host memory) and the
@@ -343,7 +350,7 @@ class RelError(pxa.StoppingCriterion):
             else:
                 fb = bufs[0]
                 seq = fb.fold(h[3], h[5])
-            if hasattr(state, "__setitem__"):
+            if self._offer_sink and hasattr(state, "__setitem__"):
                 state["__relerr_sink__"] = (self._var, bufs[1] if fb is bufs[0] else bufs[0])
             self._x_prev = x
             shape = x.shape[:-1]

@@ -87,6 +87,12 @@ if [ "$S" = "e" ]; then
   step drv2 120 $DRV
   step bench 900 python bench.py --steps 20 --warmup 5
 fi
+if [ "$S" = "f" ]; then
+  step foldlat 120 python3 scripts/fold_latency.py
+  step sr1time 300 python3 scripts/host_time_pgd_sr1.py
+  PXA_RELERR_SINK=1 step sr1time_sink 300 python3 scripts/host_time_pgd_sr1.py
+  step drv1 120 $DRV
+fi
 if [ "$S" = "pgd" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py -k "pgd or c2 or c5 or smoke or trajectory"
   step drv1 120 $DRV
