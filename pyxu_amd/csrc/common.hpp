@@ -57,10 +57,14 @@ constexpr int kVecN = 16 / sizeof(T);
 // tree, then thread 0 adds the kBlock / 64 wave results in order (`red`: kBlock / 64 doubles of LDS).  The
 // result is valid in thread 0.  Shared by pxa_tile_partials_fold (reduce.hip) and the tile kernel's own
 // last-workgroup fold (pgd_tv2d.hip), so both give the same bits.
-__device__ inline double fold_tile_stat(const double* __restrict__ pr, int64_t per_row, double* red) {
+struct PlainLoad {
+  __device__ double operator()(const double* a) const { return *a; }
+};
+template <typename Load = PlainLoad>
+__device__ inline double fold_tile_stat(const double* __restrict__ pr, int64_t per_row, double* red, Load ld = Load{}) {
   double acc = 0.0;
 #pragma unroll 8
-  for (int64_t k = threadIdx.x; k < per_row; k += kBlock) acc += pr[2 * k];
+  for (int64_t k = threadIdx.x; k < per_row; k += kBlock) acc += ld(pr + 2 * k);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -401,8 +401,11 @@ __device__ inline void wave_partials(double part_d, double part_x, double* parti
     part_x += __shfl_down(part_x, off, 64);
   }
   if ((threadIdx.x & 63) == 0) {
-    partials[2 * slot] = part_d;
-    partials[2 * slot + 1] = part_x;
+    // relaxed device-scope atomic stores: written through to the memory side (past this XCD's L2), so that the
+    // last-workgroup fold (tail_fold) on any XCD can read them without a release fence -- a device-scope fence
+    // per workgroup writes back the whole L2 (r05f: the kernel took 242 us instead of 25 with one)
+    __hip_atomic_store(partials + 2 * slot, part_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partials + 2 * slot + 1, part_x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -528,31 +531,35 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
 }
 
 // The RelError statistics of this launch, folded by the workgroup that finishes last (saves the fold launch
-// of a stop check: ~3.4 us of device time plus a launch gap per step at stop_rate 1).  Every wavefront's lane
-// 0 has written its (tile, wave) partials; a device-scope release fence, then one atomic count per workgroup;
-// the last one acquires, folds each (statistic, row) with fold_tile_stat in the order of
-// pxa_tile_partials_fold, stores the values and the completion flags (system scope, as that kernel does) and
-// resets the counter for the next launch.
+// of a stop check: ~3.4 us of device time plus a launch gap per step at stop_rate 1).  No fences: a
+// device-scope release fence writes back the whole L2 of the XCD, per workgroup.  Instead every wavefront's
+// lane 0 has written its (tile, wave) partials with relaxed device-scope atomic stores (wave_partials: write-
+// through to the memory side) and waits for them to complete (s_waitcnt vmcnt(0)) before the workgroup counts
+// itself with one relaxed device-scope atomic add; the last workgroup reads the partials with device-scope
+// atomic loads (memory side again), folds each (statistic, row) in the order of pxa_tile_partials_fold
+// (fold_tile_stat: same bits), writes the values and then, once they have completed, the completion flags to
+// the host buffer with system-scope atomic stores, and resets the counter for the next launch.
 template <typename T>
 __device__ inline void tail_fold(const PgdParams<T>& p, const double* __restrict__ partials) {
   __shared__ double red[kThreads / 64];
   __shared__ unsigned last;
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(p.counter, 1u) == gridDim.x - 1 ? 1u : 0u;
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(p.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u : 0u;
   __syncthreads();
   if (!last) return;
-  __threadfence();
+  auto ld = [](const double* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   for (int64_t q = 0; q < 2 * p.fold_rows; ++q) {
     const int64_t stat = q / p.fold_rows, r = q - stat * p.fold_rows;
-    const double t = fold_tile_stat(partials + 2 * r * p.fold_per_row + stat, p.fold_per_row, red);
-    if (threadIdx.x == 0) p.fold_vals[q] = t;
+    const double t = fold_tile_stat(partials + 2 * r * p.fold_per_row + stat, p.fold_per_row, red, ld);
+    if (threadIdx.x == 0) __hip_atomic_store(p.fold_vals + q, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (threadIdx.x == 0) {
-    *p.counter = 0u;
-    __threadfence_system();
+    __hip_atomic_store(p.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the values have reached host memory before the flags
     for (int64_t q = 0; q < 2 * p.fold_rows; ++q)
-      __hip_atomic_store(p.fold_flags + q, p.fold_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(p.fold_flags + q, p.fold_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

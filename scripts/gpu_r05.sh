@@ -88,6 +88,8 @@ if [ "$S" = "e" ]; then
   step bench 900 python bench.py --steps 20 --warmup 5
 fi
 if [ "$S" = "f" ]; then
+  step foldtest 300 $PT -m gpu tests/test_gpu_pgd_variants.py
+  PXA_RELERR_SINK=1 step foldtest_sink 300 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_solver_engine.py
   step foldlat 120 python3 scripts/fold_latency.py
   step sr1time 300 python3 scripts/host_time_pgd_sr1.py
   PXA_RELERR_SINK=1 step sr1time_sink 300 python3 scripts/host_time_pgd_sr1.py
