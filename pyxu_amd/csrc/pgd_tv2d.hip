@@ -215,13 +215,16 @@ __device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T*
 // are plain subtractions, fma(-1, a, 1 * b) == b - a to the bit, two fewer VALU per q point and per pixel.
 constexpr int kVarTV = 1, kVarUnit = 2;
 #ifndef PXA_PGD_SWEEP_BATCH
-#define PXA_PGD_SWEEP_BATCH 13
+#define PXA_PGD_SWEEP_BATCH 0
 #endif
 #ifndef PXA_PGD_SCHED_SPLIT
-#define PXA_PGD_SCHED_SPLIT 1
+#define PXA_PGD_SCHED_SPLIT 0
 #endif
 #ifndef PXA_PGD_UNIT
 #define PXA_PGD_UNIT 1
+#endif
+#ifndef PXA_PGD_RUNTIME_TV
+#define PXA_PGD_RUNTIME_TV 1
 #endif
 // build-time A/B knobs of the tile kernel's code generation (csrc/Makefile `ab` builds): pass B's G1 sweep loads
 // PT rows in scheduling windows of kSweepBatch (0: all at once), a scheduling fence between the TV stencil and
@@ -231,7 +234,12 @@ constexpr int kSweepBatch = PXA_PGD_SWEEP_BATCH;
 template <typename T, int R, bool EDGE, int VAR, typename Emit>
 __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, const T* KT, const T* GH, int ty0, int tx0,
                               Emit&& emit, int tid = threadIdx.x) {
-  constexpr bool TV = (VAR & kVarTV) != 0, UNIT = (VAR & kVarUnit) != 0;
+  constexpr bool UNIT = (VAR & kVarUnit) != 0;
+#if PXA_PGD_RUNTIME_TV
+  const bool TV = p.tv;  // (A/B build: the TV term as a uniform runtime branch, as in rounds 1-4)
+#else
+  constexpr bool TV = (VAR & kVarTV) != 0;
+#endif
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
@@ -283,6 +291,12 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
           }
           q0[c] = v0 * w;
           q1[c] = v1 * w;
+          if constexpr (UNIT) {
+            // opaque: with unit spacing the adjoint below is a plain subtraction of two q values, and the
+            // compiler would otherwise fuse a product into it (fp-contract) in some code paths and not in
+            // others -- the interior and edge tiles must round alike (test_vector_and_scalar_paths_bit_exact)
+            asm volatile("" : "+v"(q0[c]), "+v"(q1[c]));
+          }
         }
       };
       T yc[V][CW];  // yk at the item's own pixels
@@ -292,7 +306,7 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
         yrow(0, yr);
         yrow(1, yn);
         T qp0[CW + 1], qp1[CW + 1];
-        if constexpr (TV) qrow(0, yr, yn, qp0, qp1);
+        if (TV) qrow(0, yr, yn, qp0, qp1);
 #pragma unroll
         for (int u = 0; u < V; ++u) {
 #pragma unroll
@@ -300,7 +314,7 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
           yrow(u + 2, yn);
 #pragma unroll
           for (int w = 0; w < CW; ++w) yc[u][w] = yr[w + 1];
-          if constexpr (TV) {
+          if (TV) {
             T qc0[CW + 1], qc1[CW + 1];
             qrow(u + 1, yr, yn, qc0, qc1);
             // Grad^T q: flipped 2-tap adjoints, (+1/h tap at i - e_d) then (-1/h tap at i), summed over d
@@ -332,8 +346,7 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
         T g[CW], y[CW];
 #pragma unroll
         for (int w = 0; w < CW; ++w) {
-          if constexpr (TV) g[w] = acc[w][u] + tv[u][w];
-          else g[w] = acc[w][u];
+          g[w] = TV ? acc[w][u] + tv[u][w] : acc[w][u];
           y[w] = yc[u][w];
         }
         emit(k, u, ty0 + V * a + u, tx0 + c0, g, y);

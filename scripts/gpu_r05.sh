@@ -98,10 +98,10 @@ fi
 if [ "$S" = "g" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py tests/test_gpu_long_trajectories.py tests/test_gpu_small_weights.py -k "pgd or c2 or c5 or smoke or trajectory"
   for i in 1 2; do
-    for v in base unit; do PXA_LIB_PATH=ab/libpyxu_amd_$v.so step drv_${v}_$i 120 $DRV; done
+    for v in base unit ctv; do PXA_LIB_PATH=ab/libpyxu_amd_$v.so step drv_${v}_$i 120 $DRV; done
     step drv_main_$i 120 $DRV
   done
-  for v in base unit; do PXA_LIB_PATH=ab/libpyxu_amd_$v.so step c5_$v 300 python3 bench.py --only c5; done
+  for v in base unit ctv; do PXA_LIB_PATH=ab/libpyxu_amd_$v.so step c5_$v 300 python3 bench.py --only c5; done
   step c5_main 300 python3 bench.py --only c5
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
 fi
