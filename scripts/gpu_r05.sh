@@ -95,7 +95,7 @@ if [ "$S" = "f" ]; then
   PXA_RELERR_SINK=1 step sr1time_sink 300 python3 scripts/host_time_pgd_sr1.py
   step drv1 120 $DRV
 fi
-if [ "$S" = "g" ]; then
+if [ "$S" = "g" ] || [ "$S" = "h" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py tests/test_gpu_long_trajectories.py tests/test_gpu_small_weights.py -k "pgd or c2 or c5 or smoke or trajectory"
   for i in 1 2; do
     for v in base unit ctv; do PXA_LIB_PATH=ab/libpyxu_amd_$v.so step drv_${v}_$i 120 $DRV; done
@@ -104,6 +104,14 @@ if [ "$S" = "g" ]; then
   for v in base unit ctv; do PXA_LIB_PATH=ab/libpyxu_amd_$v.so step c5_$v 300 python3 bench.py --only c5; done
   step c5_main 300 python3 bench.py --only c5
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+fi
+if [ "$S" = "g" ] || [ "$S" = "h" ]; then
+  if [ "$S" = "h" ]; then
+    step c4 300 python3 bench.py --only c4
+    step c4hostprof 300 python3 scripts/c4_host_prof.py
+    step c4trace 300 rocprofv3 --kernel-trace --stats -d $P/c4 -o run --output-format csv -- python3 bench.py --only c4
+    python3 scripts/c4_timeline.py $P/c4 > $O/c4timeline.log 2>&1 || true
+  fi
 fi
 if [ "$S" = "pgd" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py -k "pgd or c2 or c5 or smoke or trajectory"
