@@ -210,36 +210,9 @@ __device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T*
 // `emit(k, u, gr, gc, g, yc)`: g = (G yk + Grad^T q) at row gr, columns gc .. gc + CW - 1 of item k,
 // yc = yk there.  The emitter finishes the pixels in place (finish_run) or stages g for the
 // coalesced epilogue (epilogue_staged).
-// VAR: compile-time variant of the objective -- bit 0: the TV term is present (lam != 0; else no q at all), bit 1:
-// unit grid spacing (h0 = h1 = 1, the Gradient's default sampling): the forward differences and their adjoint
-// are plain subtractions, fma(-1, a, 1 * b) == b - a to the bit, two fewer VALU per q point and per pixel.
-constexpr int kVarTV = 1, kVarUnit = 2;
-#ifndef PXA_PGD_SWEEP_BATCH
-#define PXA_PGD_SWEEP_BATCH 0
-#endif
-#ifndef PXA_PGD_SCHED_SPLIT
-#define PXA_PGD_SCHED_SPLIT 0
-#endif
-#ifndef PXA_PGD_UNIT
-#define PXA_PGD_UNIT 1
-#endif
-#ifndef PXA_PGD_RUNTIME_TV
-#define PXA_PGD_RUNTIME_TV 1
-#endif
-// build-time A/B knobs of the tile kernel's code generation (csrc/Makefile `ab` builds): pass B's G1 sweep loads
-// PT rows in scheduling windows of kSweepBatch (0: all at once), a scheduling fence between the TV stencil and
-// the sweep, and the unit-spacing variant
-constexpr int kSweepBatch = PXA_PGD_SWEEP_BATCH;
-
-template <typename T, int R, bool EDGE, int VAR, typename Emit>
+template <typename T, int R, bool EDGE, typename Emit>
 __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, const T* KT, const T* GH, int ty0, int tx0,
                               Emit&& emit, int tid = threadIdx.x) {
-  constexpr bool UNIT = (VAR & kVarUnit) != 0;
-#if PXA_PGD_RUNTIME_TV
-  const bool TV = p.tv;  // (A/B build: the TV term as a uniform runtime branch, as in rounds 1-4)
-#else
-  constexpr bool TV = (VAR & kVarTV) != 0;
-#endif
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
@@ -276,14 +249,8 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
       auto qrow = [&](int r, const T(&yr)[CW + 2], const T(&yn)[CW + 2], T(&q0)[CW + 1], T(&q1)[CW + 1]) {
 #pragma unroll
         for (int c = 0; c <= CW; ++c) {
-          T v0, v1;
-          if constexpr (UNIT) {
-            v0 = yn[c] - yr[c];
-            v1 = yr[c + 1] - yr[c];
-          } else {
-            v0 = fma(p.g0a, yr[c], p.g0b * yn[c]);
-            v1 = fma(p.g1a, yr[c], p.g1b * yr[c + 1]);
-          }
+          const T v0 = fma(p.g0a, yr[c], p.g0b * yn[c]);
+          const T v1 = fma(p.g1a, yr[c], p.g1b * yr[c + 1]);
           T w = tv_weight<T>(fma(v0, v0, v1 * v1), p.lam, p.mu, p.inv_mu);
           if (EDGE) {
             const int gr = ty0 + V * a - 1 + r, gc = tx0 + c0 - 1 + c;
@@ -291,12 +258,6 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
           }
           q0[c] = v0 * w;
           q1[c] = v1 * w;
-          if constexpr (UNIT) {
-            // opaque: with unit spacing the adjoint below is a plain subtraction of two q values, and the
-            // compiler would otherwise fuse a product into it (fp-contract) in some code paths and not in
-            // others -- the interior and edge tiles must round alike (test_vector_and_scalar_paths_bit_exact)
-            asm volatile("" : "+v"(q0[c]), "+v"(q1[c]));
-          }
         }
       };
       T yc[V][CW];  // yk at the item's own pixels
@@ -306,7 +267,7 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
         yrow(0, yr);
         yrow(1, yn);
         T qp0[CW + 1], qp1[CW + 1];
-        if (TV) qrow(0, yr, yn, qp0, qp1);
+        if (p.tv) qrow(0, yr, yn, qp0, qp1);
 #pragma unroll
         for (int u = 0; u < V; ++u) {
 #pragma unroll
@@ -314,20 +275,14 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
           yrow(u + 2, yn);
 #pragma unroll
           for (int w = 0; w < CW; ++w) yc[u][w] = yr[w + 1];
-          if (TV) {
+          if (p.tv) {
             T qc0[CW + 1], qc1[CW + 1];
             qrow(u + 1, yr, yn, qc0, qc1);
             // Grad^T q: flipped 2-tap adjoints, (+1/h tap at i - e_d) then (-1/h tap at i), summed over d
 #pragma unroll
             for (int w = 0; w < CW; ++w) {
-              T t0, t1;
-              if constexpr (UNIT) {
-                t0 = qp0[w + 1] - qc0[w + 1];
-                t1 = qc1[w] - qc1[w + 1];
-              } else {
-                t0 = fma(p.g0b, qp0[w + 1], p.g0a * qc0[w + 1]);
-                t1 = fma(p.g1b, qc1[w], p.g1a * qc1[w + 1]);
-              }
+              const T t0 = fma(p.g0b, qp0[w + 1], p.g0a * qc0[w + 1]);
+              const T t1 = fma(p.g1b, qc1[w], p.g1a * qc1[w + 1]);
               tv[u][w] = t0 + t1;
             }
 #pragma unroll
@@ -336,17 +291,14 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
         }
       }
       T acc[CW][V];            // acc[w][u]: column c0 + w, row V a + u
-      // the TV stencil above and the G1 sweep below are separate scheduling regions: interleaved, their live
-      // values together exceed the 128 VGPRs (spills)
-      if constexpr (PXA_PGD_SCHED_SPLIT != 0) __builtin_amdgcn_sched_barrier(0);
-      sweep<T, R, CW, L::PTP, kSweepBatch>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g1, acc);
+      sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g1, acc);
       if (edge_cols) ghost_fix_pre<T, R, CW, TY>(tx0 + c0, n1, V * a, GH, KT + kKT, acc);
 #pragma unroll
       for (int u = 0; u < V; ++u) {
         T g[CW], y[CW];
 #pragma unroll
         for (int w = 0; w < CW; ++w) {
-          g[w] = TV ? acc[w][u] + tv[u][w] : acc[w][u];
+          g[w] = p.tv ? acc[w][u] + tv[u][w] : acc[w][u];
           y[w] = yc[u][w];
         }
         emit(k, u, ty0 + V * a + u, tx0 + c0, g, y);
@@ -459,7 +411,7 @@ __device__ inline void wave_partials(double part_d, double part_x, double* parti
 
 // One output tile: phase 0 (window), pass A, [ghost columns], pass B (parked in registers), the H^T y / x
 // loads, O staging, row-major epilogue, [RelError partials].
-template <typename T, int R, bool EDGE, int VAR>
+template <typename T, int R, bool EDGE>
 __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
                                 const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
                                 T* __restrict__ xns, double* __restrict__ partials, const T* __restrict__ xrs) {
@@ -513,7 +465,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
 #pragma unroll
         for (int w = 0; w < CW; ++w) st[k][u][w] = A[tid + u * 64 + w];
   } else
-  pass_b<T, R, EDGE, VAR>(p, A, PT, KT, GH, ty0, tx0, [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
+  pass_b<T, R, EDGE>(p, A, PT, KT, GH, ty0, tx0, [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
 #pragma unroll
     for (int w = 0; w < CW; ++w) st[k][u][w] = g[w];
   });
@@ -611,7 +563,7 @@ __device__ inline void tail_fold(const PgdParams<T>& p, const double* __restrict
   }
 }
 
-template <typename T, int R, int VAR>
+template <typename T, int R>
 __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
                                                             const T* __restrict__ xp, const T* __restrict__ b,
                                                             T* __restrict__ xn, double* __restrict__ partials) {
@@ -648,18 +600,18 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
   const bool interior = p.vec_ok && img <= 0x7fffffff && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0 &&
                         tx0 - L::CA >= 0 && tx0 + TX + L::CA <= p.n1;
   if (interior)
-    pgd_tile<T, R, false, VAR>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials, xrs);
+    pgd_tile<T, R, false>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials, xrs);
   else
-    pgd_tile<T, R, true, VAR>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials, xrs);
+    pgd_tile<T, R, true>(p, smem_raw, tile, ty0, tx0, xs, xps, bs, xns, partials, xrs);
   if (p.fold_vals != nullptr) tail_fold<T>(p, partials);
 }
 
-template <typename T, int R, int VAR>
-int launch_pgd_var(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
-                   hipStream_t s) {
+template <typename T, int R>
+int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
+               hipStream_t s) {
   // Layout + the ghost terms (+ the timing trace under PXA_TUNE_PGD_DIAG bit 5)
   const size_t smem = kGhOff<T, R> + kGhBytes<T, R> + ((p.diag & 32) ? 256 : 0);
-  auto kern = pgd_tv2d_kernel<T, R, VAR>;
+  auto kern = pgd_tv2d_kernel<T, R>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -669,18 +621,6 @@ int launch_pgd_var(const PgdParams<T>& p, const void* x, const void* xp, const v
   hipLaunchKernelGGL(kern, dim3(p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp, (const T*)b,
                      (T*)xn, partials);
   return last_launch_status();
-}
-
-// the kernel variant of the objective: no TV term; TV with general spacing; TV with unit spacing (fp32 only: the
-// benchmark dtype -- fp64 keeps the general form, which gives the same bits, to bound the instantiations)
-template <typename T, int R>
-int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
-               hipStream_t s) {
-  if (!p.tv) return launch_pgd_var<T, R, 0>(p, x, xp, b, xn, partials, s);
-  const bool unit = p.g0a == T(-1) && p.g0b == T(1) && p.g1a == T(-1) && p.g1b == T(1);
-  if constexpr (sizeof(T) == 4 && PXA_PGD_UNIT != 0)
-    if (unit) return launch_pgd_var<T, R, kVarTV | kVarUnit>(p, x, xp, b, xn, partials, s);
-  return launch_pgd_var<T, R, kVarTV>(p, x, xp, b, xn, partials, s);
 }
 
 thread_local int g_last_pgd_kernel = 0;  // pxa_pgd_tv2d_last_kernel

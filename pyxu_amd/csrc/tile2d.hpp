@@ -91,7 +91,7 @@ struct Pk<float> {
 
 // Register-blocked sweep along the leading axis of a [m][pitch PS] source: for NO outputs along the
 // sweep and one V-vector across it, out[o][v] = sum_{t=0}^{4R} g[t] src[(o + t) * PS + v].
-template <typename T, int R, int NO, int PS, int SB = 0>
+template <typename T, int R, int NO, int PS>
 __device__ inline void sweep(const T* __restrict__ src, const T* __restrict__ g, T (&out)[NO][kVecN<T>]) {
   constexpr int V = kVecN<T>;
   using P = typename Pk<T>::type;
@@ -104,10 +104,6 @@ __device__ inline void sweep(const T* __restrict__ src, const T* __restrict__ g,
     for (int h = 0; h < NP; ++h) acc[o][h] = Pk<T>::splat(T(0));
 #pragma unroll
   for (int j = 0; j < NO + 4 * R; ++j) {
-    // a scheduling fence every SB rows: the compiler otherwise issues all NO + 4R row loads up front (26
-    // ds_read_b128 = 104 VGPRs for the PGD pass B at R = 6), which is the kernel's register peak
-    if constexpr (SB > 0)
-      if (j > 0 && j % SB == 0) __builtin_amdgcn_sched_barrier(0);
     const VT t = *reinterpret_cast<const VT*>(src + j * PS);
     P row[NP];
     __builtin_memcpy(&row[0], &t, sizeof(VT));
