@@ -20,12 +20,12 @@ def main():
     rows.sort()
     # the timed window: from the 2nd-to-last run of normal_rows_kernel launches of the warm-up onwards; take
     # the last 4 outer iterations' worth: the last 60% of normal_rows launches
-    idx = [i for i, r in enumerate(rows) if r[2] == "normal_rows_kernel"]
+    idx = [i for i, r in enumerate(rows) if r[2] in ("normal_rows_kernel", "normal_group_kernel")]
     if not idx:
-        raise SystemExit("no normal_rows_kernel")
+        raise SystemExit("no normal_rows_kernel / normal_group_kernel")
     lo = idx[int(len(idx) * 0.4)]
     win = rows[lo:]
-    n_cg = sum(1 for r in win if r[2] == "normal_rows_kernel")
+    n_cg = sum(1 for r in win if r[2] in ("normal_rows_kernel", "normal_group_kernel"))
     busy = collections.Counter()
     cnt = collections.Counter()
     gaps = collections.Counter()
