@@ -156,6 +156,15 @@ int pxa_clip(int dtype, int64_t n, const void* x, double lo, double hi, int has_
 /* L1Norm.prox (operator/func/norm.py:47-52): out = fmax(0, |x| - tau) * sign(x). */
 int pxa_prox_l1(int dtype, int64_t n, const void* x, double tau, void* out, void* stream);
 
+/* ADMM outer update for h = lam ||.||_1 and K = Id (opt/solver/pds.py:1606-1620) fused with the next
+ * x-update's right-hand side (QuadraticFunc.prox, operator.py:1257-1291), element-wise in one pass with the
+ * rounding of the separate map calls:  zt = z + x - u;  u' = prox_l1(x + zt, thr);
+ * z' = zt + (rho-1) x - (rho-1) u';  b = (u' - z') / tau - cgrad.  `out` holds 6 x n elements:
+ * u', z', b, b, b, 0 (the CG's b, r0, p0 and x0 = 0).  Replaces seven pxa_lincomb3 / pxa_axpby /
+ * pxa_prox_l1 / pxa_div launches and the CG set-up's fill and two copies. */
+int pxa_admm_l1_update(int dtype, int64_t n, const void* x, const void* z, const void* u, const void* cgrad,
+                       double rho_m1, double thr, double tau, void* out, void* stream);
+
 /* L21Norm.prox (norm.py:352-364) with x viewed as (outer, group, inner) and the l2 norm taken over
  * `group` at each (outer, inner):  out = x * (1 - tau / fmax(||x||_2, tau)). */
 int pxa_prox_l21(int dtype, int64_t outer, int64_t group, int64_t inner, const void* x, double tau, void* out,
@@ -205,6 +214,11 @@ int pxa_row_reduce_pow(int dtype, int64_t rows, int64_t n, double p, const void*
 size_t pxa_cg_update_workspace_bytes(int64_t rows);
 int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
                   double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, void* stream);
+
+/* pxa_cg_update without its first launch: work[0 .. rows * 64) already holds the <p, A p> partials, written
+ * together with A p by pxa_dense_normal_pdot (same partition and bits as pxa_cg_update's own). */
+int pxa_cg_update_tail(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
+                       double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, void* stream);
 
 /* RelError statistics from the fused PGD step's per-tile partials (pxa_pgd_tv2d_step[_y] with
  * `partials`): out[0 * rows + r] = sum (x_new - x)^2 and out[1 * rows + r] = sum x^2 over the per_row
@@ -342,6 +356,13 @@ int pxa_dense_matmat(int dtype, int trans, int64_t M, int64_t N, int64_t B, cons
 size_t pxa_dense_normal_workspace_bytes(int dtype, int64_t M, int64_t N, int64_t B);
 int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, const void* X, double s, double d,
                      void* Y, void* work, void* stream);
+
+/* pxa_dense_normal (B = 1) that also writes the <X, Y> partials of the CG iterating on this operator into
+ * pdot (pxa_cg_update's partition: min(64, ceil(N / 256)) doubles), folded into the partial-sum reduction
+ * launch (one launch instead of two reductions and the CG's dot); then pxa_cg_update_tail with pdot as the
+ * head of its workspace.  Same bits as pxa_dense_normal followed by pxa_cg_update. */
+int pxa_dense_normal_pdot(int dtype, int64_t M, int64_t N, const void* A, const void* X, double s, double d, void* Y,
+                          void* work, double* pdot, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Array primitives: the data movement of the operator algebra and the NumPy-named functions of the

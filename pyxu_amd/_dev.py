@@ -369,6 +369,19 @@ def prox_l1(x, tau, out=None):
     return out
 
 
+def admm_l1_update(x, z, u, cgrad, rho_m1, thr, tau):
+    """ADMM outer update (h = lam L1, K = Id) + the next CG right-hand side in one launch
+    (pxa_admm_l1_update): returns (u', z', b, r0, p0, x0), views of one (6, *x.shape) buffer."""
+    x, z, u, cgrad = require(x), require(z), require(u), require(cgrad)
+    n = x.numel()
+    assert z.numel() == n and u.numel() == n and cgrad.numel() == n
+    assert z.dtype == x.dtype and u.dtype == x.dtype and cgrad.dtype == x.dtype
+    out = empty((6,) + tuple(x.shape), x)
+    check(lib.pxa_admm_l1_update(dtcode(x), n, ptr(x), ptr(z), ptr(u), ptr(cgrad), float(rho_m1), float(thr),
+                                 float(tau), ptr(out), stream()), "pxa_admm_l1_update")
+    return tuple(out.unbind(0))
+
+
 def fenchel_prox_l1(x, sigma, lam, out=None):
     x = require(x)
     out = empty_like(x) if out is None else out
@@ -568,19 +581,21 @@ def relerr_stats(x, x_prev, out, copy=True):
     return xc
 
 
-def cg_update(x, r, p, ap, rr, rr_out, rr_host, work):
+def cg_update(x, r, p, ap, rr, rr_out, rr_host, work, have_pap=False):
     """pxa_cg_update: the CG iteration tail after A p on (rows, n) x / r / p / A p (in place), from this
     step's ||r||^2 `rr` (device float64 (rows,)); ||r'||^2 lands in rr_out (device) and in rr_host: a
     HostFlagBuffer(rows, rows, rows) (returns the publication's sequence number, which its wait() takes), a
-    pinned host tensor, or None."""
+    pinned host tensor, or None.  have_pap: `work` already holds the <p, A p> partials (pxa_cg_update_tail;
+    dense_normal(..., pdot=work) wrote them with A p)."""
     rows, n = x.shape
     seq, vp_, fp_ = 0, None, None
     if isinstance(rr_host, HostFlagBuffer):
         seq, vp_, fp_ = rr_host.next_seq(), rr_host.vptr, rr_host.fptr
     elif rr_host is not None:
         vp_ = rr_host.data_ptr()
-    check(lib.pxa_cg_update(dtcode(x), rows, n, ptr(x), ptr(r), ptr(p), ptr(ap), rr.data_ptr(), rr_out.data_ptr(),
-                            vp_, fp_, seq, work.data_ptr(), stream()), "pxa_cg_update")
+    fn = lib.pxa_cg_update_tail if have_pap else lib.pxa_cg_update
+    check(fn(dtcode(x), rows, n, ptr(x), ptr(r), ptr(p), ptr(ap), rr.data_ptr(), rr_out.data_ptr(), vp_, fp_, seq,
+             work.data_ptr(), stream()), "pxa_cg_update")
     return seq
 
 
@@ -890,9 +905,11 @@ def dense_normal_supported(A, x):
             and int(lib.pxa_dense_normal_workspace_bytes(dtcode(x), M, N, 1)) > 0)
 
 
-def dense_normal(A, x, s, d, work=None):
+def dense_normal(A, x, s, d, work=None, pdot=None):
     """Y = s * A^T (A x) + d * x in one pass over A (pxa_dense_normal); `work`: a reusable uint8 device
-    buffer of at least pxa_dense_normal_workspace_bytes bytes (allocated when None)."""
+    buffer of at least pxa_dense_normal_workspace_bytes bytes (allocated when None).  pdot: a float64 device
+    buffer that receives the CG's <x, Y> partials in the same launches (pxa_dense_normal_pdot, for
+    cg_update(..., have_pap=True) with pdot as its work)."""
     torch = _torch()
     M, N = A.shape
     wsz = int(lib.pxa_dense_normal_workspace_bytes(dtcode(x), M, N, 1))
@@ -901,8 +918,13 @@ def dense_normal(A, x, s, d, work=None):
     if work is None or work.numel() < wsz:
         work = torch.empty((wsz,), dtype=torch.uint8, device=x.device)
     Y = empty(x.shape, x)
-    check(lib.pxa_dense_normal(dtcode(x), M, N, 1, ptr(A), ptr(x), float(s), float(d), ptr(Y), ptr(work), stream()),
-          "pxa_dense_normal")
+    if pdot is None:
+        check(lib.pxa_dense_normal(dtcode(x), M, N, 1, ptr(A), ptr(x), float(s), float(d), ptr(Y), ptr(work), stream()),
+              "pxa_dense_normal")
+    else:
+        assert pdot.dtype == torch.float64 and pdot.is_cuda
+        check(lib.pxa_dense_normal_pdot(dtcode(x), M, N, ptr(A), ptr(x), float(s), float(d), ptr(Y), ptr(work),
+                                        pdot.data_ptr(), stream()), "pxa_dense_normal_pdot")
     return Y
 
 

@@ -72,6 +72,36 @@ def _memo_quad_spec(func):
     return memo
 
 
+def _chain_quadratic(op):
+    """The QuadraticFunc of a composed quadratic ``q(K x)`` (ChainRule, lhs quadratic, rhs linear) whose prox
+    the composition's prox evaluates: one per (memoised) spec, so that its per-instance caches (the constant
+    c.grad, the CG sub-solver) survive across prox calls (ADMM calls this once per outer iteration)."""
+    Q, c, t = op._quad_spec()
+    qf = op.__dict__.get("_quad_prox_fn")
+    if qf is None or qf[0] is not Q or qf[1] is not c or qf[2] is not t:
+        qf = op._quad_prox_fn = (Q, c, t, pxo.QuadraticFunc(shape=op.shape, Q=Q, c=c, t=t))
+    return qf[3]
+
+
+def quadratic_prox_target(op):
+    """The QuadraticFunc whose prox ``op.prox(arr, tau)`` evaluates (CG on Q + I / tau from b = arr / tau -
+    c.grad), or None when op's prox takes another route.  Follows the dispatch of ChainRule.prox
+    (arithmetic.py:1009-1030 of the reference) without evaluating anything."""
+    P = pxo.Property
+    if not (op.has(P.PROXIMABLE) and op.has(P.QUADRATIC)):
+        return None
+    bound = op.__dict__.get("prox")
+    if bound is None:
+        return op if isinstance(op, pxo.QuadraticFunc) and type(op).prox is pxo.QuadraticFunc.prox else None
+    if getattr(bound, "__func__", None) is not ChainRule.prox:
+        return None
+    if op._lhs.has(P.PROXIMABLE) and op._rhs.has(P.LINEAR_UNITARY):
+        return None
+    if op._lhs.has(P.QUADRATIC) and op._rhs.has(P.LINEAR):
+        return _chain_quadratic(op)
+    return None
+
+
 class Rule:
     def op(self):
         raise NotImplementedError
@@ -622,13 +652,7 @@ class ChainRule(Rule):
             if self._lhs.has(P.PROXIMABLE) and self._rhs.has(P.LINEAR_UNITARY):
                 return self._rhs.adjoint(self._lhs.prox(self._rhs.apply(arr), tau))
             if self._lhs.has(P.QUADRATIC) and self._rhs.has(P.LINEAR):
-                Q, c, t = self._quad_spec()
-                # one QuadraticFunc per (memoised) spec, so that its per-instance caches (the constant c.grad)
-                # survive across prox calls (ADMM calls this once per outer iteration)
-                qf = self.__dict__.get("_quad_prox_fn")
-                if qf is None or qf[0] is not Q or qf[1] is not c or qf[2] is not t:
-                    qf = self._quad_prox_fn = (Q, c, t, pxo.QuadraticFunc(shape=self.shape, Q=Q, c=c, t=t))
-                return qf[3].prox(arr, tau)
+                return _chain_quadratic(self).prox(arr, tau)
             if self._lhs.has(P.LINEAR) and self._rhs.has(P.PROXIMABLE):
                 return ScaleRule(op=self._rhs, cst=self._lhs_scalar()).op().prox(arr, tau)
             if P.LINEAR in (self._lhs.properties() & self._rhs.properties()):

@@ -14,23 +14,6 @@
 namespace pxa {
 namespace {
 
-constexpr int kCgBlocks = 64;  // partial-sum blocks per row
-
-__device__ inline double block_sum(double v, double* sh) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) sh[w] = v;
-  __syncthreads();
-  double r = 0.0;
-  if (threadIdx.x == 0) {
-    r = sh[0];
-    for (int k = 1; k < kBlock / 64; ++k) r += sh[k];
-  }
-  return r;  // valid in thread 0
-}
-
 // fixed-order fold of the nb partials of row `row` (every thread gets the same bits)
 __device__ inline double fold(const double* __restrict__ part, int64_t row, int nb) {
   double s = 0.0;
@@ -48,8 +31,8 @@ __global__ void __launch_bounds__(kBlock) cg_dot_kernel(int64_t n, const T* __re
   const T* pr = p + row * n;
   const T* ar = ap + row * n;
   double acc = 0.0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += (double)pr[i] * (double)ar[i];
-  const double s = block_sum(acc, sh);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc = fma((double)pr[i], (double)ar[i], acc);
+  const double s = cg_block_sum(acc, sh);
   if (threadIdx.x == 0) part[row * gridDim.x + blockIdx.x] = s;
 }
 
@@ -72,9 +55,9 @@ __global__ void __launch_bounds__(kBlock) cg_xr_kernel(int64_t n, const double* 
     xr[i] = fma(alpha, pr[i], xr[i]);            // x += alpha p
     const T rn = fma(-alpha, ar[i], rw[i]);      // r -= alpha A p
     rw[i] = rn;
-    acc += (double)rn * (double)rn;
+    acc = fma((double)rn, (double)rn, acc);
   }
-  const double s = block_sum(acc, sh);
+  const double s = cg_block_sum(acc, sh);
   if (threadIdx.x == 0) part_rr[row * gridDim.x + blockIdx.x] = s;
 }
 
@@ -107,23 +90,23 @@ __global__ void __launch_bounds__(kBlock) cg_p_kernel(int64_t n, const double* _
 
 using namespace pxa;
 
-extern "C" {
-
-size_t pxa_cg_update_workspace_bytes(int64_t rows) { return rows > 0 ? (size_t)rows * 2 * kCgBlocks * sizeof(double) : 0; }
-
-int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
-                  double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, void* stream) {
+namespace {
+int cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
+              double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, bool have_pap, void* stream) {
   PXA_CHECK_ARG(rows >= 1 && rows <= 65535 && n >= 1);
   PXA_CHECK_ARG(x && r && p && ap && rr && rr_out && work && rr_out != rr);
   hipStream_t st = as_stream(stream);
-  const int nb = (int)(n < (int64_t)kCgBlocks * kBlock ? (n + kBlock - 1) / kBlock : kCgBlocks);
+  const int nb = cg_blocks(n);
   double* part_pap = (double*)work;
   double* part_rr = part_pap + rows * kCgBlocks;
   const dim3 grid((unsigned)nb, (unsigned)rows);
   PXA_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL((cg_dot_kernel<T>), grid, dim3(kBlock), 0, st, n, (const T*)p, (const T*)ap, part_pap);
-    int e = last_launch_status();
-    if (e) return e;
+    int e = 0;
+    if (!have_pap) {
+      hipLaunchKernelGGL((cg_dot_kernel<T>), grid, dim3(kBlock), 0, st, n, (const T*)p, (const T*)ap, part_pap);
+      e = last_launch_status();
+      if (e) return e;
+    }
     hipLaunchKernelGGL((cg_xr_kernel<T>), grid, dim3(kBlock), 0, st, n, rr, part_pap, (const T*)p, (const T*)ap,
                        (T*)x, (T*)r, part_rr);
     e = last_launch_status();
@@ -132,6 +115,21 @@ int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p,
                        rr_host, (unsigned*)flags, (unsigned)seq);
     return last_launch_status();
   });
+}
+}  // namespace
+
+extern "C" {
+
+size_t pxa_cg_update_workspace_bytes(int64_t rows) { return rows > 0 ? (size_t)rows * 2 * kCgBlocks * sizeof(double) : 0; }
+
+int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
+                  double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, void* stream) {
+  return cg_update(dtype, rows, n, x, r, p, ap, rr, rr_out, rr_host, flags, seq, work, false, stream);
+}
+
+int pxa_cg_update_tail(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
+                       double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, void* stream) {
+  return cg_update(dtype, rows, n, x, r, p, ap, rr, rr_out, rr_host, flags, seq, work, true, stream);
 }
 
 }  // extern "C"

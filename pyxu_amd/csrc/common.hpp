@@ -77,6 +77,30 @@ __device__ inline double fold_tile_stat(const double* __restrict__ pr, int64_t p
   return t;
 }
 
+// CG iteration tail partition (cg.hip): the <p, A p> and ||r'||^2 partials of a row come from cg_blocks(n)
+// workgroups of kBlock threads, block b owning elements [b chunk, (b + 1) chunk), chunk = ceil(n / blocks),
+// thread t summing elements lo + t, lo + t + kBlock, ... in order, then cg_block_sum.  Shared by cg.hip and
+// the dense normal operator's fused reduction (dense.hip), so that both give the same bits.
+constexpr int kCgBlocks = 64;
+inline int cg_blocks(int64_t n) { return (int)(n < (int64_t)kCgBlocks * kBlock ? (n + kBlock - 1) / kBlock : kCgBlocks); }
+
+// shuffle-down fold per wavefront, then thread 0 adds the kBlock / 64 wave results in order (valid in thread
+// 0); every thread of the workgroup calls it, only the first kBlock threads' values count.
+__device__ inline double cg_block_sum(double v, double* sh) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0 && w < kBlock / kWave) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0) {
+    r = sh[0];
+    for (int k = 1; k < kBlock / kWave; ++k) r += sh[k];
+  }
+  return r;
+}
+
 }  // namespace pxa
 
 // dtype dispatch: `code` is PXA_F32 / PXA_F64.

@@ -1054,6 +1054,84 @@ __global__ void __launch_bounds__(kBlock) normal_final_kernel(int N4, int slices
                      fmaf(s, (float)acc.z, dd * xv.z), fmaf(s, (float)acc.w, dd * xv.w));
 }
 
+// normal_sum + normal_final + the CG's <p, A p> partials (cg.hip's cg_dot, partition cg_blocks(n)) in one
+// launch, for a CG iterating on this operator.  Workgroup b owns the cg chunk [b chunk, (b + 1) chunk) of the
+// row; its thread group y (kBlock threads) sums partials [kNormSlice y, kNormSlice (y + 1)) of a float4 column
+// in double, g ascending, as normal_sum's slice y; group 0 then adds the slice sums in slice order and forms
+// Y as normal_final, keeping Y and x in LDS; its kBlock threads finally form cg_dot's per-thread sums over
+// those copies (elements lo + t, lo + t + kBlock, ...) and cg_block_sum.  Same bits as the three launches.
+constexpr int kFdMaxChunk = 2048;  // elements per workgroup (LDS: x and Y, 16 KB)
+constexpr int kFdMaxSlices = 4;
+
+template <int S>
+__global__ void __launch_bounds__(S * kBlock) normal_final_dot_kernel(int64_t n, int G, const float4* __restrict__ part,
+                                                                      const float4* __restrict__ x, float s, float dd,
+                                                                      float4* __restrict__ Y, int64_t chunk,
+                                                                      double* __restrict__ pdot) {
+  __shared__ double4 ssum[S > 1 ? S - 1 : 1][kBlock];
+  __shared__ float4 yl[kFdMaxChunk / 4], xl[kFdMaxChunk / 4];
+  __shared__ double sh[kBlock / kWave];
+  const int64_t N4 = n / 4;
+  const int y = threadIdx.x / kBlock, t = threadIdx.x % kBlock;
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  const int64_t c4lo = lo / 4;
+  const int c4n = hi > lo ? (int)((hi - lo) / 4) : 0;
+  const int g0 = y * kNormSlice, g1 = g0 + kNormSlice < G ? g0 + kNormSlice : G;
+  for (int j0 = 0; j0 < c4n; j0 += kBlock) {
+    const int j = j0 + t;
+    double4 acc = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (j < c4n) {
+      const int64_t c = c4lo + j;
+#pragma unroll 8
+      for (int g = g0; g < g1; ++g) {
+        const float4 v = part[(int64_t)g * N4 + c];
+        acc.x += (double)v.x;
+        acc.y += (double)v.y;
+        acc.z += (double)v.z;
+        acc.w += (double)v.w;
+      }
+    }
+    if (y > 0) ssum[y - 1][t] = acc;
+    __syncthreads();
+    if (y == 0 && j < c4n) {
+      for (int k = 1; k < S; ++k) {
+        const double4 v = ssum[k - 1][t];
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+      const float4 xv = x[c4lo + j];
+      const float4 o = make_float4(fmaf(s, (float)acc.x, dd * xv.x), fmaf(s, (float)acc.y, dd * xv.y),
+                                   fmaf(s, (float)acc.z, dd * xv.z), fmaf(s, (float)acc.w, dd * xv.w));
+      Y[c4lo + j] = o;
+      yl[j] = o;
+      xl[j] = xv;
+    }
+    __syncthreads();
+  }
+  const float* yf = reinterpret_cast<const float*>(yl);
+  const float* xf = reinterpret_cast<const float*>(xl);
+  double acc = 0.0;
+  if (y == 0)
+    for (int64_t i = t; i < hi - lo; i += kBlock) acc = fma((double)xf[i], (double)yf[i], acc);
+  const double r = cg_block_sum(acc, sh);
+  if (threadIdx.x == 0) pdot[blockIdx.x] = r;
+}
+
+// cg.hip's cg_dot for one fp32 row (the fallback of the fused reduction above)
+__global__ void __launch_bounds__(kBlock) normal_pdot_kernel(int64_t n, const float* __restrict__ p,
+                                                             const float* __restrict__ ap, double* __restrict__ part) {
+  __shared__ double sh[kBlock / kWave];
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  double acc = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc = fma((double)p[i], (double)ap[i], acc);
+  const double r = cg_block_sum(acc, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
 inline int normal_groups(int64_t M) { return (int)(M < kNormG ? M : kNormG); }
 // groups of the split kernel: a multiple of 8 (one XCD per group) when M allows, at most kNormG / kParts
 inline int normal_group_count(int64_t M) {
@@ -1081,10 +1159,32 @@ inline size_t normal_workspace(int64_t M, int64_t N) {
   return normal_stats_offset(M, N) + (size_t)kParts * normal_group_count(M) * 8 * sizeof(uint64_t);
 }
 
-// fixed-order sum of the `rows` partials (rows x N fp32 at work) and s * sum + d * x
-inline int normal_reduce(int rows, int64_t N, const float* x, float s, float d, float* Y, float* work, hipStream_t st) {
+// fixed-order sum of the `rows` partials (rows x N fp32 at work) and s * sum + d * x; with `pdot`, also the
+// CG's <x, Y> partials (cg_blocks(N) doubles, cg.hip's partition and bits)
+inline int normal_reduce(int rows, int64_t N, const float* x, float s, float d, float* Y, float* work, double* pdot,
+                         hipStream_t st) {
   const int N4 = (int)(N / 4);
   const int slices = normal_slices(rows);
+  if (pdot != nullptr) {
+    const int nb = cg_blocks(N);
+    const int64_t chunk = (N + nb - 1) / nb;
+    if (chunk % 4 == 0 && chunk <= kFdMaxChunk && slices <= kFdMaxSlices) {
+      const float4* part = reinterpret_cast<const float4*>(work);
+      const float4* xv = reinterpret_cast<const float4*>(x);
+      float4* yv = reinterpret_cast<float4*>(Y);
+      if (slices == 1)
+        hipLaunchKernelGGL(normal_final_dot_kernel<1>, dim3(nb), dim3(kBlock), 0, st, N, rows, part, xv, s, d, yv, chunk, pdot);
+      else if (slices == 2)
+        hipLaunchKernelGGL(normal_final_dot_kernel<2>, dim3(nb), dim3(2 * kBlock), 0, st, N, rows, part, xv, s, d, yv, chunk, pdot);
+      else
+        hipLaunchKernelGGL(normal_final_dot_kernel<4>, dim3(nb), dim3(4 * kBlock), 0, st, N, rows, part, xv, s, d, yv, chunk, pdot);
+      return last_launch_status();
+    }
+    const int e = normal_reduce(rows, N, x, s, d, Y, work, nullptr, st);
+    if (e) return e;
+    hipLaunchKernelGGL(normal_pdot_kernel, dim3(nb), dim3(kBlock), 0, st, N, x, Y, pdot);
+    return last_launch_status();
+  }
   double4* sums = reinterpret_cast<double4*>(reinterpret_cast<unsigned char*>(work) + normal_sums_offset(rows, N));
   const unsigned cb = (unsigned)((N4 + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(normal_sum_kernel, dim3(cb, (unsigned)slices), dim3(kBlock), 0, st, N4, rows,
@@ -1098,7 +1198,7 @@ inline int normal_reduce(int rows, int64_t N, const float* x, float s, float d, 
 
 template <int NV>
 int launch_normal(int64_t M, int64_t N, const float* A, const float* x, float s, float d, float* Y, float* work,
-                  hipStream_t st) {
+                  double* pdot, hipStream_t st) {
   using P = NormPlan<NV>;
   static bool attr = false;
   if (!attr) {
@@ -1115,12 +1215,12 @@ int launch_normal(int64_t M, int64_t N, const float* A, const float* x, float s,
   else
     hipLaunchKernelGGL((normal_rows_kernel<NV, false>), dim3(G), dim3(kNormThreads), P::LDS, st, M, N4, A, x, work);
   const int e = last_launch_status();
-  return e ? e : normal_reduce(G, N, x, s, d, Y, work, st);
+  return e ? e : normal_reduce(G, N, x, s, d, Y, work, pdot, st);
 }
 
 template <int NVS>
 int launch_normal_group(int64_t M, int64_t N, const float* A, const float* x, float s, float d, float* Y, float* work,
-                        bool solo, hipStream_t st) {
+                        bool solo, double* pdot, hipStream_t st) {
   const size_t lds = GroupPlan<NVS>::LDS;
   static bool attr = false;
   if (!attr) {
@@ -1154,7 +1254,7 @@ int launch_normal_group(int64_t M, int64_t N, const float* A, const float* x, fl
     hipLaunchKernelGGL((normal_group_kernel<NVS, false>), dim3(kParts * C), dim3(kNormThreads), lds, st, M, N4, A, x,
                        work, slots, rpg, tag, (int)solo, stats, flav);
   const int e = last_launch_status();
-  return e ? e : normal_reduce(C, N, x, s, d, Y, work, st);
+  return e ? e : normal_reduce(C, N, x, s, d, Y, work, pdot, st);
 }
 
 }  // namespace
@@ -1225,8 +1325,8 @@ size_t pxa_dense_normal_workspace_bytes(int dtype, int64_t M, int64_t N, int64_t
   return normal_workspace(M, N);
 }
 
-int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, const void* X, double s, double d,
-                     void* Y, void* work, void* stream) {
+static int dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, const void* X, double s, double d, void* Y,
+                 void* work, double* pdot, void* stream) {
   PXA_CHECK_ARG(M >= 1 && N >= 1 && B >= 0);
   if (B == 0) return PXA_OK;
   PXA_CHECK_ARG(A != nullptr && X != nullptr && Y != nullptr && Y != X);
@@ -1237,21 +1337,34 @@ int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, 
   const float* a = (const float*)A;
   const float* x = (const float*)X;
   const float fs = (float)s, fd = (float)d;
+  float* y = (float*)Y;
+  float* w = (float*)work;
   const int kern = tuning(PXA_TUNE_NORMAL_KERNEL) & 15;  // (probe build: bit 4 selects plain exchange stores)
   if (kern != 1) {  // split rows (2: without the exchange, every part-dot computed by every member; same bits)
     const int64_t nvs = ((N / 4 + kParts - 1) / kParts + kNormThreads - 1) / kNormThreads;  // vectors per part
     const bool solo = kern == 2;
-    if (nvs <= 1) return launch_normal_group<1>(M, N, a, x, fs, fd, (float*)Y, (float*)work, solo, st);
-    if (nvs <= 2) return launch_normal_group<2>(M, N, a, x, fs, fd, (float*)Y, (float*)work, solo, st);
-    return launch_normal_group<4>(M, N, a, x, fs, fd, (float*)Y, (float*)work, solo, st);
+    if (nvs <= 1) return launch_normal_group<1>(M, N, a, x, fs, fd, y, w, solo, pdot, st);
+    if (nvs <= 2) return launch_normal_group<2>(M, N, a, x, fs, fd, y, w, solo, pdot, st);
+    return launch_normal_group<4>(M, N, a, x, fs, fd, y, w, solo, pdot, st);
   }
   const int64_t nv = (N / 4 + kNormThreads - 1) / kNormThreads;  // vectors per thread
-  if (nv <= 1) return launch_normal<1>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
-  if (nv <= 2) return launch_normal<2>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
-  if (nv <= 4) return launch_normal<4>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
-  if (nv <= 8) return launch_normal<8>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
-  if (nv <= 12) return launch_normal<12>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
-  return launch_normal<16>(M, N, a, x, fs, fd, (float*)Y, (float*)work, st);
+  if (nv <= 1) return launch_normal<1>(M, N, a, x, fs, fd, y, w, pdot, st);
+  if (nv <= 2) return launch_normal<2>(M, N, a, x, fs, fd, y, w, pdot, st);
+  if (nv <= 4) return launch_normal<4>(M, N, a, x, fs, fd, y, w, pdot, st);
+  if (nv <= 8) return launch_normal<8>(M, N, a, x, fs, fd, y, w, pdot, st);
+  if (nv <= 12) return launch_normal<12>(M, N, a, x, fs, fd, y, w, pdot, st);
+  return launch_normal<16>(M, N, a, x, fs, fd, y, w, pdot, st);
+}
+
+int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, const void* X, double s, double d,
+                     void* Y, void* work, void* stream) {
+  return dense_normal(dtype, M, N, B, A, X, s, d, Y, work, nullptr, stream);
+}
+
+int pxa_dense_normal_pdot(int dtype, int64_t M, int64_t N, const void* A, const void* X, double s, double d, void* Y,
+                          void* work, double* pdot, void* stream) {
+  PXA_CHECK_ARG(pdot != nullptr);
+  return dense_normal(dtype, M, N, 1, A, X, s, d, Y, work, pdot, stream);
 }
 
 }  // extern "C"

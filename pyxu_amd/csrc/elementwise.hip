@@ -48,10 +48,13 @@ int launch_map(int64_t n, Op op, const void* a, const void* b, const void* c, vo
   return last_launch_status();
 }
 
+// The contractions of a*x + b*y (+ c*z) are spelled out: with -ffp-contract=fast the backend picks which
+// product to fuse per kernel, and a fused kernel reusing these functors (admm_l1_kernel, the PDS marches'
+// fma(b, y, a * x)) must round exactly like the map launches it replaces.
 template <typename T>
 struct AxpbyOp {
   T a, b;
-  __device__ T operator()(T x, T y, T) const { return a * x + b * y; }
+  __device__ T operator()(T x, T y, T) const { return fma(b, y, a * x); }
 };
 template <typename T>
 struct ScaleOp {
@@ -70,7 +73,7 @@ struct ExtrapOp {  // (x - y) * a + x   (PGD momentum, pgd.py:179-181)
 template <typename T>
 struct Lin3Op {
   T a, b, c;
-  __device__ T operator()(T x, T y, T z) const { return a * x + b * y + c * z; }
+  __device__ T operator()(T x, T y, T z) const { return fma(c, z, fma(b, y, a * x)); }
 };
 template <typename T>
 struct DivOp {
@@ -316,12 +319,96 @@ __global__ void __launch_bounds__(kBlock) row_ratio_kernel(int64_t rows, const d
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += stride) out[i] = (T)(num[i] / den[i]);
 }
 
+// ADMM outer update for h = lam ||.||_1, K = Id, and the right-hand side of the next x-update
+// (QuadraticFunc.prox -> CG) in one pass (opt/solver/pds.py:1606-1620 + operator.py:1257-1291).  Per element,
+// the same functors and the same rounding to T after every step as the chain of map launches it replaces:
+//   zt = lincomb3(1, z, 1, x, -1, u)          u' = prox_l1(axpby(1, x, 1, zt), thr)
+//   z' = lincomb3(1, zt, rho-1, x, -(rho-1), u')
+//   b  = axpby(1, div(axpby(1, u', -1, z'), tau), -1, cgrad)
+// Planes of `out` (6 x n): u', z', b, r0 = b, p0 = b, x0 = 0 (CG's start from zero: r0 = b - A 0 = b).
+template <typename T>
+struct AdmmL1 {
+  Lin3Op<T> zt_op;
+  AxpbyOp<T> v_op;
+  ProxL1Op<T> prox;
+  Lin3Op<T> z_op;
+  AxpbyOp<T> arr_op;
+  DivOp<T> div;
+  AxpbyOp<T> b_op;
+  __device__ void operator()(T x, T z, T u, T cg, T& un, T& zn, T& b) const {
+    const T zt = zt_op(z, x, u);
+    un = prox(v_op(x, zt, T(0)), T(0), T(0));
+    zn = z_op(zt, x, un);
+    b = b_op(div(arr_op(un, zn, T(0)), T(0), T(0)), cg, T(0));
+  }
+};
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) admm_l1_kernel(int64_t n, AdmmL1<T> op, const T* __restrict__ x,
+                                                         const T* __restrict__ z, const T* __restrict__ u,
+                                                         const T* __restrict__ cg, T* __restrict__ out, bool vec) {
+  constexpr int V = kVecN<T>;
+  using VT = typename Vec4<T>::type;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nv = vec ? n / V : 0;
+  for (int64_t i = tid; i < nv; i += stride) {
+    T vx[V], vz[V], vu[V], vc[V], ou[V], oz[V], ob[V], o0[V];
+    *reinterpret_cast<VT*>(vx) = reinterpret_cast<const VT*>(x)[i];
+    *reinterpret_cast<VT*>(vz) = reinterpret_cast<const VT*>(z)[i];
+    *reinterpret_cast<VT*>(vu) = reinterpret_cast<const VT*>(u)[i];
+    *reinterpret_cast<VT*>(vc) = reinterpret_cast<const VT*>(cg)[i];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      op(vx[k], vz[k], vu[k], vc[k], ou[k], oz[k], ob[k]);
+      o0[k] = T(0);
+    }
+    VT* o = reinterpret_cast<VT*>(out);
+    const int64_t nq = n / V;
+    o[i] = *reinterpret_cast<VT*>(ou);
+    o[nq + i] = *reinterpret_cast<VT*>(oz);
+    o[2 * nq + i] = *reinterpret_cast<VT*>(ob);
+    o[3 * nq + i] = *reinterpret_cast<VT*>(ob);
+    o[4 * nq + i] = *reinterpret_cast<VT*>(ob);
+    o[5 * nq + i] = *reinterpret_cast<VT*>(o0);
+  }
+  for (int64_t i = nv * V + tid; i < n; i += stride) {
+    T un, zn, b;
+    op(x[i], z[i], u[i], cg[i], un, zn, b);
+    out[i] = un;
+    out[n + i] = zn;
+    out[2 * n + i] = b;
+    out[3 * n + i] = b;
+    out[4 * n + i] = b;
+    out[5 * n + i] = T(0);
+  }
+}
+
 }  // namespace
 }  // namespace pxa
 
 using namespace pxa;
 
 extern "C" {
+
+int pxa_admm_l1_update(int dtype, int64_t n, const void* x, const void* z, const void* u, const void* cgrad,
+                       double rho_m1, double thr, double tau, void* out, void* stream) {
+  PXA_CHECK_ARG(n >= 0);
+  if (n == 0) return PXA_OK;
+  PXA_CHECK_ARG(x && z && u && cgrad && out);
+  PXA_DISPATCH(dtype, T, {
+    const T one = T(1), rm = (T)rho_m1;
+    const AdmmL1<T> op{Lin3Op<T>{one, one, -one}, AxpbyOp<T>{one, one}, ProxL1Op<T>{(T)thr},
+                       Lin3Op<T>{one, rm, -rm},    AxpbyOp<T>{one, -one}, DivOp<T>{(T)tau},
+                       AxpbyOp<T>{one, -one}};
+    const bool vec = n % kVecN<T> == 0 && aligned16(x) && aligned16(z) && aligned16(u) && aligned16(cgrad) &&
+                     aligned16(out);
+    const int64_t items = vec ? n / kVecN<T> : n;
+    hipLaunchKernelGGL((admm_l1_kernel<T>), dim3(grid_for(items)), dim3(kBlock), 0, as_stream(stream), n, op,
+                       (const T*)x, (const T*)z, (const T*)u, (const T*)cgrad, (T*)out, vec);
+    return last_launch_status();
+  });
+}
 
 int pxa_axpby(int dtype, int64_t n, double a, const void* x, double b, const void* y, void* out, void* stream) {
   if (y == nullptr) {

@@ -13,6 +13,11 @@ __all__ = ["CG"]
 _ROWSTAT = "__rowstat__"
 
 
+# A p and the CG's <p, A p> partials from one set of launches when the operator can produce them
+# (pxa_dense_normal_pdot -> pxa_cg_update_tail; same bits either way).  Tests switch it off for the A/B.
+_FUSED_DOT = True
+
+
 def _rows2d(x):
     return x.reshape(-1, x.shape[-1])
 
@@ -53,6 +58,7 @@ class CG(pxa.Solver):
     """Solve ``A x = b`` for positive-definite ``A`` (cg.py:14-187)."""
 
     steps_taken = 0  # process-wide count of CG iterations (diagnostic: inner iterations of ADMM / prox)
+    _pap_ready = None  # A p whose <p, A p> partials the tail workspace holds (see _apply_p)
 
     def __init__(self, A, **kwargs):
         kwargs.update(log_var=kwargs.get("log_var", ("x",)))
@@ -60,7 +66,7 @@ class CG(pxa.Solver):
         self._A = A
 
     @pxrt.enforce_precision(i=("b", "x0"))
-    def m_init(self, b, x0=None, restart_rate=None):
+    def m_init(self, b, x0=None, restart_rate=None, _preset=None):
         mst = self._mstate
         b = _dev.require(b, "b")
         if restart_rate is not None:
@@ -68,7 +74,12 @@ class CG(pxa.Solver):
             mst["restart_rate"] = int(restart_rate)
         else:
             mst["restart_rate"] = self._A.dim
-        if x0 is None:
+        if _preset is not None:
+            # (x0 = 0, r0 = b, p0 = b) already written by the caller's kernel (pxa_admm_l1_update): the start
+            # from zero below, without the fill and the two copies
+            assert x0 is None and all(t.shape == b.shape and t.dtype == b.dtype for t in _preset)
+            mst["b"], mst["x"] = b, _preset[0]
+        elif x0 is None:
             mst["b"] = b
             mst["x"] = _dev.zeros(b.shape, b)
         elif b.shape == x0.shape:
@@ -91,25 +102,39 @@ class CG(pxa.Solver):
         key = (tuple(mst["x"].shape), mst["x"].dtype, str(mst["x"].device))
         if getattr(self, "_apply_key", None) != key:  # (the operator is fixed per solver: reuse across fits)
             self._apply, self._apply_key = self._make_apply(mst["x"]), key
-        if x0 is None:
-            # x = 0: A x = 0 exactly, so r = b - A x = b bit for bit -- skip the product (one full pass over
-            # the operator per solve; QuadraticFunc.prox, i.e. every ADMM x-update, starts from zero)
-            mst["residual"] = _dev.copy(mst["b"])
+        if _preset is not None:
+            mst["residual"], mst["conjugate_dir"] = _preset[1], _preset[2]
         else:
-            mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._apply(mst["x"]))
-        mst["conjugate_dir"] = _dev.copy(mst["residual"])
+            if x0 is None:
+                # x = 0: A x = 0 exactly, so r = b - A x = b bit for bit -- skip the product (one full pass over
+                # the operator per solve; QuadraticFunc.prox, i.e. every ADMM x-update, starts from zero)
+                mst["residual"] = _dev.copy(mst["b"])
+            else:
+                mst["residual"] = _dev.axpby(1.0, mst["b"], -1.0, self._apply(mst["x"]))
+            mst["conjugate_dir"] = _dev.copy(mst["residual"])
         self._rr_hist = []  # host ||r||^2 (max over rows) of the last steps: convergence-rate estimate
         self._abs_eps = self._stop_eps()
         # ||r0||^2 with an async host copy, published for the first stop check (AbsError on the residual:
         # the same reduction, so the same bits) and reused by the first step's alpha; a sub-solver then
         # launches A p0 before that check, so the device works while the host decides
         r = mst["residual"]
-        hr0 = _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)))
+        ahead = _preset[3:] if _preset is not None and len(_preset) == 5 else None
+        hr0 = ahead[0] if ahead else _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)))
         self._rr = (hr0, r)  # ||r||^2 of the current residual (then carried from the previous step's beta)
         mst[_ROWSTAT] = {"residual": (r, 2, hr0)}
         self._Ap_next = None  # A p of the current p, launched ahead of the stop check (see m_step)
         if self._astate.get("internal"):
-            self._Ap_next = self._apply(mst["conjugate_dir"])
+            self._Ap_next = ahead[1] if ahead else self._apply_p(mst["conjugate_dir"])
+
+    def _launch_start(self, r0, p0):
+        """||r0||^2 (with its async host copy) and A p0 of a solve about to start from (x0 = 0, r0, p0 = r0),
+        launched by the caller right after it wrote r0 / p0 (ADMM._m_step_l1), so that the device starts the
+        first operator pass while the host sets the solve up; m_init takes them as _preset[3:].  The same
+        launches m_init would make, hence the same bits.  None if the operator for these vectors is not set
+        up yet (the first solve)."""
+        if getattr(self, "_apply_key", None) != (tuple(p0.shape), p0.dtype, str(p0.device)):
+            return None
+        return _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r0))), self._apply_p(p0)
 
     def _make_apply(self, like):
         """A.apply, or -- when A = s K^T K + d I for one dense K (ADMM's QuadraticFunc.prox operator,
@@ -124,23 +149,53 @@ class CG(pxa.Solver):
             return self._A.apply
         work = [None]
 
+        def workspace(v):
+            if work[0] is None:
+                import torch
+
+                wsz = int(_dev.lib.pxa_dense_normal_workspace_bytes(_dev.dtcode(v), mat.shape[0], mat.shape[1], 1))
+                work[0] = torch.empty((wsz,), dtype=torch.uint8, device=v.device)
+            return work[0]
+
         def apply(v):
             if not _dev.dense_normal_supported(mat, v):
                 return self._A.apply(v)
-            import torch
-
-            if work[0] is None:
-                wsz = int(_dev.lib.pxa_dense_normal_workspace_bytes(_dev.dtcode(v), mat.shape[0], mat.shape[1], 1))
-                work[0] = torch.empty((wsz,), dtype=torch.uint8, device=v.device)
             if not sharded:
-                return _dev.dense_normal(mat, v, s, d, work=work[0])
+                return _dev.dense_normal(mat, v, s, d, work=workspace(v))
             from pyxu_amd.distributed import allreduce
 
-            y = allreduce(_dev.dense_normal(mat, v, s, 0.0, work=work[0]), "sum", group)
+            y = allreduce(_dev.dense_normal(mat, v, s, 0.0, work=workspace(v)), "sum", group)
             return _dev.axpby(1.0, y, d, v, out=y)
 
+        def apply_pdot(v, pdot):
+            if sharded or not _dev.dense_normal_supported(mat, v):
+                return None
+            return _dev.dense_normal(mat, v, s, d, work=workspace(v), pdot=pdot)
+
         apply.fused = True
+        apply.pdot = apply_pdot
         return apply
+
+    def _apply_p(self, p):
+        """A p for a CG step; when the operator can produce them in the same launches (one dense normal
+        operator, one row), also the step's <p, A p> partials into the tail workspace, marked by
+        self._pap_ready = A p for m_step's pxa_cg_update_tail."""
+        pd = getattr(self._apply, "pdot", None)
+        if pd is not None and _FUSED_DOT and p.dim() == 1:
+            Ap = pd(p, self._cg_workspace(1))
+            if Ap is not None:
+                self._pap_ready = Ap
+                return Ap
+        return self._apply(p)
+
+    def _cg_workspace(self, rows):
+        import torch
+
+        w = getattr(self, "_cg_work", None)
+        need = max(int(_dev.lib.pxa_cg_update_workspace_bytes(rows)) // 8, 1)
+        if w is None or w.numel() < need or w.device != self._mstate["x"].device:
+            w = self._cg_work = torch.empty((need,), dtype=torch.float64, device=self._mstate["x"].device)
+        return w
 
     def m_step(self):
         """cg.py:125-153.  alpha = ||r||^2 / <p, A p> and beta = ||r'||^2 / ||r||^2 are formed on the
@@ -159,7 +214,8 @@ class CG(pxa.Solver):
         x, r, p = mst["x"], mst["residual"], mst["conjugate_dir"]
         Ap, self._Ap_next = self._Ap_next, None
         if Ap is None:
-            Ap = self._apply(p)
+            Ap = self._apply_p(p)
+        have_pap, self._pap_ready = self._pap_ready is Ap, None
         if self._rr is not None and self._rr[1] is r:
             rr = self._rr[0]  # ||r||^2 of this r: the previous step's beta numerator (identical bits)
         else:
@@ -173,13 +229,14 @@ class CG(pxa.Solver):
             # the whole tail in three launches (pxa_cg_update): alpha, x, r, ||r'||^2, beta, p; ||r'||^2 is
             # written straight into pinned host memory for the next stop check
             hr = self._rows_buffers(_rows2d(x).shape[0])
-            seq = _dev.cg_update(_rows2d(x), _rows2d(r), _rows2d(p), _rows2d(Ap), rr.dev, hr[0], hr[1], self._cg_work)
+            seq = _dev.cg_update(_rows2d(x), _rows2d(r), _rows2d(p), _rows2d(Ap), rr.dev, hr[0], hr[1], self._cg_work,
+                                 have_pap=have_pap)
             hr = _KernelRows(hr[0], hr[1], seq)
             self._rr = (hr, r)
             if self._astate.get("internal"):
                 mst[_ROWSTAT] = {"residual": (r, 2, hr)}
                 if not self._predict_stop(rr_host):
-                    self._Ap_next = self._apply(p)
+                    self._Ap_next = self._apply_p(p)
             mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
             return
         pAp = _dev.row_reduce(_dev.RED_DOT, _rows2d(p), _rows2d(Ap))
@@ -201,7 +258,7 @@ class CG(pxa.Solver):
             if self._astate.get("internal"):
                 mst[_ROWSTAT] = {"residual": (r, 2, hr)}
                 if not self._predict_stop(rr_host):
-                    self._Ap_next = self._apply(p)
+                    self._Ap_next = self._apply_p(p)
         mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
 
     def _rows_buffers(self, rows):
@@ -215,8 +272,7 @@ class CG(pxa.Solver):
             bufs = [(torch.empty((rows,), dtype=torch.float64, device=dev),
                      _dev.HostFlagBuffer(rows, rows, rows)) for _ in range(2)]
             self._rr_bufs, self._rr_flip = bufs, 0
-            self._cg_work = torch.empty((max(int(_dev.lib.pxa_cg_update_workspace_bytes(rows)) // 8, 1),),
-                                        dtype=torch.float64, device=dev)
+        self._cg_workspace(rows)
         self._rr_flip ^= 1
         return bufs[self._rr_flip]
 

@@ -528,12 +528,56 @@ class ADMM(_PDS):
     def m_step(self):
         mst = self._mstate
         tau, rho = mst["tau"], mst["rho"]
+        fast = self._l1_fast_path()
+        if fast is not None:
+            return self._m_step_l1(fast, tau, rho)
         mst["x"] = self._x_update(_dev.axpby(1.0, mst["u"], -1.0, mst["z"]), tau=tau)
         Kx = self._K(mst["x"])
         z_temp = _dev.lincomb3(1.0, mst["z"], 1.0, Kx, -1.0, mst["u"])
         if not _is_null(self._h):
             mst["u"] = self._h.prox(_dev.axpby(1.0, Kx, 1.0, z_temp), tau=tau)
         mst["z"] = _dev.lincomb3(1.0, z_temp, rho - 1, Kx, -(rho - 1), mst["u"])
+
+    def _l1_fast_path(self):
+        """(QuadraticFunc q, L1 scale or None) when the outer update can run as one kernel: the x-update is
+        q.prox (CG on Q + I/tau), K = Id and h = lam ||.||_1 (lam = None: h = ||.||_1); else None."""
+        if "_l1_fast" in self.__dict__:
+            return self._l1_fast
+        from pyxu_amd.abc.arithmetic import quadratic_prox_target
+        from pyxu_amd.operator.func.norm import L1Norm
+        from pyxu_amd.operator.linop import IdentityOp
+
+        fast, h = None, self._h
+        if self._x_update_solver == "prox" and type(self._K) is IdentityOp and not _is_null(h):
+            qf = quadratic_prox_target(self._g)
+            if type(h) is L1Norm:
+                fast = None if qf is None else (qf, None)
+            elif (qf is not None and h.has(pxa.Property.CAN_EVAL) and h._expr()[0] == "scale"
+                  and type(h._op) is L1Norm):
+                fast = (qf, h._cst)
+        self._l1_fast = fast
+        return fast
+
+    def _m_step_l1(self, fast, tau, rho):
+        """m_step for h = lam L1, K = Id and a CG x-update (pds.py:1606-1620): the outer update and the next
+        x-update's right-hand side in one launch (pxa_admm_l1_update, same roundings as the chain of map
+        launches of the general m_step), whose b / r0 / p0 / x0 planes the next CG solve starts from.  The
+        first step (or one after the state was replaced) forms b the general way."""
+        mst = self._mstate
+        qf, cst = fast
+        pre = self.__dict__.get("_l1_pre")
+        if pre is not None and pre[0] is mst["u"] and pre[1] is mst["z"] and pre[2] == float(tau):
+            x = qf._prox_solve(pre[3], tau, preset=pre[4:])
+        else:
+            x = self._x_update(_dev.axpby(1.0, mst["u"], -1.0, mst["z"]), tau=tau)
+        _, c, _ = qf._quad_spec()
+        thr = pxrt.coerce(tau) if cst is None else pxrt.coerce(pxrt.coerce(tau) * cst)  # ScaleRule -> L1Norm.prox
+        u, z, b, r0, p0, x0 = _dev.admm_l1_update(x, mst["z"], mst["u"], qf._c_grad(c, x), rho - 1, thr, tau)
+        # the next solve's ||r0||^2 and first operator pass go to the device now, ahead of the host's
+        # bookkeeping between the two x-updates
+        ahead = qf._prox_cg(tau)[0]._launch_start(r0, p0)
+        mst["x"], mst["u"], mst["z"] = x, u, z
+        self._l1_pre = (u, z, float(tau), b, x0, r0, p0) + (ahead if ahead is not None else ())
 
     def _x_update(self, arr, tau):
         if self._x_update_solver == "custom":

@@ -39,6 +39,14 @@ if [ "$S" = "new" ]; then
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
   step bench 900 python bench.py --steps 20 --warmup 5
 fi
+if [ "$S" = "admm" ]; then
+  step admmtests 600 $PT -m gpu tests/test_gpu_admm_fused.py tests/test_gpu_dense_normal.py
+  step admmtests2 900 $PT -m gpu tests/test_gpu_pds_fused.py tests/test_gpu_parity.py tests/test_gpu_solver_engine.py tests/test_gpu_blocks.py tests/test_gpu_long_trajectories.py
+  step c4a 300 python3 bench.py --only c4
+  step c4b 300 python3 bench.py --only c4
+  step c4trace 300 rocprofv3 --kernel-trace --stats -d $P/c4 -o run --output-format csv -- python3 bench.py --only c4
+  python3 scripts/c4_timeline.py $P/c4 > $O/c4timeline.log 2>&1 || true
+fi
 if [ "$S" = "a" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_long_trajectories.py tests/test_gpu_small_weights.py -k "pgd or c2 or c5"
   step drvnew 120 $DRV

@@ -180,3 +180,35 @@ def test_cg_published_residual_stat_gives_same_stop_decisions():
             res[internal] = (s._astate["idx"], to_NUMPY(s.solution()))
     assert res[True][0] == res[False][0]
     assert np.array_equal(res[True][1], res[False][1])
+
+
+@pytest.mark.parametrize("M,N,mode", [(1024, 8192, 0), (256, 65536, 0), (300, 1000, 0), (64, 40000, 0),
+                                      (512, 8192, 1), (2048, 65536, 1)])
+def test_fused_cg_dot_same_bits(M, N, mode):
+    """CG on the dense normal operator with <p, A p> folded into the operator's reduction launch
+    (pxa_dense_normal_pdot + pxa_cg_update_tail) against the separate cg_dot launch: the same iterates and
+    iteration count, bit for bit.  Shapes: the fused kernel with 2 partial slices (N % 256 chunks), chunks
+    that are not float4 multiples or beyond the LDS stage (N = 1000, 40000: the fallback dot launch), and the
+    one-workgroup-per-row kernel (mode 1: 8 slices, the fallback)."""
+    import pyxu_amd.opt.solver.cg as cgm
+
+    rng = np.random.default_rng(M + N)
+    A = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    res = {}
+    old = _dev.tuning(_dev.TUNE_NORMAL_KERNEL, mode)
+    try:
+        for fused in (True, False):
+            cgm._FUSED_DOT = fused
+            with pxrt.Precision(pxrt.Width.SINGLE):
+                K = pxa.LinOp.from_array(to_device(A))
+                q = pxa.QuadraticFunc(shape=(1, N), Q=K.T * K)
+                x = q.prox(to_device(b), 0.5)  # CG on K^T K + 2 I, the sub-solver ADMM runs
+                slvr = q._prox_cg(np.float32(0.5))[0]
+                assert slvr._apply.fused
+                res[fused] = (slvr._astate["idx"], to_NUMPY(x))
+    finally:
+        cgm._FUSED_DOT = True
+        _dev.tuning(_dev.TUNE_NORMAL_KERNEL, old)
+    assert res[True][0] == res[False][0] and res[True][0] >= 5
+    assert np.array_equal(res[True][1].view(np.uint32), res[False][1].view(np.uint32))
