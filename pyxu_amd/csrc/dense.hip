@@ -1054,70 +1054,51 @@ __global__ void __launch_bounds__(kBlock) normal_final_kernel(int N4, int slices
                      fmaf(s, (float)acc.z, dd * xv.z), fmaf(s, (float)acc.w, dd * xv.w));
 }
 
-// normal_sum + normal_final + the CG's <p, A p> partials (cg.hip's cg_dot, partition cg_blocks(n)) in one
-// launch, for a CG iterating on this operator.  Workgroup b owns the cg chunk [b chunk, (b + 1) chunk) of the
-// row; its thread group y (kBlock threads) sums partials [kNormSlice y, kNormSlice (y + 1)) of a float4 column
-// in double, g ascending, as normal_sum's slice y; group 0 then adds the slice sums in slice order and forms
-// Y as normal_final, keeping Y and x in LDS; its kBlock threads finally form cg_dot's per-thread sums over
-// those copies (elements lo + t, lo + t + kBlock, ...) and cg_block_sum.  Same bits as the three launches.
+// normal_final + the CG's <p, A p> partials (cg.hip's cg_dot, partition cg_blocks(n)) in one launch, for a
+// CG iterating on this operator (after normal_sum, whose slice sums it reads).  Workgroup b owns the cg chunk
+// [b chunk, (b + 1) chunk) of the row: its threads form Y as normal_final (slice sums added in slice order)
+// for the chunk's float4 columns, keep Y and x in LDS, then form cg_dot's per-thread sums over those copies
+// (elements lo + t, lo + t + kBlock, ...) and cg_block_sum.  Same bits as normal_final + cg_dot.
+// (A variant that also summed the G partials, normal_sum's 16 MB at C4, ran on only the 64 cg workgroups:
+// 11.3 us against 4.6 + 4.5 + 4.5 for the three launches, r05m.)
 constexpr int kFdMaxChunk = 2048;  // elements per workgroup (LDS: x and Y, 16 KB)
-constexpr int kFdMaxSlices = 4;
 
-template <int S>
-__global__ void __launch_bounds__(S * kBlock) normal_final_dot_kernel(int64_t n, int G, const float4* __restrict__ part,
-                                                                      const float4* __restrict__ x, float s, float dd,
-                                                                      float4* __restrict__ Y, int64_t chunk,
-                                                                      double* __restrict__ pdot) {
-  __shared__ double4 ssum[S > 1 ? S - 1 : 1][kBlock];
+__global__ void __launch_bounds__(kBlock) normal_final_dot_kernel(int64_t n, int slices, const double4* __restrict__ sums,
+                                                                  const float4* __restrict__ x, float s, float dd,
+                                                                  float4* __restrict__ Y, int64_t chunk,
+                                                                  double* __restrict__ pdot) {
   __shared__ float4 yl[kFdMaxChunk / 4], xl[kFdMaxChunk / 4];
   __shared__ double sh[kBlock / kWave];
   const int64_t N4 = n / 4;
-  const int y = threadIdx.x / kBlock, t = threadIdx.x % kBlock;
+  const int t = threadIdx.x;
   const int64_t lo = (int64_t)blockIdx.x * chunk;
   const int64_t hi = lo + chunk < n ? lo + chunk : n;
   const int64_t c4lo = lo / 4;
   const int c4n = hi > lo ? (int)((hi - lo) / 4) : 0;
-  const int g0 = y * kNormSlice, g1 = g0 + kNormSlice < G ? g0 + kNormSlice : G;
-  for (int j0 = 0; j0 < c4n; j0 += kBlock) {
-    const int j = j0 + t;
-    double4 acc = make_double4(0.0, 0.0, 0.0, 0.0);
-    if (j < c4n) {
-      const int64_t c = c4lo + j;
-#pragma unroll 8
-      for (int g = g0; g < g1; ++g) {
-        const float4 v = part[(int64_t)g * N4 + c];
-        acc.x += (double)v.x;
-        acc.y += (double)v.y;
-        acc.z += (double)v.z;
-        acc.w += (double)v.w;
-      }
+  for (int j = t; j < c4n; j += kBlock) {
+    const int64_t c = c4lo + j;
+    double4 acc = sums[c];
+    for (int y = 1; y < slices; ++y) {
+      const double4 v = sums[(int64_t)y * N4 + c];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
     }
-    if (y > 0) ssum[y - 1][t] = acc;
-    __syncthreads();
-    if (y == 0 && j < c4n) {
-      for (int k = 1; k < S; ++k) {
-        const double4 v = ssum[k - 1][t];
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
-      }
-      const float4 xv = x[c4lo + j];
-      const float4 o = make_float4(fmaf(s, (float)acc.x, dd * xv.x), fmaf(s, (float)acc.y, dd * xv.y),
-                                   fmaf(s, (float)acc.z, dd * xv.z), fmaf(s, (float)acc.w, dd * xv.w));
-      Y[c4lo + j] = o;
-      yl[j] = o;
-      xl[j] = xv;
-    }
-    __syncthreads();
+    const float4 xv = x[c];
+    const float4 o = make_float4(fmaf(s, (float)acc.x, dd * xv.x), fmaf(s, (float)acc.y, dd * xv.y),
+                                 fmaf(s, (float)acc.z, dd * xv.z), fmaf(s, (float)acc.w, dd * xv.w));
+    Y[c] = o;
+    yl[j] = o;
+    xl[j] = xv;
   }
+  __syncthreads();
   const float* yf = reinterpret_cast<const float*>(yl);
   const float* xf = reinterpret_cast<const float*>(xl);
   double acc = 0.0;
-  if (y == 0)
-    for (int64_t i = t; i < hi - lo; i += kBlock) acc = fma((double)xf[i], (double)yf[i], acc);
+  for (int64_t i = t; i < hi - lo; i += kBlock) acc = fma((double)xf[i], (double)yf[i], acc);
   const double r = cg_block_sum(acc, sh);
-  if (threadIdx.x == 0) pdot[blockIdx.x] = r;
+  if (t == 0) pdot[blockIdx.x] = r;
 }
 
 // cg.hip's cg_dot for one fp32 row (the fallback of the fused reduction above)
@@ -1168,16 +1149,15 @@ inline int normal_reduce(int rows, int64_t N, const float* x, float s, float d, 
   if (pdot != nullptr) {
     const int nb = cg_blocks(N);
     const int64_t chunk = (N + nb - 1) / nb;
-    if (chunk % 4 == 0 && chunk <= kFdMaxChunk && slices <= kFdMaxSlices) {
-      const float4* part = reinterpret_cast<const float4*>(work);
-      const float4* xv = reinterpret_cast<const float4*>(x);
-      float4* yv = reinterpret_cast<float4*>(Y);
-      if (slices == 1)
-        hipLaunchKernelGGL(normal_final_dot_kernel<1>, dim3(nb), dim3(kBlock), 0, st, N, rows, part, xv, s, d, yv, chunk, pdot);
-      else if (slices == 2)
-        hipLaunchKernelGGL(normal_final_dot_kernel<2>, dim3(nb), dim3(2 * kBlock), 0, st, N, rows, part, xv, s, d, yv, chunk, pdot);
-      else
-        hipLaunchKernelGGL(normal_final_dot_kernel<4>, dim3(nb), dim3(4 * kBlock), 0, st, N, rows, part, xv, s, d, yv, chunk, pdot);
+    if (chunk % 4 == 0 && chunk <= kFdMaxChunk) {
+      const unsigned cb = (unsigned)((N4 + kBlock - 1) / kBlock);
+      double4* sums = reinterpret_cast<double4*>(reinterpret_cast<unsigned char*>(work) + normal_sums_offset(rows, N));
+      hipLaunchKernelGGL(normal_sum_kernel, dim3(cb, (unsigned)slices), dim3(kBlock), 0, st, N4, rows,
+                         reinterpret_cast<const float4*>(work), sums);
+      int e = last_launch_status();
+      if (e) return e;
+      hipLaunchKernelGGL(normal_final_dot_kernel, dim3(nb), dim3(kBlock), 0, st, N, slices, sums,
+                         reinterpret_cast<const float4*>(x), s, d, reinterpret_cast<float4*>(Y), chunk, pdot);
       return last_launch_status();
     }
     const int e = normal_reduce(rows, N, x, s, d, Y, work, nullptr, st);

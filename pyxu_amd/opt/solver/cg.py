@@ -77,7 +77,7 @@ class CG(pxa.Solver):
         if _preset is not None:
             # (x0 = 0, r0 = b, p0 = b) already written by the caller's kernel (pxa_admm_l1_update): the start
             # from zero below, without the fill and the two copies
-            assert x0 is None and all(t.shape == b.shape and t.dtype == b.dtype for t in _preset)
+            assert x0 is None and all(t.shape == b.shape and t.dtype == b.dtype for t in _preset[:3])
             mst["b"], mst["x"] = b, _preset[0]
         elif x0 is None:
             mst["b"] = b
