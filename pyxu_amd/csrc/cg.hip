@@ -14,10 +14,18 @@
 namespace pxa {
 namespace {
 
-// fixed-order fold of the nb partials of row `row` (every thread gets the same bits)
+// fixed-order fold of the nb partials of row `row` (every thread gets the same bits): s = 0 + part[0] + part[1]
+// + ... in order.  The partials are loaded 64 at a time, one per lane, and broadcast lane by lane into the
+// sequential sum, instead of one dependent L2 round trip per partial.
 __device__ inline double fold(const double* __restrict__ part, int64_t row, int nb) {
+  const int lane = threadIdx.x & 63;
+  const double* pr = part + row * nb;
   double s = 0.0;
-  for (int k = 0; k < nb; ++k) s += part[row * nb + k];
+  for (int k0 = 0; k0 < nb; k0 += 64) {
+    const double v = k0 + lane < nb ? pr[k0 + lane] : 0.0;
+    const int m = nb - k0 < 64 ? nb - k0 : 64;
+    for (int j = 0; j < m; ++j) s += __shfl(v, j, 64);
+  }
   return s;
 }
 
@@ -36,6 +44,11 @@ __global__ void __launch_bounds__(kBlock) cg_dot_kernel(int64_t n, const T* __re
   if (threadIdx.x == 0) part[row * gridDim.x + blockIdx.x] = s;
 }
 
+// The streaming loads of a thread's elements lo + t, lo + t + kBlock, ... are issued kCgBatch at a time, the
+// first batch before the partial fold (alpha / beta do not gate them); the per-thread order of the sums is the
+// element order, as in cg_dot.
+constexpr int kCgBatch = 4;
+
 template <typename T>
 __global__ void __launch_bounds__(kBlock) cg_xr_kernel(int64_t n, const double* __restrict__ rr,
                                                        const double* __restrict__ part_pap, const T* __restrict__ p,
@@ -43,19 +56,41 @@ __global__ void __launch_bounds__(kBlock) cg_xr_kernel(int64_t n, const double* 
                                                        double* __restrict__ part_rr) {
   __shared__ double sh[kBlock / 64];
   const int64_t row = blockIdx.y;
-  const T alpha = (T)(rr[row] / fold(part_pap, row, gridDim.x));
   const int64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = blockIdx.x * chunk;
   const int64_t hi = lo + chunk < n ? lo + chunk : n;
   const T* pr = p + row * n;
   const T* ar = ap + row * n;
   T* xr = x + row * n;
   T* rw = r + row * n;
+  T pv[kCgBatch], av[kCgBatch], xv[kCgBatch], rv[kCgBatch];
+  auto load = [&](int64_t ib) {
+#pragma unroll
+    for (int k = 0; k < kCgBatch; ++k) {
+      const int64_t i = ib + (int64_t)k * kBlock;
+      if (i < hi) {
+        pv[k] = pr[i];
+        av[k] = ar[i];
+        xv[k] = xr[i];
+        rv[k] = rw[i];
+      }
+    }
+  };
+  const int64_t i0 = lo + threadIdx.x;
+  load(i0);
+  const T alpha = (T)(rr[row] / fold(part_pap, row, gridDim.x));
   double acc = 0.0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    xr[i] = fma(alpha, pr[i], xr[i]);            // x += alpha p
-    const T rn = fma(-alpha, ar[i], rw[i]);      // r -= alpha A p
-    rw[i] = rn;
-    acc = fma((double)rn, (double)rn, acc);
+  for (int64_t ib = i0; ib < hi; ib += (int64_t)kCgBatch * kBlock) {
+    if (ib != i0) load(ib);
+#pragma unroll
+    for (int k = 0; k < kCgBatch; ++k) {
+      const int64_t i = ib + (int64_t)k * kBlock;
+      if (i < hi) {
+        xr[i] = fma(alpha, pv[k], xv[k]);          // x += alpha p
+        const T rn = fma(-alpha, av[k], rv[k]);    // r -= alpha A p
+        rw[i] = rn;
+        acc = fma((double)rn, (double)rn, acc);
+      }
+    }
   }
   const double s = cg_block_sum(acc, sh);
   if (threadIdx.x == 0) part_rr[row * gridDim.x + blockIdx.x] = s;
@@ -68,13 +103,33 @@ __global__ void __launch_bounds__(kBlock) cg_p_kernel(int64_t n, const double* _
                                                       double* __restrict__ rr_host, unsigned* __restrict__ flags,
                                                       unsigned seq) {
   const int64_t row = blockIdx.y;
-  const double rn = fold(part_rr, row, gridDim.x);
-  const T beta = (T)(rn / rr[row]);
   const int64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = blockIdx.x * chunk;
   const int64_t hi = lo + chunk < n ? lo + chunk : n;
   const T* rw = r + row * n;
   T* pw = p + row * n;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) pw[i] = fma(beta, pw[i], rw[i]);  // p = r + beta p
+  T rv[kCgBatch], pv[kCgBatch];
+  auto load = [&](int64_t ib) {
+#pragma unroll
+    for (int k = 0; k < kCgBatch; ++k) {
+      const int64_t i = ib + (int64_t)k * kBlock;
+      if (i < hi) {
+        rv[k] = rw[i];
+        pv[k] = pw[i];
+      }
+    }
+  };
+  const int64_t i0 = lo + threadIdx.x;
+  load(i0);
+  const double rn = fold(part_rr, row, gridDim.x);
+  const T beta = (T)(rn / rr[row]);
+  for (int64_t ib = i0; ib < hi; ib += (int64_t)kCgBatch * kBlock) {
+    if (ib != i0) load(ib);
+#pragma unroll
+    for (int k = 0; k < kCgBatch; ++k) {
+      const int64_t i = ib + (int64_t)k * kBlock;
+      if (i < hi) pw[i] = fma(beta, pv[k], rv[k]);  // p = r + beta p
+    }
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     rr_out[row] = rn;
     if (rr_host) rr_host[row] = rn;
