@@ -209,9 +209,6 @@ class AbsError(pxa.StoppingCriterion):
 
     # hook: combine a device row statistic across shards (identity on one process)
     _reduce = None
-    # offer the fused PGD step a host buffer to fold its statistics into (pxa_pgd_tv2d_plan_step's last-workgroup
-    # fold): off until its flag latency is understood (r05e: ~200 us per check against 3.4 us for the fold launch)
-    _offer_sink = os.environ.get("PXA_RELERR_SINK", "0") == "1"
 
     def info(self):
         if self._val.size == 1:
@@ -316,9 +313,14 @@ class RelError(pxa.StoppingCriterion):
 
     # hook: combine a device row statistic across shards (identity on one process)
     _reduce = None
-    # offer the fused PGD step a host buffer to fold its statistics into (pxa_pgd_tv2d_plan_step's last-workgroup
-    # fold): off until its flag latency is understood (r05e: ~200 us per check against 3.4 us for the fold launch)
-    _offer_sink = os.environ.get("PXA_RELERR_SINK", "0") == "1"
+    # Offer the fused PGD step a host buffer to fold its statistics into ("__relerr_sink__" of the solver state):
+    # the step then launches the fold right behind its own launch, instead of this criterion launching it at the
+    # next check, after the host's decision on the previous one -- at stop_rate 1 that put a host hop between
+    # every step and its fold (r05q: 36 us per step, the device idle ~9 us of it).  PXA_RELERR_SINK=1 folds in
+    # the step's last workgroup instead (pxa_pgd_tv2d_plan_step's rel_values; same bits, but its flags reached
+    # the host ~200 us late on MI355X, r05e).
+    _offer_sink = True
+    _in_kernel_fold = os.environ.get("PXA_RELERR_SINK", "0") == "1"
 
     def stop_async(self, state):
         """stop() in two phases: the statistics (written by the device into pinned host memory) and the
@@ -351,7 +353,7 @@ class RelError(pxa.StoppingCriterion):
                 fb = bufs[0]
                 seq = fb.fold(h[3], h[5])
             if self._offer_sink and hasattr(state, "__setitem__"):
-                state["__relerr_sink__"] = (self._var, bufs[1] if fb is bufs[0] else bufs[0])
+                state["__relerr_sink__"] = (self._var, bufs[1] if fb is bufs[0] else bufs[0], self._in_kernel_fold)
             self._x_prev = x
             shape = x.shape[:-1]
 
