@@ -29,9 +29,9 @@ Sub-records on the same line (north_star):
         (--c3-three-launch: the three-launch step A / B / C; single GPU: replicas only at N > 1);
   "k4": SURVEY §8(d)'s "Gradient + prox" kernel alone (pxa_tv_dual_update) at 2048^2 and 1024^3;
   "dense_mfma": the dense LinOp's MFMA path (8192 x 65536 K, B = 64 / 128 right-hand sides) in TFLOP/s.
-The solver sub-records (c2_4096, c5, c4, and c3 per algorithm) carry a `cpu_baseline` (the oracle on the host's
-cores, bounded sample); the kernel-only records (k4, dense_mfma) carry rooflines instead, the oracle having no
-kernel-level equivalent of them.
+Every sub-record (c2_4096, c5, c4, c3 per algorithm, k4 per shape, dense_mfma) carries a `cpu_baseline`: the
+oracle (or, for dense_mfma, NumPy's matmul, which is the reference's dense apply) on the host's cores, a bounded
+sample whose size and scaling the record states.
 
 Roofline convention.  `frac` is the dominant kernel's time against ITS OWN compulsory bytes (every array
 it must read or write, once): the fused PGD launch reads x, x_prev, H^T y and writes x_new = 16 B/pixel.  `frac_survey` keeps SURVEY §8(d)'s 48 B/pixel figure for the same time; that model is not a
@@ -299,6 +299,55 @@ def cpu_baseline_c4(M, N, threads, steps=4, lam=0.01):
         if ctxm is not None:
             ctxm.restore_original_limits()
     return 1e3 * ((t2 - t1) - (t1 - t0)) / steps, used
+
+
+def cpu_baseline_k4(shape, budget_s, sigma=0.28, lam=0.01, rho=1.0, seed=11):
+    """K4 (the PDS dual update z <- (1 - rho) z + rho fenchel_prox_{sigma lam L1}(z + sigma Grad w), the
+    reference's Moreau form, operator.py:940-944 + diff.py Gradient + norm.py:47-52) with the oracle on one host
+    thread, on `shape`.  Returns (ms per update, updates timed, seconds)."""
+    import oracle as orc
+
+    rng = np.random.default_rng(seed)
+    n = int(np.prod(shape))
+    w = rng.standard_normal(n).astype(np.float32)
+    z = rng.standard_normal(len(shape) * n).astype(np.float32)
+    prox = lambda v, t: orc.l1_prox(v, lam * t)
+
+    def update():
+        zin = z + np.float32(sigma) * orc.gradient_apply(w, shape)
+        return np.float32(1 - rho) * z + np.float32(rho) * orc.fenchel_prox(prox, zin.astype(np.float32), sigma)
+
+    update()  # page-in
+    k, t0 = 0, time.perf_counter()
+    while k < 1 or time.perf_counter() - t0 < budget_s:
+        update()
+        k += 1
+    dt = time.perf_counter() - t0
+    return 1e3 * dt / k, k, dt
+
+
+def cpu_baseline_mfma(M, N, B, threads):
+    """dense_mfma: the dense LinOp's stacked apply Y = X K^T (base.py:334-512, NumPy's matmul on the host)
+    for B right-hand sides, fp32 BLAS on `threads` threads.  Returns (ms per apply, TFLOP/s, BLAS threads)."""
+    try:
+        from threadpoolctl import threadpool_info, threadpool_limits
+    except ImportError:  # pragma: no cover
+        threadpool_limits, threadpool_info = None, None
+    K = np.full((M, N), 0.5, dtype=np.float32)  # (BLAS time does not depend on the values)
+    X = np.full((B, N), 0.25, dtype=np.float32)
+    ctxm = threadpool_limits(limits=threads, user_api="blas") if threadpool_limits else None
+    try:
+        used = max((i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"), default=1) \
+            if threadpool_info else threads
+        X @ K.T  # page-in, BLAS warm-up
+        t0 = time.perf_counter()
+        for _ in range(3):
+            X @ K.T
+        ms = 1e3 * (time.perf_counter() - t0) / 3
+    finally:
+        if ctxm is not None:
+            ctxm.restore_original_limits()
+    return ms, 2.0 * M * N * B / (ms * 1e-3) / 1e12, used
 
 
 def cpu_baseline_c3(n, budget_s, seed=7, lam=0.01, sigma=2.0):
@@ -848,6 +897,26 @@ def sub_cpu_baselines(sub, args):
                               f"thread) on a {args.c3_cpu_n}^3 volume of the same problem: {k} iterations in {dt:.1f} s; "
                               f"{n3}^3 rate = voxel-iterations/s / {n3}^3 (every operator of the step is O(voxels)), "
                               f"on {model}"}
+    if "k4" in sub:
+        for key, shape in (("2d_2048", (2048, 2048)), ("3d_1024", (256, 256, 256))):
+            if key not in sub["k4"]:
+                continue
+            ms, k, dt = cpu_baseline_k4(shape, min(budget, 3.0))
+            full = sub["k4"][key]["shape"]
+            scale = float(np.prod(full)) / float(np.prod(shape))
+            sub["k4"][key]["cpu_baseline"] = {
+                "value": round(ms * scale, 2), "unit": "ms per update", "cores": 1, "kind": "port",
+                "sample": f"oracle dual update (Moreau-form fenchel_prox of lam L1, oracle.gradient_apply; one thread) on "
+                          f"{'x'.join(map(str, shape))}: {k} updates in {dt:.1f} s"
+                          + (f", scaled by the element count to {'x'.join(map(str, full))}" if scale != 1 else "")
+                          + f", on {model}"}
+    if "dense_mfma" in sub:
+        M, N = sub["dense_mfma"]["M"], sub["dense_mfma"]["N"]
+        ms, tf, used = cpu_baseline_mfma(M, N, 64, th)
+        sub["dense_mfma"]["cpu_baseline"] = {
+            "value": round(tf, 3), "unit": "TFLOP/s", "ms_per_apply_b64": round(ms, 2), "cores": used, "kind": "port",
+            "sample": f"NumPy X @ K.T (the reference's dense LinOp apply) for B = 64, {M}x{N} fp32 K on the host, BLAS "
+                      f"on {used} threads, 3 applies, on {model}"}
     if "c4" in sub:
         ms, used = cpu_baseline_c4(args.c4_m, args.c4_n, th)
         per_outer = sub["c4"].get("cg_iters_per_outer") or 13.0
