@@ -60,11 +60,28 @@ constexpr int kVecN = 16 / sizeof(T);
 struct PlainLoad {
   __device__ double operator()(const double* a) const { return *a; }
 };
-template <typename Load = PlainLoad>
+// WIDE (the fold kernel; not the tile kernel's own tail, where the 64 extra VGPRs spill): up to kFoldBatch *
+// kBlock partials (8 192: a 2048^2 image) every thread issues all its loads before the first add (one memory
+// round trip instead of four batches of eight; the partials were written by every XCD, so they come from the
+// Infinity Cache, not this XCD's L2), same sum order, same bits.
+constexpr int kFoldBatch = 32;
+template <bool WIDE = false, typename Load = PlainLoad>
 __device__ inline double fold_tile_stat(const double* __restrict__ pr, int64_t per_row, double* red, Load ld = Load{}) {
   double acc = 0.0;
+  if (WIDE && per_row <= (int64_t)kFoldBatch * kBlock) {
+    double v[kFoldBatch];
+#pragma unroll
+    for (int j = 0; j < kFoldBatch; ++j) {
+      const int64_t k = threadIdx.x + (int64_t)j * kBlock;
+      v[j] = k < per_row ? ld(pr + 2 * k) : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < kFoldBatch; ++j)
+      if (threadIdx.x + (int64_t)j * kBlock < per_row) acc += v[j];
+  } else {
 #pragma unroll 8
-  for (int64_t k = threadIdx.x; k < per_row; k += kBlock) acc += ld(pr + 2 * k);
+    for (int64_t k = threadIdx.x; k < per_row; k += kBlock) acc += ld(pr + 2 * k);
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(kBlock) tile_partials_fold_kernel(int64_t rows
   __shared__ double red[kBlock / kWave];
   const int64_t q = blockIdx.x;  // q = stat * rows + row
   const int64_t stat = q / rows, r = q - stat * rows;
-  const double t = fold_tile_stat(part + 2 * r * per_row + stat, per_row, red);
+  const double t = fold_tile_stat<true>(part + 2 * r * per_row + stat, per_row, red);
   if (threadIdx.x == 0) {
     out[q] = t;
     if (flags != nullptr) {  // completion flag of this statistic, ordered after its value system-wide

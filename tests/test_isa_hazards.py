@@ -81,3 +81,35 @@ def test_no_store_data_hazard_in_shipped_kernels(tmp_path):
         dis = subprocess.run([LLVM, "-d", "--mcpu=gfx950", str(co)], check=True, capture_output=True, text=True).stdout
         found += [(co.name, s, n) for s, n in store_data_hazards(dis.splitlines())]
     assert not found, found[:8]
+
+
+def _kernel_notes(tmp_path):
+    """(name, metadata text) of every kernel in the library's gfx950 code objects."""
+    out = []
+    for co in _code_objects(tmp_path):
+        notes = subprocess.run([LLVM.replace("llvm-objdump", "llvm-readelf"), "--notes", str(co)], check=True,
+                               capture_output=True, text=True).stdout
+        for ent in re.split(r"\n\s+- \.agpr_count:", notes):
+            m = re.search(r"\.name:\s+(\S+)", ent)
+            if m:
+                out.append((m.group(1), ent))
+    return out
+
+
+@pytest.mark.skipif(not (os.path.exists(LLVM) and os.path.exists(LIB)), reason="needs the ROCm toolchain and the built library")
+def test_hot_kernels_do_not_spill(tmp_path):
+    """The PGD tile kernel (fp32, radius 6: the headline), the fp32 radius-6 look-ahead PDS kernels and the dense normal
+    operator keep their registers: a scratch spill there costs more than any of their round-5 A/B variants won
+    (a shared helper once pulled 64 extra VGPRs into the tile kernel's tail and spilled 14).  SGPR spills, which
+    land in VGPR lanes, not in memory, are allowed (kernel D has 10-14)."""
+    hot = ("pgd_tv2d_kernelIfLi6", "pds_march_kernelIfLi6", "pds_plane_kernelIfLi6", "normal_group_kernel")
+    seen = {}
+    for name, ent in _kernel_notes(tmp_path):
+        for h in hot:
+            if h in name:
+                v = re.search(r"\.vgpr_spill_count:\s+(\d+)", ent)
+                sg = re.search(r"\.sgpr_spill_count:\s+(\d+)", ent)
+                seen[name] = (int(v.group(1)) if v else 0, int(sg.group(1)) if sg else 0)
+    assert any("pgd_tv2d_kernelIfLi6" in n for n in seen), "tile kernel not found"
+    spilled = {n[:80]: v for n, v in seen.items() if v[0] != 0}  # VGPR spills go to scratch memory
+    assert not spilled, spilled
