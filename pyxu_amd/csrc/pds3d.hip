@@ -35,10 +35,37 @@
 //
 // Parity: the step follows the reference's arithmetic per voxel except that G x replaces
 // S^T (S x - y) + ... (same operator, different fp32 rounding order: see pgd_tv2d.hip).
+#include <atomic>
+#include <map>
+#include <mutex>
+
 #include "pds_march.hpp"
 
 namespace pxa {
 namespace pds {
+
+// kernel D's soft-coupling counters (pds_march.hpp): per device, grown on demand, zeroed once
+unsigned* progress_counters(int64_t units) {
+  static std::mutex mu;
+  static std::map<int, std::pair<unsigned*, int64_t>> bufs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  auto& b = bufs[dev];
+  if (b.second < units) {
+    unsigned* p = nullptr;
+    if (hipMalloc((void**)&p, (size_t)units * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, (size_t)units * sizeof(unsigned)) != hipSuccess) return nullptr;
+    // (the previous, smaller buffer stays allocated: a kernel still in flight may use it)
+    b = {p, units};
+  }
+  return b.first;
+}
+
+unsigned next_progress_tag() {
+  static std::atomic<unsigned> n{0};
+  return ((n.fetch_add(1) % 65535u) + 1u) << 16;
+}
 
 // ------------------------------------------------------------------ kernel C: dual update
 template <typename T>

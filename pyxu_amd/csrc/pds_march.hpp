@@ -23,11 +23,41 @@ template <typename T>
 struct PdsD {
   PdsA<T> a;  // march parameters: geometry, axis-0 taps, tau, prox, segments
   T sigma, lam, rho, omr;
+  // soft progress coupling of row neighbours (PXA_TUNE_PDS_MARCH bit 2, A/B; prog == nullptr: off): per unit a
+  // counter (launch tag << 16 | planes done) in prog[(s nseg + segment) blocks + blk]; bpr = blocks per row
+  unsigned* prog;
+  unsigned tag;
+  int bpr, lag, nseg, blocks;
 };
+
+// Soft coupling (see PdsD): thread 0 publishes the unit's progress every second plane; the first lane of each
+// wavefront then reads the row - 1 and row + 1 neighbours' counters and, while one of them has started in this
+// launch (same tag) and lags more than `lag` planes behind, sleeps -- at most kCoupleSpins times per check, so
+// that progress never depends on a neighbour being resident.  Only L2 reuse depends on it, not correctness.
+constexpr int kCoupleSpins = 64;
+__device__ __forceinline__ void couple_wait(unsigned* prog, unsigned tag, unsigned me, int64_t up, int64_t dn, int done,
+                                            int lag) {
+  if (threadIdx.x == 0) __hip_atomic_store(prog + me, tag | (unsigned)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((threadIdx.x & 63) == 0) {
+    for (int spin = 0; spin < kCoupleSpins; ++spin) {
+      bool wait = false;
+      if (up >= 0) {
+        const unsigned v = __hip_atomic_load(prog + up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wait |= (v & 0xFFFF0000u) == tag && (int)(v & 0xFFFFu) + lag < done;
+      }
+      if (dn >= 0) {
+        const unsigned v = __hip_atomic_load(prog + dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wait |= (v & 0xFFFF0000u) == tag && (int)(v & 0xFFFFu) + lag < done;
+      }
+      if (!wait) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+}
 
 // One work unit of kernel D: in-plane block `blk` (kAThreads * NP consecutive positions) of axis-0 segment `segi`
 // of volume `s`, marched over the segment's planes (+ the G0 halo planes).
-template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT>
+template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT, bool CP = false>
 __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict__ w, const T* __restrict__ z,
                                            const T* __restrict__ src, T* __restrict__ zo, T* __restrict__ ao,
                                            T* __restrict__ q, unsigned blk, int segi, int64_t s) {
@@ -259,8 +289,13 @@ __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict
     // windows held as shift registers: one copy of the plane body.  rv[t] = v at plane qp - 2 R0 + t;
     // rh[t] = (H0 v) at plane qp - 3 R0 + t.  (Static ring slots as in pds_axis0_kernel, i.e. the plane
     // body unrolled RING times, measured no faster: profiles/r03z_pds_march_ring_ab.txt.)
+    const bool couple = CP && p.prog != nullptr;  // (CP: a separate instance, so the default keeps its SGPRs)
+    const int64_t cbase = (s * p.nseg + segi) * (int64_t)p.blocks;
+    const int64_t cup = couple && blk >= (unsigned)p.bpr ? cbase + blk - p.bpr : -1;
+    const int64_t cdn = couple && (int64_t)blk + p.bpr < p.blocks ? cbase + blk + p.bpr : -1;
 #pragma unroll 1
     for (int qp = first; qp <= last; ++qp) {
+      if (couple && ((qp - first) & 1) == 0) couple_wait(p.prog, p.tag, (unsigned)(cbase + blk), cup, cdn, qp - first, p.lag);
 #pragma unroll
       for (int t = 0; t + 1 < RING; ++t)
 #pragma unroll
@@ -317,7 +352,7 @@ __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict
 // r05c): HBM fetch 25.7 -> 23.8 GiB per launch (1.29 -> 1.19 x compulsory), but kernel D 8.8 -> 11.0 ms (PD3O)
 // and 10.2 -> 12.0 ms (Condat-Vu): the marches running in lockstep cost more than the re-fetched rows, so the
 // default stays one workgroup per unit, dispatched as slots free up.
-template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT>
+template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT, bool CP = false>
 __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T* __restrict__ w,
                                                               const T* __restrict__ z, const T* __restrict__ src,
                                                               T* __restrict__ zo, T* __restrict__ ao,
@@ -325,12 +360,17 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
                                                               unsigned units) {
   for (unsigned u = blockIdx.x; u < units; u += gridDim.x) {
     const unsigned r = u % blocks, rest = u / blocks;
-    march_unit<T, R0, NP, PD3O, ISO, DUAL, NT>(p, w, z, src, zo, ao, q, xcd_tile(r, blocks), (int)(rest % nseg),
+    march_unit<T, R0, NP, PD3O, ISO, DUAL, NT, CP>(p, w, z, src, zo, ao, q, xcd_tile(r, blocks), (int)(rest % nseg),
                                                (int64_t)(rest / nseg));
   }
 }
 
 // ------------------------------------------------------------------ host side
+// The coupling's counters: one device buffer per device, grown on demand and zeroed once (tags make old contents
+// harmless); launch tags 1..65535 in turn (0 never matches: a zeroed counter reads as "not started").
+unsigned* progress_counters(int64_t units);
+unsigned next_progress_tag();
+
 template <typename T, int R0, bool PD3O, bool ISO, bool DUAL>
 int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, const void* z, const void* src, void* zo,
              void* ao, void* q, hipStream_t st) {
@@ -345,11 +385,33 @@ int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, cons
   auto kern = np == 2 ? pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL, true> : pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true>;
   // grid: one workgroup per unit (PXA_TUNE_PDS_MARCH bit 1: the resident capacity, persistent; see above)
   unsigned grid = (unsigned)units;
+  PdsD<T> pdc = pd;
+  pdc.prog = nullptr;
+  const int64_t bpr = pd.a.g.n2 % ((int64_t)kAThreads * np) == 0 ? pd.a.g.n2 / ((int64_t)kAThreads * np) : 0;
+  // (the coupled instance exists for the C3 configuration only: fp32, radius 6, one position per thread)
+  constexpr bool kCoupled = std::is_same<T, float>::value && R0 == 6 && DUAL;
+  if (kCoupled && (tuning(PXA_TUNE_PDS_MARCH) & 4) && bpr > 0 && np == 1) {
+    pdc.prog = progress_counters(units);
+    if (pdc.prog == nullptr) return PXA_ERR_ARG;
+    pdc.tag = next_progress_tag();
+    pdc.bpr = (int)bpr;
+    pdc.lag = 2 + (tuning(PXA_TUNE_PDS_MARCH) >> 3);  // planes a neighbour may lag (bits 3+: extra slack)
+    pdc.nseg = nseg;
+    pdc.blocks = (int)blocks;
+  }
   if (tuning(PXA_TUNE_PDS_MARCH) & 2) {
     const unsigned cap = (unsigned)resident_grid((const void*)kern, kAThreads, 0);
     if (grid > cap) grid = cap;
   }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kAThreads), 0, st, pd, (const T*)w, (const T*)z, (const T*)src, (T*)zo,
+  if constexpr (kCoupled) {
+    if (pdc.prog != nullptr) {
+      hipLaunchKernelGGL((pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true, true>), dim3(grid), dim3(kAThreads), 0, st,
+                         pdc, (const T*)w, (const T*)z, (const T*)src, (T*)zo, (T*)ao, (T*)q, (unsigned)blocks,
+                         (unsigned)nseg, (unsigned)units);
+      return last_launch_status();
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kAThreads), 0, st, pdc, (const T*)w, (const T*)z, (const T*)src, (T*)zo,
                      (T*)ao, (T*)q, (unsigned)blocks, (unsigned)nseg, (unsigned)units);
   return last_launch_status();
 }

@@ -47,6 +47,18 @@ if [ "$S" = "admm" ]; then
   step c4trace 300 rocprofv3 --kernel-trace --stats -d $P/c4 -o run --output-format csv -- python3 bench.py --only c4
   python3 scripts/c4_timeline.py $P/c4 > $O/c4timeline.log 2>&1 || true
 fi
+if [ "$S" = "couple" ]; then
+  step ctests 600 $PT -m gpu tests/test_gpu_pds_fused.py -k "coupled or persistent or lookahead_matches"
+  step c3base 300 python3 bench.py --only c3
+  PXA_TUNE=7=4 step c3c0 300 python3 bench.py --only c3
+  PXA_TUNE=7=68 step c3c8 300 python3 bench.py --only c3
+  PXA_TUNE=7=20 step c3c2 300 python3 bench.py --only c3
+  step c3base2 300 python3 bench.py --only c3
+  B3="python3 bench.py --only c3 --c3-steps 3"
+  PXA_TUNE=7=4 step fetchc3c 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetchc3c -o run --output-format csv -- $B3
+  PXA_TUNE=7=4 step writec3c 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writec3c -o run --output-format csv -- $B3
+  python3 scripts/pmc_traffic.py $P/fetchc3c $P/writec3c "pds_march_kernel<float, 6, 1, true, false, true, true, true>" pds_march_kernel_pd3o_coupled@1024^3 $P/traffic_c3c.json $T || true
+fi
 if [ "$S" = "a" ]; then
   step pgdtests 600 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_long_trajectories.py tests/test_gpu_small_weights.py -k "pgd or c2 or c5"
   step drvnew 120 $DRV

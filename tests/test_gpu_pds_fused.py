@@ -302,3 +302,23 @@ def test_pds_lookahead_persistent_grid_bit_exact(algo):
         _dev.tuning(_dev.TUNE_PDS_MARCH, prev)
     for k in a:
         assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+@pytest.mark.parametrize("slack", [0, 8])
+def test_pds_lookahead_coupled_march_bit_exact(algo, slack):
+    """Kernel D with the soft progress coupling of row neighbours (PXA_TUNE_PDS_MARCH bit 2; bits 3+ widen the
+    allowed lag) gives the default launch's bits: the coupling only delays workgroups, it never changes what
+    they compute.  256-wide rows (one block per row) and 512-wide ones (two), more units than resident
+    workgroups, so some neighbours are not resident when others wait for them (the bounded spin)."""
+    for shape in ((40, 256, 256), (24, 128, 512)):
+        case = (shape, 2.0, "iso", "pos", np.float32, False)
+        x0 = np.random.default_rng(9).uniform(0, 1, int(np.prod(shape))).astype(np.float32)
+        a = _run(algo, case, 4, True, x0)
+        prev = _dev.tuning(_dev.TUNE_PDS_MARCH, 4 | (slack << 3))
+        try:
+            b = _run(algo, case, 4, True, x0)
+        finally:
+            _dev.tuning(_dev.TUNE_PDS_MARCH, prev)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (shape, k)
