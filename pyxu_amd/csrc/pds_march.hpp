@@ -30,28 +30,30 @@ struct PdsD {
   int bpr, lag, nseg, blocks;
 };
 
-// Soft coupling (see PdsD): thread 0 publishes the unit's progress every second plane; the first lane of each
-// wavefront then reads the row - 1 and row + 1 neighbours' counters and, while one of them has started in this
-// launch (same tag) and lags more than `lag` planes behind, sleeps -- at most kCoupleSpins times per check, so
-// that progress never depends on a neighbour being resident.  Only L2 reuse depends on it, not correctness.
+// Soft coupling (see PdsD): every second plane thread 0 publishes the unit's progress (a vector store), then the
+// wavefront reads the row - 1 / row + 1 neighbours' counters through the scalar unit (glc: from the XCD's L2,
+// where a same-XCD neighbour's write-through store lands; a vector load would wait for every vector load and
+// store in flight, i.e. drain the march: r05z2, 2 x the kernel time even with no waiting) and, while a neighbour
+// that has started in this launch (same tag) lags more than `lag` planes behind, sleeps -- at most kCoupleSpins
+// times, so that progress never depends on a neighbour being resident.  Only L2 reuse depends on the coupling,
+// not correctness.
 constexpr int kCoupleSpins = 64;
-__device__ __forceinline__ void couple_wait(unsigned* prog, unsigned tag, unsigned me, int64_t up, int64_t dn, int done,
+__device__ __forceinline__ unsigned couple_read(const unsigned* a) {
+  unsigned v;
+  asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ bool couple_lags(unsigned v, unsigned tag, int done, int lag) {
+  return (v & 0xFFFF0000u) == tag && (int)(v & 0xFFFFu) + lag < done;
+}
+__device__ __forceinline__ void couple_step(unsigned* prog, unsigned tag, unsigned me, int64_t up, int64_t dn, int done,
                                             int lag) {
   if (threadIdx.x == 0) __hip_atomic_store(prog + me, tag | (unsigned)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if ((threadIdx.x & 63) == 0) {
-    for (int spin = 0; spin < kCoupleSpins; ++spin) {
-      bool wait = false;
-      if (up >= 0) {
-        const unsigned v = __hip_atomic_load(prog + up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        wait |= (v & 0xFFFF0000u) == tag && (int)(v & 0xFFFFu) + lag < done;
-      }
-      if (dn >= 0) {
-        const unsigned v = __hip_atomic_load(prog + dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        wait |= (v & 0xFFFF0000u) == tag && (int)(v & 0xFFFFu) + lag < done;
-      }
-      if (!wait) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
+  for (int spin = 0; spin < kCoupleSpins; ++spin) {
+    const bool wait = (up >= 0 && couple_lags(couple_read(prog + up), tag, done, lag)) ||
+                      (dn >= 0 && couple_lags(couple_read(prog + dn), tag, done, lag));
+    if (!wait) break;
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
@@ -295,7 +297,7 @@ __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict
     const int64_t cdn = couple && (int64_t)blk + p.bpr < p.blocks ? cbase + blk + p.bpr : -1;
 #pragma unroll 1
     for (int qp = first; qp <= last; ++qp) {
-      if (couple && ((qp - first) & 1) == 0) couple_wait(p.prog, p.tag, (unsigned)(cbase + blk), cup, cdn, qp - first, p.lag);
+      if (couple && ((qp - first) & 1) == 0) couple_step(p.prog, p.tag, (unsigned)(cbase + blk), cup, cdn, qp - first, p.lag);
 #pragma unroll
       for (int t = 0; t + 1 < RING; ++t)
 #pragma unroll
