@@ -34,6 +34,17 @@
 // contiguous band of tiles so that halo re-reads of x / x_prev hit its own L2.
 #include "tile2d.hpp"
 
+// Wave priority (s_setprio) of the window-load phase: its loads issue ahead of the passes of the other
+// workgroups resident on the SIMD, so that the next round's windows are in flight sooner (r06b, interleaved A/B:
+// 2048^2 24.4 -> 23.4 us; C5 and 4096^2 unchanged within noise; priority 3 or also raising the epilogue's
+// H^T y loads gave the same).  Scheduling only: the same bits.
+#ifndef PXA_PGD_PRIO
+#define PXA_PGD_PRIO 1
+#endif
+#ifndef PXA_PGD_PRIO_EPI
+#define PXA_PGD_PRIO_EPI 0  // (A/B builds: the epilogue's H^T y loads too)
+#endif
+
 // Measurement probes (s_memtime phase trace, skip probes, staggered starts: PXA_TUNE_PGD_DIAG /
 // PXA_TUNE_PGD_STAGGER) exist only in the probe build (`make -C pyxu_amd/csrc probe`, scripts/ that time
 // kernel phases); the production library compiles them out, so its kernel carries no probe branch.
@@ -439,11 +450,17 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     if (tracing && (tid & 63) == 0) ts[(tid >> 6) * 8 + pt] = clock64();
   };
   tmark(0);
+#if PXA_PGD_PRIO
+  __builtin_amdgcn_s_setprio(PXA_PGD_PRIO);  // the window loads issue ahead of other workgroups' passes
+#endif
   if (kProbes && (p.diag & 128)) {  // timing probe only (WRONG results): no window loads, yk = 0
     for (int i = tid; i < L::AR * L::AP; i += kThreads) A[i] = T(0);
   } else {
     load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
   }
+#if PXA_PGD_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   tmark(1);
   __syncthreads();
   tmark(2);
@@ -476,7 +493,13 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
 #pragma unroll
       for (int w = 0; w < kVecN<T>; ++w) hb.v[s][w] = T(0);
   } else {
+#if PXA_PGD_PRIO_EPI
+    __builtin_amdgcn_s_setprio(PXA_PGD_PRIO_EPI);
+#endif
     load_staged<T, R, EDGE>(p, ty0, tx0, bs, hb.v);  // in flight during the O staging
+#if PXA_PGD_PRIO_EPI
+    __builtin_amdgcn_s_setprio(0);
+#endif
   }
   tmark(5);
   __syncthreads();  // every G1 sweep is done with PT: O may overwrite it
