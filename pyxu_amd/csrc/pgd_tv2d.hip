@@ -35,7 +35,7 @@
 #include "tile2d.hpp"
 
 // Wave priority (s_setprio) of the window-load phase: its loads issue ahead of the passes of the other
-// workgroups resident on the SIMD, so that the next round's windows are in flight sooner (r06b, interleaved A/B:
+// workgroups resident on the SIMD, so that the next round's windows are in flight sooner (r05zb, interleaved A/B:
 // 2048^2 24.4 -> 23.4 us; C5 and 4096^2 unchanged within noise; priority 3 or also raising the epilogue's
 // H^T y loads gave the same).  Scheduling only: the same bits.
 #ifndef PXA_PGD_PRIO
