@@ -35,14 +35,18 @@
 #include "tile2d.hpp"
 
 // Wave priority (s_setprio) of the window-load phase: its loads issue ahead of the passes of the other
-// workgroups resident on the SIMD, so that the next round's windows are in flight sooner (r05zb, interleaved A/B:
-// 2048^2 24.4 -> 23.4 us; C5 and 4096^2 unchanged within noise; priority 3 or also raising the epilogue's
-// H^T y loads gave the same).  Scheduling only: the same bits.
+// workgroups resident on the SIMD, so that the next round's windows are in flight sooner.  Interleaved A/B
+// (profiles/r05zb_pgd_prio_ab.txt): 2048^2 24.4 -> 23.4 us on one box, no change on another (r05zc); C5 and
+// 4096^2 unchanged within noise; priority 2 or 3, or also raising the epilogue, gave the same.  Scheduling
+// only: the same bits.
 #ifndef PXA_PGD_PRIO
 #define PXA_PGD_PRIO 1
 #endif
 #ifndef PXA_PGD_PRIO_EPI
 #define PXA_PGD_PRIO_EPI 0  // (A/B builds: the epilogue's H^T y loads too)
+#endif
+#ifndef PXA_PGD_PRIO_FIN
+#define PXA_PGD_PRIO_FIN 0  // (A/B builds: the finishing row-major epilogue)
 #endif
 
 // Measurement probes (s_memtime phase trace, skip probes, staggered starts: PXA_TUNE_PGD_DIAG /
@@ -527,6 +531,9 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   if (want_part) load_staged<T, R, EDGE>(p, ty0, tx0, xrs, hb.x);
   __syncthreads();
   tmark(6);
+#if PXA_PGD_PRIO_FIN
+  __builtin_amdgcn_s_setprio(PXA_PGD_PRIO_FIN);  // A/B builds: the finishing stores ahead of other passes
+#endif
   {
     int r0, cq;
     S::lane(tid, r0, cq);
