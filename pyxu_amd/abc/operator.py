@@ -500,7 +500,10 @@ class QuadraticFunc(ProxDiffFunc):
         slvr, stop_crit = self._prox_cg(tau)
         # = slvr.fit(b=b, stop_crit=stop_crit), no side files
         slvr._solve_inline(b=b, stop_crit=stop_crit, **({} if preset is None else {"_preset": preset}))
-        return slvr.solution()
+        # = slvr.solution() (CG: the state's x), without the history flush stats() does first: nobody reads an
+        # inline sub-solve's history, and flushing its ~13 deferred records cost ~50 us between ADMM's x-update
+        # and the rest of its step (C4 device timeline, r05zd)
+        return slvr._mstate["x"]
 
     def asloss(self, data=None):
         from pyxu_amd.operator.func.loss import shift_loss

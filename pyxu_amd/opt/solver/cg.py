@@ -27,18 +27,26 @@ class _HostRows:
     behind an event: the host waits for it only where it branches on the value (the ||r||^2 <= eps test
     of the next step), by which time that step's A p, <p, A p> and x update are already queued."""
 
-    def __init__(self, dev):
+    def __init__(self, dev, pool=None):
+        """pool: a solver's list of reusable (pinned buffer, event) slots, taken round robin (a pinned allocation
+        and an event per statistic cost ~10 us of host time at every CG set-up and explicit-residual step)."""
         import torch
 
         self.dev = dev
-        self._h = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True)
+        slot = None
+        if pool is not None:
+            pool[1] = (pool[1] + 1) % len(pool[0])
+            slot = pool[0][pool[1]]
+            if slot is None or slot[0].shape != dev.shape or slot[0].dtype != dev.dtype:
+                slot = pool[0][pool[1]] = (torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True), torch.cuda.Event())
+        self._h, self._ev = slot if slot is not None else (torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True),
+                                                            torch.cuda.Event())
         self._h.copy_(dev, non_blocking=True)
-        self._ev = torch.cuda.Event()
         _dev.record_event(self._ev)
 
     def host(self):
         _dev.wait_event(self._ev)
-        return self._h.numpy()
+        return self._h.numpy().copy()  # (the pinned slot is reused later)
 
 
 class _KernelRows(_HostRows):
@@ -119,7 +127,7 @@ class CG(pxa.Solver):
         # launches A p0 before that check, so the device works while the host decides
         r = mst["residual"]
         ahead = _preset[3:] if _preset is not None and len(_preset) == 5 else None
-        hr0 = ahead[0] if ahead else _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)))
+        hr0 = ahead[0] if ahead else _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)), self._hr_pool())
         self._rr = (hr0, r)  # ||r||^2 of the current residual (then carried from the previous step's beta)
         mst[_ROWSTAT] = {"residual": (r, 2, hr0)}
         self._Ap_next = None  # A p of the current p, launched ahead of the stop check (see m_step)
@@ -134,7 +142,7 @@ class CG(pxa.Solver):
         up yet (the first solve)."""
         if getattr(self, "_apply_key", None) != (tuple(p0.shape), p0.dtype, str(p0.device)):
             return None
-        return _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r0))), self._apply_p(p0)
+        return _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r0)), self._hr_pool()), self._apply_p(p0)
 
     def _make_apply(self, like):
         """A.apply, or -- when A = s K^T K + d I for one dense K (ADMM's QuadraticFunc.prox operator,
@@ -188,6 +196,14 @@ class CG(pxa.Solver):
                 return Ap
         return self._apply(p)
 
+    def _hr_pool(self):
+        """Four (pinned buffer, event) slots for _HostRows, round robin: a statistic is read by the stop check
+        and the step after it, long before its slot comes round again."""
+        pool = self.__dict__.get("_hr_slots")
+        if pool is None:
+            pool = self._hr_slots = [[None] * 4, 0]
+        return pool
+
     def _cg_workspace(self, rows):
         import torch
 
@@ -219,7 +235,7 @@ class CG(pxa.Solver):
         if self._rr is not None and self._rr[1] is r:
             rr = self._rr[0]  # ||r||^2 of this r: the previous step's beta numerator (identical bits)
         else:
-            rr = _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)))
+            rr = _HostRows(_dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r)), self._hr_pool())
         self._rr = None
         eps = pxrt.Width(np.dtype(str(x.dtype).replace("torch.", ""))).eps()
         rr_host = rr.host()  # already waited for by the stop check of this iteration (same value)
@@ -251,7 +267,7 @@ class CG(pxa.Solver):
             _dev.axpby(0.0, p, 1.0, r, out=p)  # beta = 0
         else:
             rr_new = _dev.row_reduce(_dev.RED_SUMSQ, _rows2d(r))
-            hr = _HostRows(rr_new)  # async copy of ||r'||^2, event recorded before beta / p / A p'
+            hr = _HostRows(rr_new, self._hr_pool())  # async copy of ||r'||^2, event recorded before beta / p / A p'
             beta = _dev.row_ratio(rr_new, rr.dev, p)
             _dev.axpy_rows(beta, 1.0, _rows2d(p), _rows2d(r), out=_rows2d(p))  # p = r + beta p
             self._rr = (hr, r)
