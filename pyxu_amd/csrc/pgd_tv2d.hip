@@ -221,6 +221,104 @@ __device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T*
   }
 }
 
+// ---- TV dual once per pixel (fp32 lane map of pass B; PXA_PGD_TVX=0 builds the 5 x 3 window path for A/B).  Pass B's item (4 rows x 2
+// columns) needs q at its own 8 pixels, q0 one row above and q1 one column to the left; the default path
+// evaluates q on the 5 x 3 window (15 per item, 1.9 x per pixel).  Here an item evaluates its own 8, writes
+// its last row's q0 and last column's q1 to an exchange area in A's rows that pass B no longer reads, lanes
+// 0..47 of the wavefront evaluate the wavefront's halo (16 q0 of the tile row above, 32 q1 of the column to the
+// left of the wavefront's 16 columns), and every item reads its neighbours' values back.  Same q expressions,
+// same bits.  Within one wavefront (items (a, cb) of a wavefront: all 8 row groups x 8 column items) LDS
+// accesses execute in order, so no barrier is needed.  Interleaved A/B (r05zj, profiles/r05zj_pgd_tvx_ab.txt):
+// bit-identical at 2048^2 and 1000 x 1500; kernel 23.5 -> 23.3 us at 2048^2, C5 0.657 -> 0.651 ms, 4096^2 76.6 ->
+// 72.9 us: the VALU saved is partly spent on the exchange's LDS traffic.
+#ifndef PXA_PGD_TVX
+#define PXA_PGD_TVX 1
+#endif
+constexpr int kTvxFloats = 9 * 16 + 9 * 32;  // per wavefront: q0 [row group + 1][16 cols], q1 [col item + 1][32 rows]
+
+template <typename T, int R, bool EDGE>
+__device__ inline void tv_exchange(const PgdParams<T>& p, T* A, int ty0, int tx0, int tid, int a, int cb,
+                                   T (&yc)[kVecN<T>][2], T (&tv)[kVecN<T>][2]) {
+  using L = Layout<T, R>;
+  constexpr int V = L::V;
+  constexpr int CA = L::CA;
+  const int n0 = p.n0, n1 = p.n1;
+  const int lane = tid & 63, wv = tid >> 6, cbl = cb & 7;
+  const int c0 = 2 * cb;
+  // own rows (window rows 1..V) and the row below, columns c0 .. c0 + 2
+  T y[V + 1][3];
+#pragma unroll
+  for (int r = 0; r <= V; ++r) {
+    const T* arow = A + (V * a + r + 2 * R) * L::AP + CA + c0;
+    T mid[2], hi[2];
+    ld_pair<T>(arow, mid);
+    ld_pair<T>(arow + 2, hi);
+    y[r][0] = mid[0];
+    y[r][1] = mid[1];
+    y[r][2] = hi[0];
+  }
+#pragma unroll
+  for (int u = 0; u < V; ++u)
+#pragma unroll
+    for (int w = 0; w < 2; ++w) yc[u][w] = y[u][w];
+  if (!p.tv) return;
+  auto qat = [&](T yc_, T ydn, T yrt, int gr, int gc, T& q0, T& q1) {
+    const T v0 = fma(p.g0a, yc_, p.g0b * ydn);
+    const T v1 = fma(p.g1a, yc_, p.g1b * yrt);
+    T w = tv_weight<T>(fma(v0, v0, v1 * v1), p.lam, p.mu, p.inv_mu);
+    if (EDGE && !(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) w = T(0);
+    q0 = v0 * w;
+    q1 = v1 * w;
+  };
+  T q0[V][2], q1[V][2];
+#pragma unroll
+  for (int u = 0; u < V; ++u)
+#pragma unroll
+    for (int w = 0; w < 2; ++w)
+      qat(y[u][w], y[u + 1][w], y[u][w + 1], ty0 + V * a + u, tx0 + c0 + w, q0[u][w], q1[u][w]);
+  // exchange area of this wavefront: waves 0, 1 in A's top dead rows, 2, 3 in the bottom ones
+  T* E = A + (wv < 2 ? 0 : (TY + 2 * R + 1) * L::AP) + (wv & 1) * kTvxFloats;
+  T* E0 = E;            // [a + 1][col within the wavefront's 16]
+  T* E1 = E + 9 * 16;   // [col item + 1][row]
+  // halo of the wavefront: lanes 0..15 the q0 of tile row -1 (its 16 columns), lanes 16..47 the q1 of the column
+  // left of its first column (tile rows 0..31)
+  if (lane < 48) {
+    T hq0, hq1;
+    if (lane < 16) {
+      const int tc = 16 * wv + lane;
+      const T* r0 = A + (2 * R - 1) * L::AP + CA + tc;
+      qat(r0[0], r0[L::AP], r0[1], ty0 - 1, tx0 + tc, hq0, hq1);
+      E0[lane] = hq0;
+    } else {
+      const int j = lane - 16, tc = 16 * wv - 1;
+      const T* r0 = A + (j + 2 * R) * L::AP + CA + tc;
+      qat(r0[0], r0[L::AP], r0[1], ty0 + j, tx0 + tc, hq0, hq1);
+      E1[j] = hq1;
+    }
+  }
+  {
+    const T b[2] = {q0[V - 1][0], q0[V - 1][1]};
+    st_vec<T, 2>(E0 + (a + 1) * 16 + 2 * cbl, b);
+    const T c[4] = {q1[0][1], q1[1][1], q1[2][1], q1[3][1]};
+    st_vec<T, 4>(E1 + (cbl + 1) * 32 + 4 * a, c);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  T up[2], left[4];
+  ld_vec<T, 2>(E0 + a * 16 + 2 * cbl, up);
+  ld_vec<T, 4>(E1 + cbl * 32 + 4 * a, left);
+#pragma unroll
+  for (int u = 0; u < V; ++u)
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const T qa = u == 0 ? up[w] : q0[u - 1][w];
+      const T ql = w == 0 ? left[u] : q1[u][0];
+      const T t0 = fma(p.g0b, qa, p.g0a * q0[u][w]);
+      const T t1 = fma(p.g1b, ql, p.g1a * q1[u][w]);
+      tv[u][w] = t0 + t1;
+    }
+}
+
 // ---- pass B: G1 along rows + Grad^T q, handed per output row-run to
 // `emit(k, u, gr, gc, g, yc)`: g = (G yk + Grad^T q) at row gr, columns gc .. gc + CW - 1 of item k,
 // yc = yk there.  The emitter finishes the pixels in place (finish_run) or stages g for the
@@ -277,7 +375,11 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
       };
       T yc[V][CW];  // yk at the item's own pixels
       T tv[V][CW];
-      {
+      constexpr bool kX = PXA_PGD_TVX && sizeof(T) == 4 && L::NA == 8 && CW == 2 && KB == 1 &&
+                          (2 * R - 1) * L::AP >= kTvxFloats * 2;
+      if constexpr (kX) {
+        tv_exchange<T, R, EDGE>(p, const_cast<T*>(A), ty0, tx0, tid, a, cb, yc, tv);
+      } else {
         T yr[CW + 2], yn[CW + 2];
         yrow(0, yr);
         yrow(1, yn);
