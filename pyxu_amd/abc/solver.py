@@ -537,18 +537,31 @@ class Solver:
         hist = ast["history"]
         msgs = []
         run, run_dtype = [], None
+        run_logs = []  # (index in run of the record the line shows, iteration, stamp)
+
+        def line(stamp, it, names, values):
+            return "\n".join([f"[{stamp}] Iteration {it:>_d}"] + [f"\t{f}: {v}" for f, v in zip(names, values)])
 
         def close_run():
+            # one structured array per run of same-layout records; the run's log lines are formatted from its
+            # columns as Python scalars (f"{v}" of a NumPy scalar is f"{v.item()}": same text as record by record,
+            # at a third of the cost -- at stop_rate 1 every step writes one)
             if run:
+                names = run_dtype.names
                 try:
                     arr = np.array(run, dtype=run_dtype)
+                    cols = [arr[n].tolist() for n in names] if run_logs else None
                 except (TypeError, ValueError):  # non-scalar info() values: field by field, as numpy assigns them
                     arr = np.zeros(len(run), dtype=run_dtype)
                     for i, r in enumerate(run):
-                        for name, v in zip(run_dtype.names, r):
+                        for name, v in zip(names, r):
                             arr[i][name] = v
+                    cols = None
                 hist.append(arr)
+                for k, it, stamp in run_logs:
+                    msgs.append(line(stamp, it, names, [c[k] for c in cols] if cols is not None else arr[k]))
                 run.clear()
+                run_logs.clear()
 
         for it, data, stamp, ftype, log in items:
             if data is not None:
@@ -560,13 +573,12 @@ class Solver:
                     close_run()
                     run_dtype = dtype
                 run.append((it, *data.values()))
-            if log:
-                close_run()
-                h = hist[-1][-1]
-                lines = [f"[{stamp}] Iteration {it:>_d}"]
-                for field, value in zip(h.dtype.names, h):
-                    lines.append(f"\t{field}: {value}")
-                msgs.append("\n".join(lines))
+            if log:  # the line shows the newest history record
+                if run:
+                    run_logs.append((len(run) - 1, it, stamp))
+                else:
+                    h = hist[-1][-1]
+                    msgs.append(line(stamp, it, h.dtype.names, h))
         close_run()
         if msgs:
             self._log_lines(msgs, flush)
