@@ -475,6 +475,12 @@ int pxa_pgd_tv2d_plan(int dtype, int64_t stack, int64_t y_images, int64_t n0, in
 int pxa_pgd_tv2d_plan_step(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
                            const void* hty, void* x_new, double* partials, const void* x_ref, double* rel_values,
                            uint32_t* rel_flags, uint32_t seq, void* stream);
+/* As pxa_pgd_tv2d_plan_step with rel_values / rel_flags required, the fold done by a pxa_tile_partials_fold
+ * launch enqueued right behind the step (same bits as the in-kernel fold, flags seen ~3 us after the step
+ * instead of the last workgroup's late write-back): the stop_rate-1 path, one C call per iteration. */
+int pxa_pgd_tv2d_plan_step_fold(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
+                                const void* hty, void* x_new, double* partials, const void* x_ref, double* rel_values,
+                                uint32_t* rel_flags, uint32_t seq, void* stream);
 int pxa_pgd_tv2d_plan_free(void* plan);
 int pxa_pgd_tv2d_last_kernel(void);
 /* Diagnostics: s_memtime stamps of the tile kernel's last launch under PXA_TUNE_PGD_DIAG bit 5

@@ -971,13 +971,16 @@ class PgdPlan:
                                     float(lam), float(mu), int(prox), ct.byref(h)), "pxa_pgd_tv2d_plan")
         self._h = h.value
         self._fn = lib.pxa_pgd_tv2d_plan_step
+        self._fn_fold = lib.pxa_pgd_tv2d_plan_step_fold
         self._free = lib.pxa_pgd_tv2d_plan_free
 
-    def step(self, x, x_prev, hty, x_new, a, tau, prox_w, partials=None, x_ref=None, sink=None, seq=0):
-        """One iteration; with `sink` (a HostFlagBuffer of (2, rows) values) the launch also folds its partials
-        there under publication `seq`."""
+    def step(self, x, x_prev, hty, x_new, a, tau, prox_w, partials=None, x_ref=None, sink=None, seq=0,
+             fold_launch=False):
+        """One iteration; with `sink` (a HostFlagBuffer of (2, rows) values) its partials are also folded there
+        under publication `seq`: by the launch's last workgroup, or with `fold_launch` by a fold launch enqueued
+        behind it in the same C call (pxa_pgd_tv2d_plan_step_fold)."""
         ev = _TIMER.begin() if _TIMER is not None else None  # measurement hook (bench.py), normally None
-        r = self._fn(self._h, float(a), float(tau), float(prox_w), x.data_ptr(), x_prev.data_ptr(), hty.data_ptr(),
+        r = (self._fn_fold if fold_launch else self._fn)(self._h, float(a), float(tau), float(prox_w), x.data_ptr(), x_prev.data_ptr(), hty.data_ptr(),
                      x_new.data_ptr(), partials.data_ptr() if partials is not None else None,
                      x_ref.data_ptr() if x_ref is not None else None, sink.vptr if sink is not None else None,
                      sink.fptr if sink is not None else None, int(seq), stream())

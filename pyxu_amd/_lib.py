@@ -88,6 +88,7 @@ EXPORTS = {
     "pxa_pgd_tv2d_plan": (i32, [i32, i64, i64, i64, i64, i32, P_i32, P_f64, i32, P_i32, P_f64, f64, f64, f64, f64, i32,
                                 ct.POINTER(vp)]),
     "pxa_pgd_tv2d_plan_step": (i32, [vp, f64, f64, f64, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp]),
+    "pxa_pgd_tv2d_plan_step_fold": (i32, [vp, f64, f64, f64, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp]),
     "pxa_pgd_tv2d_plan_free": (i32, [vp]),
     "pxa_pgd_tv2d_step": (
         i32,

@@ -488,8 +488,8 @@ __device__ inline void finish_vec(const PgdParams<T>& p, int gr, int gc, const T
 #pragma unroll
       for (int w = 0; w < V; ++w) {
         const double dd = (double)xo[w] - (double)xv[w];
-        part_d += dd * dd;
-        part_x += (double)xv[w] * (double)xv[w];
+        part_d = fma(dd, dd, part_d);  // explicit: the vector and scalar paths must contract alike
+        part_x = fma((double)xv[w], (double)xv[w], part_x);
       }
     }
   } else if (gr < n0) {
@@ -499,8 +499,8 @@ __device__ inline void finish_vec(const PgdParams<T>& p, int gr, int gc, const T
         xns[(int64_t)gr * n1 + gc + w] = xo[w];
         if (want_part) {
           const double dd = (double)xo[w] - (double)xv[w];
-          part_d += dd * dd;
-          part_x += (double)xv[w] * (double)xv[w];
+          part_d = fma(dd, dd, part_d);
+          part_x = fma((double)xv[w], (double)xv[w], part_x);
         }
       }
     }
@@ -930,6 +930,20 @@ int pxa_pgd_tv2d_plan_step(void* plan, double a, double tau, double prox_w, cons
                           seq, pl->counter, as_stream(stream));
   return pgd_run<double>(pl->pd, pl->R, a, tau, prox_w, x, x_prev, hty, x_new, partials, x_ref, rel_values, rel_flags, seq,
                          pl->counter, as_stream(stream));
+}
+
+int pxa_pgd_tv2d_plan_step_fold(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
+                                const void* hty, void* x_new, double* partials, const void* x_ref, double* rel_values,
+                                uint32_t* rel_flags, uint32_t seq, void* stream) {
+  PXA_CHECK_ARG(plan != nullptr && partials != nullptr && rel_values != nullptr && rel_flags != nullptr);
+  const PgdPlan* pl = (const PgdPlan*)plan;
+  const int64_t stack = pl->dtype == PXA_F32 ? pl->pf.stack : pl->pd.stack;
+  const int64_t rows = stack / (pl->dtype == PXA_F32 ? pl->pf.y_images : pl->pd.y_images);
+  const int64_t per_row = (int64_t)(pl->dtype == PXA_F32 ? pl->pf.ntiles : pl->pd.ntiles) * (kThreads / 64) / rows;
+  const int e = pxa_pgd_tv2d_plan_step(plan, a, tau, prox_w, x, x_prev, hty, x_new, partials, x_ref, nullptr, nullptr,
+                                       0, stream);
+  if (e != PXA_OK) return e;
+  return pxa_tile_partials_fold(rows, per_row, partials, rel_values, rel_flags, seq, stream);
 }
 
 int pxa_pgd_tv2d_plan_free(void* plan) {

@@ -155,13 +155,13 @@ class PGD(pxa.Solver):
             sink = mst.pop("__relerr_sink__", None) if want else None
             in_kernel = sink is not None and sink[0] == "x" and len(sink) > 2 and bool(sink[2])
             sink = sink[1] if sink is not None and sink[0] == "x" else None
-            seq = sink.next_seq() if in_kernel else 0
+            # the fold: in the launch's last workgroup (PXA_RELERR_SINK=1), else a fold launch right behind it,
+            # enqueued by the same C call (a side stream for it, so that it ran beside the next launch, cost more
+            # host time in the event record / wait than it saved: r05s)
+            seq = sink.next_seq() if sink is not None else 0
             p["plan"].step(x, xp, p["hty"], out, a, tau, tau * p["prox_scale"], partials=parts,
-                           x_ref=None if xref is x else xref, sink=sink if in_kernel else None, seq=seq)
-            if sink is not None and not in_kernel:
-                # the fold launch right behind this one (a side stream for it, so that it ran beside the next
-                # launch, cost more host time in the event record / wait than it saved: r05s)
-                seq = sink.fold(parts, p["tiles_per_row"])
+                           x_ref=None if xref is x else xref, sink=sink, seq=seq,
+                           fold_launch=sink is not None and not in_kernel)
             if want:  # (var, x_new, the x the statistics are relative to, partials, rows, tiles per row, folded)
                 mst["__relerr__"] = ("x", out, xref, parts, p["rows"], p["tiles_per_row"],
                                      (sink, seq) if sink is not None else None)

@@ -161,11 +161,13 @@ def test_fused_relerr_matches_separate_pass(stack, rows, stop_rate):
 
 @pytest.mark.parametrize("case", [((2048, 2048), 1, 1), ((128, 192), 6, 2), ((40, 36), 2, 2)],
                          ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}")
-def test_in_kernel_fold_matches_fold_kernel(case):
+@pytest.mark.parametrize("fold_launch", [False, True], ids=["in_kernel", "step_fold"])
+def test_in_kernel_fold_matches_fold_kernel(case, fold_launch):
     """pxa_pgd_tv2d_plan_step with a RelError sink: the workgroup that finishes last folds the partials into the
     host buffer with its completion flags -- the same bits as pxa_tile_partials_fold on the same partials, the
     same x_new as a launch without the fold, and the device counter is reset for the next launch (two launches
-    in a row both publish)."""
+    in a row both publish).  pxa_pgd_tv2d_plan_step_fold (the fold launched behind the step by the same C
+    call): the same."""
     sh, stack, y_images = case
     s = _plan(sh, stack, y_images, 2.0, "pos")
     m, p = s._mstate, s._plan
@@ -177,7 +179,8 @@ def test_in_kernel_fold_matches_fold_kernel(case):
         parts = _parts(s)
         seq = sink.next_seq()
         out = _dev.empty_like(x)
-        p["plan"].step(x, xp, hty, out, 0.37, m["tau"], m["tau"] * p["prox_scale"], partials=parts, sink=sink, seq=seq)
+        p["plan"].step(x, xp, hty, out, 0.37, m["tau"], m["tau"] * p["prox_scale"], partials=parts, sink=sink, seq=seq,
+                       fold_launch=fold_launch)
         sink.wait(seq)
         got = sink.values.copy()
         ref = _dev.empty_f64((2, rows), x)
