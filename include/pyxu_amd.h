@@ -5,11 +5,22 @@
  * Every entry point is a plain `extern "C"` function over raw device pointers and sizes:
  *   - returns 0 on success, a HIP error code (>0) or a PXA_ERR_* code (<0) on failure
  *     (pxa_error_string() gives a message); no exception crosses the ABI;
- *   - the caller owns every buffer (device pointers, e.g. torch-ROCm `data_ptr()`), the library never
- *     allocates persistent device memory; scratch space is passed in explicitly;
+ *   - the caller owns every buffer (device pointers, e.g. torch-ROCm `data_ptr()`); scratch space is
+ *     passed in explicitly.  The compute entry points never allocate device memory and never
+ *     synchronise, so they are graph-capturable, including the first call on a new FFT length (its
+ *     twiddle table lives in static device memory of the library and is filled by a kernel enqueued on
+ *     the caller's stream: tests/test_gpu_fft.py::test_fft_graph_capture_cold_length).  The exceptions,
+ *     all outside the compute calls or behind measurement knobs:
+ *       * pxa_pgd_tv2d_plan() allocates the plan's 4-byte device counter (released by
+ *         pxa_pgd_tv2d_plan_free()); call it before a capture, then capture pxa_pgd_tv2d_plan_step();
+ *       * pxa_host_alloc() / pxa_host_free() allocate / release coherent host memory (their purpose);
+ *       * pxa_tuning(PXA_TUNE_PDS_MARCH, bit 2), the opt-in coupled kernel-D variant of A/B runs,
+ *         allocates its progress counters on first use;
+ *       * pxa_pds_kernel_ms() and pxa_pgd_tile_trace() (measurement hooks) wait for recorded events /
+ *         copy a device symbol to the host;
  *   - `stream` is a hipStream_t (NULL = legacy default stream); launches are asynchronous;
- *   - functions are stateless and re-entrant (safe from Pyxu's solver worker thread,
- *     reference src/pyxu/abc/solver.py:710-718) and graph-capturable (no alloc/sync inside);
+ *   - functions are re-entrant (safe from Pyxu's solver worker thread, reference
+ *     src/pyxu/abc/solver.py:710-718);
  *   - arrays are C-contiguous, laid out exactly as the reference's NDArrays: a leading stack of
  *     independent problems followed by the row-major flattening of `arg_shape`
  *     (reference src/pyxu/operator/linop/stencil/stencil.py:441-461).

@@ -235,7 +235,12 @@ def _tuning_from_env():
     spec = os.environ.get("PXA_TUNE", "").strip()
     for item in filter(None, (t.strip() for t in spec.split(","))):
         k, _, v = item.partition("=")
-        tuning(int(k), int(v))
+        try:
+            tuning(int(k), int(v))
+        except (ValueError, TypeError, RuntimeError) as e:  # a malformed item must not break the import
+            import warnings
+
+            warnings.warn(f"PXA_TUNE: ignoring {item!r} ({e})", RuntimeWarning, stacklevel=2)
 
 
 def empty(shape, like):
@@ -659,7 +664,17 @@ class HostFlagBuffer:
         return self.values.reshape(2, self.rows)
 
     def next_seq(self):
+        """A new publication number, for a kernel about to be launched on the CURRENT stream: that stream is
+        remembered with it, so that wait() asks the publishing stream (not whichever stream is current by
+        then) whether the publication can still land."""
         self.seq = (self.seq % 0xFFFFFFFE) + 1
+        global _RAW_STREAM
+        if _RAW_STREAM is None:
+            _RAW_STREAM = _raw_stream_fn()
+        streams = self.__dict__.setdefault("_streams", {})
+        streams[self.seq] = int(_RAW_STREAM() or 0)  # the raw handle: ~10x cheaper than a torch stream object
+        if len(streams) > 16:
+            streams.pop(next(iter(streams)))
         return self.seq
 
     def fold(self, parts, per_row):
@@ -674,7 +689,17 @@ class HostFlagBuffer:
         instead of spinning forever when the stream has drained without publishing `seq` (an earlier
         kernel faulted, the publishing kernel never ran, or `seq` was overwritten by a later publication);
         an asynchronous device error surfaces through the stream query."""
-        wait_flags(self.flags, seq, spin_s, lambda: _torch().cuda.current_stream().query())
+        raw = self.__dict__.get("_streams", {}).get(seq)
+
+        def idle():  # only asked once the spin has expired: building the stream object here costs nothing
+            torch = _torch()
+            if raw is None:  # a sequence number this buffer did not hand out: the current stream is all we know
+                return torch.cuda.current_stream().query()
+            if raw == 0:
+                return torch.cuda.default_stream().query()
+            return torch.cuda.ExternalStream(raw).query()
+
+        wait_flags(self.flags, seq, spin_s, idle)
 
     def __del__(self):
         if getattr(self, "_ptr", None):

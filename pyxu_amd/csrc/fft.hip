@@ -18,6 +18,7 @@
 #include <cmath>
 #include <map>
 #include <mutex>
+#include <set>
 #include <utility>
 #include <vector>
 
@@ -680,26 +681,6 @@ __global__ void __launch_bounds__(TH, 4) fft_lds_kernel(FftPlan p, const Cx<T>* 
   run_lines(std::true_type{}, lf_out, store_lines);
 }
 
-// Stage twiddle tables of a power-of-two plan: the stage of span ns and radix R reads w_{ns R}^k, k < ns,
-// at tw[ns + k] (the spans are distinct powers of two, so the ranges [ns, 2 ns) do not overlap; n entries
-// in all).  exp(-2 pi i k / (ns R)) in long double on the host, then rounded to T (correctly rounded for
-// fp32 and, but for ties at the 2^-64 level, for fp64).
-template <typename T>
-void fill_twiddle_table(const FftPlan& p, std::vector<Cx<T>>& tw) {
-  const int64_t n = p.n;
-  tw.assign((size_t)n, Cx<T>{T(1), T(0)});
-  int64_t ns = 1;
-  for (int s = 0; s < p.nst; ++s) {
-    const int R = p.radix[s];
-    if (ns > 1)
-      for (int64_t k = 0; k < ns && ns + k < n; ++k) {
-        const long double a = 2.0L * 3.141592653589793238462643383279502884L * (long double)k / (long double)(ns * R);
-        tw[(size_t)(ns + k)] = Cx<T>{(T)cosl(a), (T)(-sinl(a))};
-      }
-    ns *= R;
-  }
-}
-
 // out[i] = a[i] * b[i % nb] (b conjugated if CONJ): spectrum product of an FFT convolution
 template <typename T, bool CONJ>
 __global__ void __launch_bounds__(kBlock) cmul_kernel(int64_t n, int64_t nb, const Cx<T>* __restrict__ a,
@@ -808,31 +789,83 @@ int launch_stockham(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream
   return last_launch_status();
 }
 
-// Twiddle table of length n, in device memory of the current device: built once per (device, n, T) on the
-// host and uploaded with a synchronous hipMemcpy, then kept for the process (a few KB per length).  Keyed by
-// the device ordinal, so a process that drives several GPUs never passes one device's table to another; no
-// stream is touched (no hipStreamSynchronize that would break a stream capture in progress -- the first call
-// for a length must still happen outside a capture, since it allocates).
+// Twiddle tables of the power-of-two in-LDS kernel, in static device memory of the code object (no allocation at
+// run time): the table of length n occupies [n, 2n) of g_tw_f32 / g_tw_f64 (n <= LdsFft<T, 1024>::E: 16384 fp32,
+// 8192 fp64; 256 KB each).  The first call for a length (per device) enqueues tw_fill_kernel on the caller's
+// stream and marks the table built; calls during a stream capture enqueue the fill into the graph every time and
+// mark nothing (the graph may never run), so pxa_fft_ex is graph-capturable on a length never seen before
+// (tests/test_gpu_fft.py::test_fft_graph_capture_cold_length).  No allocation, no synchronisation: a concurrent
+// first use of one length on a second stream must be ordered after the first by the caller, as for any buffer.
+constexpr int kTwMaxF32 = 16384, kTwMaxF64 = 8192;
+__device__ Cx<float> g_tw_f32[2 * kTwMaxF32];
+__device__ Cx<double> g_tw_f64[2 * kTwMaxF64];
+
 template <typename T>
-const Cx<T>* twiddle_table(const FftPlan& p) {
+constexpr int tw_max() {
+  return sizeof(T) == 4 ? kTwMaxF32 : kTwMaxF64;
+}
+template <typename T>
+__device__ inline Cx<T>* tw_store();
+template <>
+__device__ inline Cx<float>* tw_store<float>() {
+  return g_tw_f32;
+}
+template <>
+__device__ inline Cx<double>* tw_store<double>() {
+  return g_tw_f64;
+}
+
+// Stage twiddles: the stage of span ns and radix R reads w_{ns R}^k, k < ns, at tw[ns + k] (the spans are
+// distinct powers of two, so the ranges [ns, 2 ns) do not overlap; n entries in all, the rest 1 + 0i).
+// exp(-2 pi i k / (ns R)) from sincospi of the exact dyadic argument 2k / (ns R) in double, rounded to T
+// (fp32: correctly rounded but for results within an fp64 ulp of a rounding boundary; fp64: ~1 ulp).
+template <typename T>
+__global__ void __launch_bounds__(256) tw_fill_kernel(FftPlan p) {
+  const int64_t n = p.n;
+  Cx<T>* tw = tw_store<T>() + n;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    Cx<T> w{T(1), T(0)};
+    int64_t ns = 1;
+    for (int s = 0; s < p.nst; ++s) {
+      const int R = p.radix[s];
+      if (ns > 1 && j >= ns && j < 2 * ns) {
+        double sn, cs;
+        sincospi(2.0 * (double)(j - ns) / (double)(ns * R), &sn, &cs);
+        w = Cx<T>{(T)cs, (T)(-sn)};
+      }
+      ns *= R;
+    }
+    tw[j] = w;
+  }
+}
+
+template <typename T>
+const Cx<T>* twiddle_table(const FftPlan& p, hipStream_t st) {
+  if (p.n > tw_max<T>()) return nullptr;
   static std::mutex mu;
-  static std::map<std::pair<int, int64_t>, Cx<T>*> tables;
+  static std::map<int, Cx<T>*> bases;       // device address of the table store, per device
+  static std::set<std::pair<int, int64_t>> built;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  const std::pair<int, int64_t> key{dev, p.n};
   std::lock_guard<std::mutex> lock(mu);
-  auto it = tables.find(key);
-  if (it != tables.end()) return it->second;
-  std::vector<Cx<T>> host;
-  fill_twiddle_table<T>(p, host);
-  Cx<T>* tw = nullptr;
-  if (hipMalloc((void**)&tw, host.size() * sizeof(Cx<T>)) != hipSuccess) return nullptr;
-  if (hipMemcpy(tw, host.data(), host.size() * sizeof(Cx<T>), hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(tw);
-    return nullptr;
+  auto bi = bases.find(dev);
+  if (bi == bases.end()) {
+    void* a = nullptr;
+    const hipError_t e = sizeof(T) == 4 ? hipGetSymbolAddress(&a, HIP_SYMBOL(g_tw_f32))
+                                        : hipGetSymbolAddress(&a, HIP_SYMBOL(g_tw_f64));
+    if (e != hipSuccess || a == nullptr) return nullptr;
+    bi = bases.emplace(dev, (Cx<T>*)a).first;
   }
-  tables[key] = tw;
-  return tw;
+  const std::pair<int, int64_t> key{dev, p.n};
+  if (!built.count(key)) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess) return nullptr;
+    const unsigned blocks = (unsigned)((p.n + 255) / 256);
+    hipLaunchKernelGGL(tw_fill_kernel<T>, dim3(blocks), dim3(256), 0, st, p);
+    if (hipGetLastError() != hipSuccess) return nullptr;
+    if (cap == hipStreamCaptureStatusNone) built.insert(key);
+  }
+  return bi->second + p.n;
 }
 
 template <typename T>
@@ -884,8 +917,8 @@ int launch_lds_fft_th(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, const C
 template <typename T>
 int launch_lds_fft(FftPlan p, bool inv, const Cx<T>* src, Cx<T>* dst, hipStream_t st) {
   if (!factor_lds<T>(p.n, p)) return PXA_ERR_UNSUPPORTED;
-  const Cx<T>* tw = twiddle_table<T>(p);
-  if (tw == nullptr) return launch_stockham<T>(p, inv, src, dst, st);  // no memory for the table
+  const Cx<T>* tw = twiddle_table<T>(p, st);
+  if (tw == nullptr) return launch_stockham<T>(p, inv, src, dst, st);  // (no table for this length)
   return lds_fft_threads<T>(p) == 1024 ? launch_lds_fft_th<T, 1024>(p, inv, src, dst, tw, st)
                                        : launch_lds_fft_th<T, 512>(p, inv, src, dst, tw, st);
 }

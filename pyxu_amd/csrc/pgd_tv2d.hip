@@ -662,6 +662,13 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   }
 }
 
+// (Opt-in: PXA_RELERR_SINK=1; gfx950-specific.)  The hand-off below uses no release / acquire: it is the first row
+// of the measured write-through hand-off table of MI355X_MICROARCH.md ("Workgroup dispatch, XCD placement &
+// inter-workgroup visibility": one lane per storing workgroup signals with an agent-scope atomic add behind every
+// storing wave's s_waitcnt vmcnt(0) and a workgroup barrier; all payload stores and loads are sc1, i.e. relaxed
+// agent-scope atomics; the workgroup whose add returned last reads).  That form is measured on gfx950 / ROCm 7.2,
+// not an architectural guarantee of the HIP memory model, which is why the mode stays opt-in and the default fold is
+// a separate launch (pxa_tile_partials_fold); A/B numbers with the mode on depend on it.
 // The RelError statistics of this launch, folded by the workgroup that finishes last (saves the fold launch
 // of a stop check: ~3.4 us of device time plus a launch gap per step at stop_rate 1).  No fences: a
 // device-scope release fence writes back the whole L2 of the XCD, per workgroup.  Instead every wavefront's
@@ -908,11 +915,14 @@ int pxa_pgd_tv2d_plan(int dtype, int64_t stack, int64_t y_images, int64_t n0, in
     e = pgd_params<float>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, prox, pl->pf, pl->R);
   else if (dtype == PXA_F64)
     e = pgd_params<double>(stack, y_images, n0, n1, nt0, off0, coef0, nt1, off1, coef1, h0, h1, lam, mu, prox, pl->pd, pl->R);
-  if (e == PXA_OK) {
-    e = (int)hipMalloc((void**)&pl->counter, sizeof(unsigned));
-    if (e == PXA_OK) e = (int)hipMemset(pl->counter, 0, sizeof(unsigned));
+  if (e == PXA_OK) {  // HIP failures: the positive hipError_t (the header's convention: HIP codes > 0, PXA_ERR_* < 0)
+    hipError_t he = hipMalloc((void**)&pl->counter, sizeof(unsigned));
+    if (he != hipSuccess) pl->counter = nullptr;
+    else he = hipMemset(pl->counter, 0, sizeof(unsigned));
+    if (he != hipSuccess) e = (int)he > 0 ? (int)he : PXA_ERR_UNSUPPORTED;
   }
   if (e != PXA_OK) {
+    if (pl->counter) (void)hipFree(pl->counter);
     delete pl;
     return e;
   }

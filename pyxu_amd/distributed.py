@@ -79,12 +79,26 @@ def shard_range(n, rank=None, world_size=None, group=None):
     return lo, lo + q + (1 if rank < rem else 0)
 
 
+def collectives_at_world1():
+    """True when ``PXA_DIST_COLLECTIVES=always``: the collectives below run even in a world of one
+    process instead of short-circuiting.  A one-GPU box can then drive the RCCL path end to end
+    (a world-size-1 ``nccl`` group: ``tests/test_gpu_rccl.py``); the results must not change."""
+    import os
+
+    return os.environ.get("PXA_DIST_COLLECTIVES", "").lower() == "always"
+
+
+def _initialised():
+    dist = _dist()
+    return dist.is_available() and dist.is_initialized()
+
+
 def allreduce(t, op="sum", group=None):
-    """In-place all-reduce of tensor `t` over `group` (no-op on one process).  Device tensors go
-    through RCCL, host tensors through gloo; the reduction order is the library's (fixed for a
-    given world size)."""
+    """In-place all-reduce of tensor `t` over `group` (no-op on one process, unless
+    :func:`collectives_at_world1`).  Device tensors go through RCCL, host tensors through gloo; the
+    reduction order is the library's (fixed for a given world size)."""
     rank, w = world(group)
-    if w == 1:
+    if w == 1 and not (collectives_at_world1() and _initialised()):
         return t
     dist = _dist()
     ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
@@ -108,7 +122,7 @@ def gather_slabs(x_local, n_global, group=None):
     import torch
 
     rank, w = world(group)
-    if w == 1:
+    if w == 1 and not (collectives_at_world1() and _initialised()):
         return x_local
     # the pad below copies by raw pointer and all_gather needs dense storage: permuted / strided views of a
     # slab are made contiguous first

@@ -28,8 +28,10 @@ class _HostRows:
     of the next step), by which time that step's A p, <p, A p> and x update are already queued."""
 
     def __init__(self, dev, pool=None):
-        """pool: a solver's list of reusable (pinned buffer, event) slots, taken round robin (a pinned allocation
-        and an event per statistic cost ~10 us of host time at every CG set-up and explicit-residual step)."""
+        """pool: a solver's list of reusable [pinned buffer, event, generation] slots, taken round robin (a pinned
+        allocation and an event per statistic cost ~10 us of host time at every CG set-up and explicit-residual
+        step).  A slot is re-taken only after len(pool) newer statistics; host() checks the slot's generation,
+        so an object whose slot was re-taken before it was read raises instead of returning the newer value."""
         import torch
 
         self.dev = dev
@@ -38,13 +40,19 @@ class _HostRows:
             pool[1] = (pool[1] + 1) % len(pool[0])
             slot = pool[0][pool[1]]
             if slot is None or slot[0].shape != dev.shape or slot[0].dtype != dev.dtype:
-                slot = pool[0][pool[1]] = (torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True), torch.cuda.Event())
-        self._h, self._ev = slot if slot is not None else (torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True),
-                                                            torch.cuda.Event())
+                slot = pool[0][pool[1]] = [torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True),
+                                           torch.cuda.Event(), 0]
+            slot[2] += 1
+        else:
+            slot = [torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True), torch.cuda.Event(), 1]
+        self._slot, self._gen = slot, slot[2]
+        self._h, self._ev = slot[0], slot[1]
         self._h.copy_(dev, non_blocking=True)
         _dev.record_event(self._ev)
 
     def host(self):
+        if self._slot[2] != self._gen:
+            raise RuntimeError("CG row statistic read after its pinned slot was reused by a newer one")
         _dev.wait_event(self._ev)
         return self._h.numpy().copy()  # (the pinned slot is reused later)
 

@@ -66,14 +66,19 @@ def instrument(solver) -> None:
     Idempotent: a solver fitted twice is wrapped once."""
     prof, dbg = enabled(), debug_sync()
     if not (prof or dbg):
-        orig = solver.__dict__.pop("_pxa_m_step_orig", None)
-        if orig is not None:  # flags cleared since the last fit: restore the plain method
-            solver.__dict__.pop("m_step", None)
+        saved = solver.__dict__.pop("_pxa_m_step_orig", None)
+        if saved is not None:  # flags cleared since the last fit: restore what m_step was before wrapping
+            orig, was_instance_attr = saved
+            if was_instance_attr:
+                solver.m_step = orig  # an instance-level override the solver had of its own
+            else:
+                solver.__dict__.pop("m_step", None)  # the class method again
         return
-    orig = solver.__dict__.get("_pxa_m_step_orig")
-    if orig is None:
-        orig = solver.m_step
-        solver._pxa_m_step_orig = orig
+    saved = solver.__dict__.get("_pxa_m_step_orig")
+    if saved is None:
+        saved = (solver.m_step, "m_step" in solver.__dict__)
+        solver._pxa_m_step_orig = saved
+    orig = saved[0]
     name = type(solver).__name__
 
     def m_step():

@@ -1,0 +1,52 @@
+# usage: bash scripts/gpu_r06.sh <tag> <stage>
+# GPU calls of round 6.  Stages:
+#   new    the tests added / touched this round, the default driver bench line, a kernel trace of the headline
+#   full   the whole -m gpu suite + smoke
+#   bench  the default bench line (all sub-records)
+#   prof   rocprofv3 kernel trace (--stats) of the headline + the PGD PMC passes (traffic, occupancy, waits)
+#   c3prof / k4prof  kernel traces + traffic PMC passes of the C3 / K4 legs
+# Test failures (rc 1) do not stop the run; any other failure (fault, abort, timeout) ends it there.
+set -o pipefail
+T=${1:-r06}
+S=${2:-new}
+O=gpurun_out/$T
+mkdir -p $O
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>: run with a time limit; stop the script unless rc in {0, 1}
+  local name=$1 lim=$2; shift 2
+  echo "== $name"
+  timeout -k 10 $lim "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -3 $O/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+PT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+P=$O/prof
+mkdir -p $P
+DRV="python3 bench.py --steps 20 --warmup 5 --no-sub --cpu-seconds 0"
+export PXA_FAIL_DIR=$O/fail
+pmc_pgd() {  # the headline's PGD counters, one pass each (separate runs: FETCH / WRITE / SQ)
+  step pgdfetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/pgdfetch -o run --output-format csv -- $DRV
+  step pgdwrite 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/pgdwrite -o run --output-format csv -- $DRV
+  step pgdsq 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS --kernel-trace -d $P/pgdsq -o run --output-format csv -- $DRV
+  step pgdsq2 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES --kernel-trace -d $P/pgdsq2 -o run --output-format csv -- $DRV
+}
+if [ "$S" = "new" ]; then
+  step newtests 900 $PT -m gpu tests/test_gpu_rccl.py tests/test_gpu_fft.py tests/test_gpu_solver_engine.py \
+       tests/test_gpu_admm_fused.py tests/test_gpu_dense_normal.py tests/test_gpu_distributed.py
+  step drv1 120 $DRV
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+fi
+if [ "$S" = "full" ]; then
+  step pytest 1200 $PT tests -m gpu
+  step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$S" = "bench" ]; then
+  step bench 1000 python bench.py --steps 20 --warmup 5
+fi
+if [ "$S" = "prof" ]; then
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+  pmc_pgd
+fi
+echo done

@@ -16,18 +16,25 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-def _init(rank, world, port):
+def _init(rank, world, port, backend="gloo"):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: the rank's device must be bound before the group is created
+        import torch
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     return dist
 
 
 def run(rank, world, port, scenario, q, kwargs):
     try:
-        dist = _init(rank, world, port)
+        kwargs = dict(kwargs)
+        dist = _init(rank, world, port, kwargs.pop("_backend", "gloo"))
         out = globals()[scenario](rank, world, **kwargs)
         q.put((rank, out))
         dist.barrier()
@@ -286,6 +293,92 @@ def gpu_row_sharded_admm(rank, world, M, N, n_iter):
             s1 = pxs.ADMM(f=f1, h=lam * pxo.L1Norm(dim=N), show_progress=False)
             s1.fit(x0=to_device(np.zeros(N, np.float32)), tau=tau, stop_crit=pxst.MaxIter(n_iter))
             out["x_ref"] = to_NUMPY(s1.solution())
+    return out
+
+
+def gpu_rccl_world1(rank, world, B, sh, iters, eps, M, N, n_iter):
+    """The RCCL (``nccl`` backend) path of pyxu_amd.distributed on ONE GPU: a world-size-1 group with
+    PXA_DIST_COLLECTIVES=always, so that every collective the sharded solvers issue is a real RCCL call on
+    device buffers.  Returns the sharded results next to the unsharded ones, the collectives seen and
+    whether librccl is mapped into the process."""
+    import torch
+    import torch.distributed as dist
+
+    import pyxu_amd.abc as pxa
+    import pyxu_amd.distributed as pd
+    import pyxu_amd.operator as pxo
+    import pyxu_amd.opt.solver as pxs
+    import pyxu_amd.opt.stop as pxst
+    import pyxu_amd.runtime as pxrt
+    from pyxu_amd.util import to_device, to_NUMPY
+
+    assert str(dist.get_backend()).lower() == "nccl" and pd.collectives_at_world1()
+    calls = []
+    ar0, ag0 = dist.all_reduce, dist.all_gather
+
+    def all_reduce(t, *a, **k):
+        calls.append(("all_reduce", bool(t.is_cuda)))
+        return ar0(t, *a, **k)
+
+    def all_gather(lst, t, *a, **k):
+        calls.append(("all_gather", bool(t.is_cuda)))
+        return ag0(lst, t, *a, **k)
+
+    dist.all_reduce, dist.all_gather = all_reduce, all_gather
+    out = {}
+    # C5: batched PGD (fused kernel) with the global RelError all-reduced through RCCL vs the plain RelError
+    rng = np.random.default_rng(13)
+    n = int(np.prod(sh))
+    ys = rng.standard_normal((B, n)).astype(np.float32)
+    lam, mu = 0.02, 0.01
+
+    def solve(crit):
+        with pxrt.Precision(pxrt.Width.SINGLE):
+            H = pxo.Gaussian(arg_shape=(B, *sh), sigma=(0, 2.0, 2.0))
+            G = pxo.Gradient(arg_shape=(B, *sh), directions=(1, 2))
+            f = 0.5 * pxo.SquaredL2Norm(dim=B * n).asloss(to_device(ys.reshape(-1))) * H + \
+                lam * pxo.L21Norm(arg_shape=(2, B, *sh)).moreau_envelope(mu) * G
+            f.diff_lipschitz = 1 + 8 * lam / mu
+            s = pxs.PGD(f=f, g=pxo.PositiveOrthant(dim=B * n), show_progress=False)
+            s.fit(x0=to_device(np.zeros(B * n, np.float32)), stop_crit=pxst.MaxIter(iters) | crit)
+            assert s._plan is not None
+            _, hist = s.stats()
+            return s.solution(), int(hist["iteration"][-1])
+
+    k0 = len(calls)
+    x_sh, it_sh = solve(pd.ShardedRelError(eps=eps))
+    out["pgd_collectives"] = calls[k0:]
+    x_ref, it_ref = solve(pxst.RelError(eps=eps))
+    g = pd.gather_slabs(x_sh.reshape(B, n), B)
+    out.update(pgd_x=to_NUMPY(x_sh), pgd_x_ref=to_NUMPY(x_ref), pgd_it=it_sh, pgd_it_ref=it_ref, gathered=to_NUMPY(g),
+               gathered_is_cuda=bool(g.is_cuda))
+    # C4: RowShardedLinOp (adjoint = local adjoint + RCCL all-reduce) and ADMM through its sharded normal operator
+    rng = np.random.default_rng(17)
+    K = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float32)
+    xs = np.zeros(N, np.float32)
+    xs[rng.choice(N, 8, replace=False)] = rng.standard_normal(8)
+    y = (K @ xs).astype(np.float32)
+    z = rng.standard_normal((3, M)).astype(np.float32)
+    with pxrt.Precision(pxrt.Width.SINGLE):
+        Ks = pd.RowShardedLinOp(to_device(K.copy()), M)
+        Kf = pxa.LinOp.from_array(to_device(K))
+        k0 = len(calls)
+        out["adj_sharded"] = to_NUMPY(Ks.adjoint(to_device(z)))
+        out["adj_collectives"] = calls[k0:]
+        out["adj_ref"] = to_NUMPY(Kf.adjoint(to_device(z)))
+        f = 0.5 * pxo.SquaredL2Norm(dim=M).asloss(to_device(y)) * Ks
+        s = pxs.ADMM(f=f, h=0.05 * pxo.L1Norm(dim=N), show_progress=False)
+        k0 = len(calls)
+        s.fit(x0=to_device(np.zeros(N, np.float32)), tau=1.0, stop_crit=pxst.MaxIter(n_iter))
+        out["admm_collectives"] = len(calls) - k0
+        out["admm_x"] = to_NUMPY(s.solution())
+        f1 = 0.5 * pxo.SquaredL2Norm(dim=M).asloss(to_device(y)) * Kf
+        s1 = pxs.ADMM(f=f1, h=0.05 * pxo.L1Norm(dim=N), show_progress=False)
+        s1.fit(x0=to_device(np.zeros(N, np.float32)), tau=1.0, stop_crit=pxst.MaxIter(n_iter))
+        out["admm_x_ref"] = to_NUMPY(s1.solution())
+    dist.all_reduce, dist.all_gather = ar0, ag0
+    with open("/proc/self/maps") as fh:
+        out["rccl_libs"] = sorted({ln.split()[-1] for ln in fh if "rccl" in ln.lower() and "/" in ln})
     return out
 
 

