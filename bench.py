@@ -61,7 +61,8 @@ SURVEY_BYTES_PER_PIXEL = 48  # 8 reads + 4 writes of fp32 p
 MFMA_F32_PEAK_TF = 157.3  # dense fp32 MFMA peak (MI355X_MICROARCH.md, Matrix cores: = the f32 vector peak)
 CPU_THREADS_MAX = 16  # the GPU box's CPU share per GPU (gpurun: 16)
 # pxa_pgd_tv2d_last_kernel() -> (mode name, own compulsory bytes per pixel): the arrays the launch reads / writes
-PGD_MODES = {1: ("x, x_prev, H^T y -> x_new", 16)}
+PGD_MODES = {1: ("x, x_prev, H^T y -> x_new (tile kernel)", 16), 2: ("x, x_prev, H^T y -> x_new (strip kernel)", 16)}
+PGD_KERNELS = {1: "pgd_tv2d_kernel", 2: "pgd_strip_kernel"}  # the rocprof name of each mode's kernel
 
 
 # ----------------------------------------------------------------------------- launcher (no GPU here)
@@ -525,8 +526,16 @@ def last_pgd_mode():
     return PGD_MODES.get(int(lib.pxa_pgd_tv2d_last_kernel()), ("none", 16))
 
 
-def roofline(pixels, kern_ms, own_bpp, traffic_key, kernel=KERNEL, mode=""):
+def last_pgd_kernel():
+    """rocprof name of the fused PGD kernel this thread launched last (tile or strip kernel)."""
+    from pyxu_amd._lib import lib
+
+    return PGD_KERNELS.get(int(lib.pxa_pgd_tv2d_last_kernel()), KERNEL)
+
+
+def roofline(pixels, kern_ms, own_bpp, traffic_key, kernel=None, mode=""):
     """The dominant kernel against its own compulsory bytes (frac) and SURVEY §8(d)'s figure (frac_survey)."""
+    kernel = kernel or last_pgd_kernel()
     own = own_bpp * pixels
     achieved = own / (kern_ms * 1e-3) / 1e9
     surv = SURVEY_BYTES_PER_PIXEL * pixels

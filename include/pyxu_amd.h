@@ -59,7 +59,10 @@ extern "C" {
 #define PXA_MODE_EDGE 4
 
 /* Kernel-selection knobs (pxa_tuning). */
-#define PXA_TUNE_PGD_KERNEL 0 /* reserved (kernel variants measured slower were removed; 0 = the tile kernel) */
+#define PXA_TUNE_PGD_KERNEL 0 /* fused PGD step (pxa_pgd_tv2d_step / _plan_step): 0 / 1 the tile kernel (default); v >= 2 the
+                                * strip kernel with strips of v tiles (a workgroup walks a column strip, keeping the shared
+                                * window rows in LDS and prefetching each next tile's new rows; 16-B aligned rows only, else
+                                * the tile kernel).  Same bits; measured slower (A/B and tests only). */
 #define PXA_TUNE_NORMAL_KERNEL 1 /* A/B of pxa_dense_normal: 0 row-split kernel (each row in four column parts,
                                     one workgroup each, part-dots exchanged), 1 one workgroup per row (results
                                     equal up to summation order), 2 the row-split kernel computing every part-dot
@@ -466,8 +469,8 @@ int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int6
  * x_ref instead of x, i.e. (sum (x_new-x_ref)^2, sum x_ref^2): RelError at stop_rate > 1 compares with the
  * iterate of the previous check (opt/stop.py:353-382) — pxa_pgd_tv2d_partials_count() gives the
  * number of slots (tiles x 4; the slots of one image are contiguous).  prox codes: 0 none, 1 positive
- * orthant, 2 l1 with weight prox_w.  pxa_pgd_tv2d_last_kernel() is 1 once the calling thread has
- * launched the tile kernel (0 before).
+ * orthant, 2 l1 with weight prox_w.  pxa_pgd_tv2d_last_kernel() is the kernel the calling thread launched
+ * last: 1 the tile kernel, 2 the strip kernel (PXA_TUNE_PGD_KERNEL), 0 none yet.
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
 /* Prepared form of pxa_pgd_tv2d_step for a solver's iterations (replaces the same call per PGD.m_step,

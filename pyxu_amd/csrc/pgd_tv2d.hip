@@ -89,6 +89,8 @@ struct PgdParams {
   unsigned* counter;
   unsigned fold_seq;
   int64_t fold_rows, fold_per_row;
+  // strip kernel (pgd_strip_kernel): tiles per strip, strip groups per tile column of an image, strips in all
+  unsigned slen, sgroups, nstrips;
 };
 
 // Round 3 also measured a variant that carried yk as solver state (the epilogue writing the next
@@ -191,7 +193,7 @@ __device__ inline void load_window(const PgdParams<T>& p, T* A, int ty0, int tx0
 }
 
 // ---- pass A: PT[col][row] = (G0 yk)[row][col] for the TY tile rows and all A columns
-template <typename T, int R, bool EDGE>
+template <typename T, int R, bool EDGE, int D = 0>
 __device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T* KT, int ty0, int tid = threadIdx.x) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
@@ -208,7 +210,7 @@ __device__ inline void pass_a(const PgdParams<T>& p, const T* A, T* PT, const T*
     if (it < L::NPA) {
       const int a = it % L::NA, b = it / L::NA;  // row group fastest (conflict-free reads/writes)
       T acc[V][V];
-      sweep<T, R, V, L::AP>(A + (V * a) * L::AP + V * b, p.g0, acc);
+      sweep<T, R, V, L::AP, D>(A + (V * a) * L::AP + V * b, p.g0, acc);
       if (edge_rows) ghost_fix<T, R, V, L::AP>(ty0 + V * a, p.n0, ty0 - 2 * R, A + V * b, p.k0, KT, acc);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
@@ -238,7 +240,7 @@ constexpr int kTvxFloats = 9 * 16 + 9 * 32;  // per wavefront: q0 [row group + 1
 
 template <typename T, int R, bool EDGE>
 __device__ inline void tv_exchange(const PgdParams<T>& p, T* A, int ty0, int tx0, int tid, int a, int cb,
-                                   T (&yc)[kVecN<T>][2], T (&tv)[kVecN<T>][2]) {
+                                   T (&yc)[kVecN<T>][2], T (&tv)[kVecN<T>][2], T* xarea23) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
@@ -276,8 +278,9 @@ __device__ inline void tv_exchange(const PgdParams<T>& p, T* A, int ty0, int tx0
 #pragma unroll
     for (int w = 0; w < 2; ++w)
       qat(y[u][w], y[u + 1][w], y[u][w + 1], ty0 + V * a + u, tx0 + c0 + w, q0[u][w], q1[u][w]);
-  // exchange area of this wavefront: waves 0, 1 in A's top dead rows, 2, 3 in the bottom ones
-  T* E = A + (wv < 2 ? 0 : (TY + 2 * R + 1) * L::AP) + (wv & 1) * kTvxFloats;
+  // exchange area of this wavefront: waves 0, 1 in A's top dead rows, 2, 3 in the bottom ones -- or, in the strip
+  // kernel (whose bottom window rows are the next tile's top rows), in `xarea23` beside the tile's LDS carve
+  T* E = (wv < 2 ? A : xarea23 != nullptr ? xarea23 : A + (TY + 2 * R + 1) * L::AP) + (wv & 1) * kTvxFloats;
   T* E0 = E;            // [a + 1][col within the wavefront's 16]
   T* E1 = E + 9 * 16;   // [col item + 1][row]
   // halo of the wavefront: lanes 0..15 the q0 of tile row -1 (its 16 columns), lanes 16..47 the q1 of the column
@@ -323,9 +326,9 @@ __device__ inline void tv_exchange(const PgdParams<T>& p, T* A, int ty0, int tx0
 // `emit(k, u, gr, gc, g, yc)`: g = (G yk + Grad^T q) at row gr, columns gc .. gc + CW - 1 of item k,
 // yc = yk there.  The emitter finishes the pixels in place (finish_run) or stages g for the
 // coalesced epilogue (epilogue_staged).
-template <typename T, int R, bool EDGE, typename Emit>
+template <typename T, int R, bool EDGE, typename Emit, int D = 0>
 __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, const T* KT, const T* GH, int ty0, int tx0,
-                              Emit&& emit, int tid = threadIdx.x) {
+                              Emit&& emit, int tid = threadIdx.x, T* xarea23 = nullptr) {
   using L = Layout<T, R>;
   constexpr int V = L::V;
   constexpr int CA = L::CA;
@@ -378,7 +381,7 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
       constexpr bool kX = PXA_PGD_TVX && sizeof(T) == 4 && L::NA == 8 && CW == 2 && KB == 1 &&
                           (2 * R - 1) * L::AP >= kTvxFloats * 2;
       if constexpr (kX) {
-        tv_exchange<T, R, EDGE>(p, const_cast<T*>(A), ty0, tx0, tid, a, cb, yc, tv);
+        tv_exchange<T, R, EDGE>(p, const_cast<T*>(A), ty0, tx0, tid, a, cb, yc, tv, xarea23);
       } else {
         T yr[CW + 2], yn[CW + 2];
         yrow(0, yr);
@@ -408,7 +411,7 @@ __device__ inline void pass_b(const PgdParams<T>& p, const T* A, const T* PT, co
         }
       }
       T acc[CW][V];            // acc[w][u]: column c0 + w, row V a + u
-      sweep<T, R, CW, L::PTP>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g1, acc);
+      sweep<T, R, CW, L::PTP, D>(PT + (CA - 2 * R + c0) * L::PTP + V * a, p.g1, acc);
       if (edge_cols) ghost_fix_pre<T, R, CW, TY>(tx0 + c0, n1, V * a, GH, KT + kKT, acc);
 #pragma unroll
       for (int u = 0; u < V; ++u) {
@@ -526,12 +529,32 @@ __device__ inline void wave_partials(double part_d, double part_x, double* parti
   }
 }
 
-// One output tile: phase 0 (window), pass A, [ghost columns], pass B (parked in registers), the H^T y / x
-// loads, O staging, row-major epilogue, [RelError partials].
-template <typename T, int R, bool EDGE>
-__device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
-                                const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
-                                T* __restrict__ xns, double* __restrict__ partials, const T* __restrict__ xrs) {
+// Prefetch point of the strip kernel's next-window rows inside a tile (PXA_PGD_STRIP_ISSUE): 0 right after pass A
+// (the loads overlap pass B and the epilogue, and occupy registers through pass B), 1 after the epilogue's own
+// loads (they overlap the O staging and the finishing stores only).
+#ifndef PXA_PGD_STRIP_ISSUE
+#define PXA_PGD_STRIP_ISSUE 1
+#endif
+// Rows in flight per G sweep (tile2d.hpp sweep's D): 0 = compiler-scheduled (tile kernel default); the strip kernel
+// limits it so that its prefetched rows fit beside the passes in 128 VGPRs
+#ifndef PXA_PGD_SWEEP_DEPTH
+#define PXA_PGD_SWEEP_DEPTH 0
+#endif
+#ifndef PXA_PGD_STRIP_DEPTH
+#define PXA_PGD_STRIP_DEPTH 6
+#endif
+
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+// The phases of one output tile once its window is in A (behind a barrier): pass A, [ghost columns], pass B
+// (parked in registers), the H^T y / x loads, O staging, row-major epilogue, [RelError partials].  `mid` runs at the
+// strip kernel's prefetch point; `xarea23`: see tv_exchange (nullptr in the tile kernel).
+template <typename T, int R, bool EDGE, int D, typename Mid>
+__device__ inline void pgd_tile_body(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
+                                     const T* __restrict__ bs, T* __restrict__ xns, double* __restrict__ partials,
+                                     const T* __restrict__ xrs, T* xarea23, Mid&& mid, const int tid) {
   using L = Layout<T, R>;
   using S = Stage<T, R>;
   constexpr int CW = L::CW;
@@ -543,39 +566,21 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   T* GH = reinterpret_cast<T*>(smem + kGhOff<T, R>);  // boundary-column ghost terms (edge-column tiles)
   const int n1 = p.n1;
   const bool edge_cols = EDGE && (tx0 < R || tx0 + TX > n1 - R);
-  const int tid = threadIdx.x;
-  if (EDGE && tid < 2 * R + 1) {
-    KT[tid] = p.k0[tid];
-    KT[kKT + tid] = p.k1[tid];
-  }
   double part_d = 0.0, part_x = 0.0;
   const bool want_part = partials != nullptr;
-  const bool tracing = kProbes && (p.diag & 32) != 0;
+  const bool tracing = kProbes && (p.diag & 32) != 0 && xarea23 == nullptr;
   unsigned long long* ts = reinterpret_cast<unsigned long long*>(smem + kGhOff<T, R> + kGhBytes<T, R>);
   auto tmark = [&](int pt) {
     if (tracing && (tid & 63) == 0) ts[(tid >> 6) * 8 + pt] = clock64();
   };
-  tmark(0);
-#if PXA_PGD_PRIO
-  __builtin_amdgcn_s_setprio(PXA_PGD_PRIO);  // the window loads issue ahead of other workgroups' passes
-#endif
-  if (kProbes && (p.diag & 128)) {  // timing probe only (WRONG results): no window loads, yk = 0
-    for (int i = tid; i < L::AR * L::AP; i += kThreads) A[i] = T(0);
-  } else {
-    load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
-  }
-#if PXA_PGD_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
-  tmark(1);
-  __syncthreads();
   tmark(2);
   const bool skip_passes = kProbes && (p.diag & 64) != 0;  // timing probe only (WRONG results)
-  if (!skip_passes) pass_a<T, R, EDGE>(p, A, PT, KT, ty0);
+  if (!skip_passes) pass_a<T, R, EDGE, D>(p, A, PT, KT, ty0, tid);
   tmark(3);
   __syncthreads();
+  if (PXA_PGD_STRIP_ISSUE == 0) mid();
   if (edge_cols) {
-    ghost_cols_coop<T, R>(p.k1, PT, GH, tx0, n1);
+    ghost_cols_coop<T, R>(p.k1, PT, GH, tx0, n1, tid);
     __syncthreads();
   }
   tmark(4);
@@ -588,10 +593,13 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
 #pragma unroll
         for (int w = 0; w < CW; ++w) st[k][u][w] = A[tid + u * 64 + w];
   } else
-  pass_b<T, R, EDGE>(p, A, PT, KT, GH, ty0, tx0, [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
+  {
+    auto park = [&](int k, int u, int, int, const T(&g)[CW], const T(&)[CW]) {
 #pragma unroll
-    for (int w = 0; w < CW; ++w) st[k][u][w] = g[w];
-  });
+      for (int w = 0; w < CW; ++w) st[k][u][w] = g[w];
+    };
+    pass_b<T, R, EDGE, decltype(park)&, D>(p, A, PT, KT, GH, ty0, tx0, park, tid, xarea23);
+  }
   StagedB<T, R> hb;
   if (kProbes && (p.diag & 512)) {  // timing probe only (WRONG results): no H^T y loads
 #pragma unroll
@@ -602,7 +610,7 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
 #if PXA_PGD_PRIO_EPI
     __builtin_amdgcn_s_setprio(PXA_PGD_PRIO_EPI);
 #endif
-    load_staged<T, R, EDGE>(p, ty0, tx0, bs, hb.v);  // in flight during the O staging
+    load_staged<T, R, EDGE>(p, ty0, tx0, bs, hb.v, tid);  // in flight during the O staging
 #if PXA_PGD_PRIO_EPI
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -630,7 +638,8 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     }
   }
   // x (RelError partials only) is loaded once pass B's parked results are out of the registers
-  if (want_part) load_staged<T, R, EDGE>(p, ty0, tx0, xrs, hb.x);
+  if (want_part) load_staged<T, R, EDGE>(p, ty0, tx0, xrs, hb.x, tid);
+  if (PXA_PGD_STRIP_ISSUE != 0) mid();
   __syncthreads();
   tmark(6);
 #if PXA_PGD_PRIO_FIN
@@ -660,6 +669,42 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     const int slot = bid == 0 ? 0 : bid == 1 ? 1 : bid == nb / 2 ? 2 : 3;
     if (tid < 32) g_tile_trace[slot * 32 + tid] = ts[tid];
   }
+}
+
+
+// One output tile of the tile kernel: phase 0 (window) into A, then the body.
+template <typename T, int R, bool EDGE>
+__device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
+                                const T* __restrict__ xs, const T* __restrict__ xps, const T* __restrict__ bs,
+                                T* __restrict__ xns, double* __restrict__ partials, const T* __restrict__ xrs) {
+  using L = Layout<T, R>;
+  T* A = reinterpret_cast<T*>(smem);
+  T* KT = A + L::AR * L::AP + L::AC * L::PTP;
+  const int tid = threadIdx.x;
+  if (EDGE && tid < 2 * R + 1) {
+    KT[tid] = p.k0[tid];
+    KT[kKT + tid] = p.k1[tid];
+  }
+  const bool tracing = kProbes && (p.diag & 32) != 0;
+  unsigned long long* ts = reinterpret_cast<unsigned long long*>(smem + kGhOff<T, R> + kGhBytes<T, R>);
+  auto tmark = [&](int pt) {
+    if (tracing && (tid & 63) == 0) ts[(tid >> 6) * 8 + pt] = clock64();
+  };
+  tmark(0);
+#if PXA_PGD_PRIO
+  __builtin_amdgcn_s_setprio(PXA_PGD_PRIO);  // the window loads issue ahead of other workgroups' passes
+#endif
+  if (kProbes && (p.diag & 128)) {  // timing probe only (WRONG results): no window loads, yk = 0
+    for (int i = tid; i < L::AR * L::AP; i += kThreads) A[i] = T(0);
+  } else {
+    load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+  }
+#if PXA_PGD_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
+  tmark(1);
+  __syncthreads();
+  pgd_tile_body<T, R, EDGE, PXA_PGD_SWEEP_DEPTH>(p, smem, tile, ty0, tx0, bs, xns, partials, xrs, nullptr, NoHook{}, tid);
 }
 
 // (Opt-in: PXA_RELERR_SINK=1; gfx950-specific.)  The hand-off below uses no release / acquire: it is the first row
@@ -745,9 +790,192 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
   if (p.fold_vals != nullptr) tail_fold<T>(p, partials);
 }
 
+thread_local int g_last_pgd_kernel = 0;  // pxa_pgd_tv2d_last_kernel
+
+// ---- strip kernel: one workgroup walks a column strip of `slen` tiles downwards, keeping the window rows two
+// vertically adjacent tiles share.  Tile i + 1's window (rows ty0 + TY - 2R .. ty0 + 2 TY + 2R) overlaps tile i's in
+// 4R rows; only its TY new rows are loaded -- issued into registers while tile i computes (PXA_PGD_STRIP_ISSUE), so
+// their latency overlaps pass B / the epilogue instead of opening the next tile -- then, once tile i's epilogue is
+// done, the 4R shared rows move up in LDS (rows TY.. -> 0..) and the new rows are written below them as yk.  Per tile
+// the arithmetic is the tile kernel's (same functions, same order): x_new and the RelError partials are bit-identical
+// (tests/test_gpu_pgd_variants.py).  LDS: the tile carve + the TV-exchange area of waves 2, 3 (the tile kernel puts
+// it in the window's bottom dead rows, which here are the next tile's top rows): 39.8 KB, four workgroups per CU.
+// MEASURED SLOWER, kept opt-in for A/B (PXA_TUNE_PGD_KERNEL = strip length; round 6, profiles/r06b_pgd_strip_ab.txt):
+// 2048^2 29.8 us against 23.9-25.2 (strips of 2), 4096^2 93.7 against 71.6 (8), C5 0.640 against 0.631 ms (16).  The
+// prefetch can only be issued after the epilogue's own loads (held through pass B, the rows need ~24 VGPRs the
+// passes do not have: 66 spilled), so it hides little; the loop keeps ~170 SGPRs of parameters and strip state live
+// (spilled to VGPR lanes: a v_readlane before many tap uses in the sweeps); and the four workgroups of a CU walk their
+// strips in lockstep for the whole launch, where the tile kernel's second round starts de-phased.  R 7, 8 spill VGPRs.
+template <typename T, int R>
+struct NewRows {  // the next tile's TY new window rows of x and x_prev, per thread
+  using L = Layout<T, R>;
+  static constexpr int NR = TY * L::NGA;
+  static constexpr int K1 = cdiv(NR, kThreads);
+  T xv[K1][L::V], pv[K1][L::V];
+};
+
+// Branch-free: every lane loads a whole 16-B vector from an address clamped into the image and zeroes it when the
+// vector lies outside (the strip kernel runs only with vec_ok: rows 16-B aligned, n1 % V == 0, so a window vector is
+// wholly inside or wholly outside) -- no exec-masked loads, whose results the compiler waited for and spilled.
+template <typename T, int R>
+__device__ inline void rows_issue(const PgdParams<T>& p, int ty0n, int tx0, const T* __restrict__ xs,
+                                  const T* __restrict__ xps, NewRows<T, R>& w, const int lt) {
+  using L = Layout<T, R>;
+  constexpr int V = L::V;
+  const int n0 = p.n0, n1 = p.n1;
+#pragma unroll
+  for (int k = 0; k < NewRows<T, R>::K1; ++k) {
+    int it = lt + k * kThreads;
+    if (it >= NewRows<T, R>::NR) it = NewRows<T, R>::NR - 1;  // (surplus lanes of the last batch: dropped later)
+    const int r = it / L::NGA, g = it - r * L::NGA;
+    const int gr = ty0n + 2 * R + r, gc = tx0 - L::CA + V * g;  // window row 4R + r of the tile at ty0n
+    const bool in = gr >= 0 && gr < n0 && gc >= 0 && gc < n1;
+    const int cr = gr < 0 ? 0 : gr >= n0 ? n0 - 1 : gr, cc = gc < 0 ? 0 : gc >= n1 ? n1 - V : gc;
+    const int64_t off = (int64_t)cr * n1 + cc;
+    ld_vec<T, V>(xs + off, w.xv[k]);
+    ld_vec<T, V>(xps + off, w.pv[k]);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      w.xv[k][v] = in ? w.xv[k][v] : T(0);
+      w.pv[k][v] = in ? w.pv[k][v] : T(0);
+    }
+  }
+}
+
+// Next window, behind a barrier that follows every read of A by the current tile: the 4R rows shared with the next
+// tile move up (rows TY .. TY + 4R - 1 -> 0 .. 4R - 1: disjoint ranges, so each thread copies its vectors directly),
+// a barrier, then the new rows go in below them as yk (4R .. AR - 1, which overlaps the copy's source rows).
+template <typename T, int R>
+__device__ inline void window_advance(const PgdParams<T>& p, T* A, const NewRows<T, R>& w, const int lt) {
+  using L = Layout<T, R>;
+  constexpr int V = L::V;
+  using VT = typename Vec4<T>::type;
+  constexpr int NS = 4 * R * L::NGA;
+  VT* A4 = reinterpret_cast<VT*>(__builtin_assume_aligned(A, 16));
+#pragma unroll
+  for (int k = 0; k < cdiv(NS, kThreads); ++k) {
+    const int it = lt + k * kThreads;
+    if (it < NS) {
+      const int r = it / L::NGA, g = it - r * L::NGA;
+      A4[(r * L::AP) / V + g] = A4[((TY + r) * L::AP) / V + g];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NewRows<T, R>::K1; ++k) {
+    const int it = lt + k * kThreads;
+    if (it < NewRows<T, R>::NR) {
+      const int r = it / L::NGA, g = it - r * L::NGA;
+      T out[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) out[v] = fma(w.xv[k][v] - w.pv[k][v], p.a, w.xv[k][v]);  // as win_store
+      st_vec<T, V>(A + (4 * R + r) * L::AP + V * g, out);
+    }
+  }
+}
+
+template <typename T, int R>
+constexpr size_t kStripXOff = kGhOff<T, R> + kGhBytes<T, R>;  // the TV-exchange area of waves 2, 3
+constexpr size_t kStripXBytes = (size_t)2 * kTvxFloats * sizeof(float);
+
+template <typename T, int R>
+__global__ void __launch_bounds__(kThreads, 4) pgd_strip_kernel(PgdParams<T> p, const T* __restrict__ x,
+                                                             const T* __restrict__ xp, const T* __restrict__ b,
+                                                             T* __restrict__ xn, double* __restrict__ partials) {
+  using L = Layout<T, R>;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  T* A = reinterpret_cast<T*>(smem_raw);
+  T* KT = A + L::AR * L::AP + L::AC * L::PTP;
+  T* X23 = reinterpret_cast<T*>(smem_raw + kStripXOff<T, R>);
+  const int tid = threadIdx.x;
+  if (tid < 2 * R + 1) {
+    KT[tid] = p.k0[tid];
+    KT[kKT + tid] = p.k1[tid];
+  }
+  unsigned strip = xcd_tile(blockIdx.x, p.nstrips);
+  {  // the last XCD band walks backwards (longest-first: the bottom-edge strips), as in the tile kernel
+    const unsigned nb = p.nstrips, q8 = nb >> 3, r8 = nb & 7u, g8 = blockIdx.x & 7u;
+    if (g8 == 7u) {
+      const unsigned lo = 7u * q8 + (r8 < 7u ? r8 : 7u), len = q8 + (7u < r8 ? 1u : 0u);
+      strip = lo + (len - 1u - (strip - lo));
+    }
+  }
+  // strip = (image, strip group, tile column), tile column fastest: an XCD's band spans whole strip rows, so the
+  // column halos of neighbouring strips are L2 hits
+  const unsigned tiles1 = (unsigned)p.tiles1, per_img = p.sgroups * tiles1;
+  const unsigned si = strip / per_img, rem = strip - si * per_img;
+  const unsigned sg = rem / tiles1, tc = rem - sg * tiles1;
+  const int tr0 = (int)(sg * p.slen);
+  const int tr1 = tr0 + (int)p.slen < p.tiles0 ? tr0 + (int)p.slen : p.tiles0;
+  const int tx0 = (int)tc * TX;
+  const int64_t img = (int64_t)p.n0 * p.n1;
+  const T* xs = x + (int64_t)si * img;
+  const T* xps = xp + (int64_t)si * img;
+  const T* bs = b + (int64_t)(si % (unsigned)p.y_images) * img;
+  T* xns = xn + (int64_t)si * img;
+  const T* xrs = (p.xref != nullptr ? p.xref : x) + (int64_t)si * img;
+  const unsigned tpi = (unsigned)p.tiles0 * tiles1;
+  const bool cols_in = p.vec_ok && img <= 0x7fffffff && tx0 - L::CA >= 0 && tx0 + TX + L::CA <= p.n1;
+  {
+    const int ty0 = tr0 * TY;
+#if PXA_PGD_PRIO
+    __builtin_amdgcn_s_setprio(PXA_PGD_PRIO);
+#endif
+    if (cols_in && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0) load_window<T, R, false>(p, A, ty0, tx0, xs, xps);
+    else load_window<T, R, true>(p, A, ty0, tx0, xs, xps);
+#if PXA_PGD_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  }
+  NewRows<T, R> nw;
+  for (int tr = tr0; tr < tr1; ++tr) {
+    // the thread index laundered per tile: its derived addresses are recomputed in every tile instead of being
+    // hoisted out of the loop and kept live across it (the loop-invariant form spilled ~70-200 VGPRs)
+    int ltid = tid;
+    asm volatile("" : "+v"(ltid));
+    const int ty0 = tr * TY;
+    const unsigned tile = si * tpi + (unsigned)tr * tiles1 + tc;
+    const bool more = tr + 1 < tr1;
+    __syncthreads();  // the window of this tile is in A
+    // (issued for the last tile of the strip too, clamped into the image, so that no branch guards the loads)
+    auto issue = [&]() { rows_issue<T, R>(p, ty0 + TY, tx0, xs, xps, nw, ltid); };
+    if (cols_in && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0)
+      pgd_tile_body<T, R, false, PXA_PGD_STRIP_DEPTH>(p, smem_raw, tile, ty0, tx0, bs, xns, partials, xrs, X23, issue, ltid);
+    else
+      pgd_tile_body<T, R, true, PXA_PGD_STRIP_DEPTH>(p, smem_raw, tile, ty0, tx0, bs, xns, partials, xrs, X23, issue, ltid);
+    if (more) {
+      __syncthreads();  // every read of this window is done
+      window_advance<T, R>(p, A, nw, ltid);
+    }
+  }
+  if (p.fold_vals != nullptr) tail_fold<T>(p, partials);
+}
+
+template <typename T, int R>
+int launch_pgd_strip(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
+                     hipStream_t s) {
+  const size_t smem = kStripXOff<T, R> + kStripXBytes;
+  auto kern = pgd_strip_kernel<T, R>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(p.nstrips), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp, (const T*)b,
+                     (T*)xn, partials);
+  return last_launch_status();
+}
+
 template <typename T, int R>
 int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
                hipStream_t s) {
+  constexpr bool strip_fits = kStripXOff<T, R> + kStripXBytes <= (size_t)160 * 1024;  // (fp64 at large R: no)
+  if (strip_fits && p.slen >= 2) {
+    const int e = launch_pgd_strip<T, R>(p, x, xp, b, xn, partials, s);
+    if (e == PXA_OK) g_last_pgd_kernel = 2;
+    return e;
+  }
+  g_last_pgd_kernel = 1;
   // Layout + the ghost terms (+ the timing trace under PXA_TUNE_PGD_DIAG bit 5)
   const size_t smem = kGhOff<T, R> + kGhBytes<T, R> + ((p.diag & 32) ? 256 : 0);
   auto kern = pgd_tv2d_kernel<T, R>;
@@ -762,7 +990,6 @@ int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void*
   return last_launch_status();
 }
 
-thread_local int g_last_pgd_kernel = 0;  // pxa_pgd_tv2d_last_kernel
 
 // Iteration-invariant parameters (taps folded per offset, G = k (*) k, geometry, prox kind); `R` the blur reach.
 template <typename T>
@@ -844,6 +1071,20 @@ int pgd_run(PgdParams<T> p, int R, double a, double tau, double prox_w, const vo
   // slots of one image, hence of one row, are contiguous
   p.fold_rows = p.stack / p.y_images;
   p.fold_per_row = (int64_t)p.ntiles * (kThreads / 64) / p.fold_rows;
+  // kernel choice (PXA_TUNE_PGD_KERNEL): 0 / 1 the tile kernel (default); v >= 2 the strip kernel with strips of v
+  // tiles (A/B and tests: measured slower, see the strip kernel's comment)
+  {
+    const int64_t kv = tuning(PXA_TUNE_PGD_KERNEL);
+    int64_t sl = 1;
+    if (kv >= 2) sl = kv;
+    if (sl > p.tiles0) sl = p.tiles0;
+    if (sl < 1 || !p.vec_ok) sl = 1;  // (the strip kernel's row prefetch moves whole 16-B vectors only)
+    p.slen = (unsigned)sl;
+    p.sgroups = (unsigned)((p.tiles0 + sl - 1) / sl);
+    const int64_t ns = p.stack * (int64_t)p.sgroups * p.tiles1;
+    p.nstrips = (unsigned)ns;
+    if (ns > 0x7fffffff) p.slen = 1;
+  }
   int st;
   switch (R) {
     case 1: st = launch_pgd<T, 1>(p, x, x_prev, hty, x_new, partials, s); break;
@@ -855,7 +1096,6 @@ int pgd_run(PgdParams<T> p, int R, double a, double tau, double prox_w, const vo
     case 7: st = launch_pgd<T, 7>(p, x, x_prev, hty, x_new, partials, s); break;
     default: st = launch_pgd<T, 8>(p, x, x_prev, hty, x_new, partials, s); break;
   }
-  if (st == PXA_OK) g_last_pgd_kernel = 1;
   return st;
 }
 

@@ -91,19 +91,49 @@ struct Pk<float> {
 
 // Register-blocked sweep along the leading axis of a [m][pitch PS] source: for NO outputs along the
 // sweep and one V-vector across it, out[o][v] = sum_{t=0}^{4R} g[t] src[(o + t) * PS + v].
-template <typename T, int R, int NO, int PS>
+// D = 0: the compiler schedules the NO + 4R row loads (it hoists most of them: ~4 VGPRs per row live at once).
+// D > 0: at most D rows in flight -- row j + D is loaded when row j is consumed, and a scheduling barrier (only
+// VALU / SALU may cross it) keeps the LDS reads in that order -- so a sweep holds ~4 (D + 1) row registers: the
+// PGD strip kernel's budget for its prefetched window rows.  Same FMAs in the same order: same bits.
+template <typename T, int R, int NO, int PS, int D = 0>
 __device__ inline void sweep(const T* __restrict__ src, const T* __restrict__ g, T (&out)[NO][kVecN<T>]) {
   constexpr int V = kVecN<T>;
   using P = typename Pk<T>::type;
   constexpr int NP = V / Pk<T>::W;
   using VT = typename Vec4<T>::type;
+  constexpr int NJ = NO + 4 * R;
   P acc[NO][NP];
 #pragma unroll
   for (int o = 0; o < NO; ++o)
 #pragma unroll
     for (int h = 0; h < NP; ++h) acc[o][h] = Pk<T>::splat(T(0));
+  if constexpr (D > 0) {
+    VT ring[D];
 #pragma unroll
-  for (int j = 0; j < NO + 4 * R; ++j) {
+    for (int j = 0; j < D && j < NJ; ++j) ring[j] = *reinterpret_cast<const VT*>(src + j * PS);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const VT t = ring[j % D];
+      if (j + D < NJ) ring[j % D] = *reinterpret_cast<const VT*>(src + (j + D) * PS);
+      P row[NP];
+      __builtin_memcpy(&row[0], &t, sizeof(VT));
+#pragma unroll
+      for (int o = 0; o < NO; ++o) {
+        const int k = j - o;
+        if (k >= 0 && k <= 4 * R) {
+          const P gg = Pk<T>::splat(g[k]);
+#pragma unroll
+          for (int h = 0; h < NP; ++h) acc[o][h] = gg * row[h] + acc[o][h];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0x6);  // VALU and SALU may move across, LDS reads may not
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) __builtin_memcpy(&out[o][0], &acc[o][0], sizeof(T) * V);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
     const VT t = *reinterpret_cast<const VT*>(src + j * PS);
     P row[NP];
     __builtin_memcpy(&row[0], &t, sizeof(VT));

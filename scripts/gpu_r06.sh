@@ -38,6 +38,18 @@ if [ "$S" = "new" ]; then
   step drv1 120 $DRV
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
 fi
+if [ "$S" = "strip" ]; then
+  step pgdtests 900 $PT -m gpu tests/test_gpu_pgd_variants.py tests/test_gpu_bench_shapes.py tests/test_gpu_parity.py -k "pgd or c2 or c5 or smoke or trajectory or strip"
+  for i in 1 2; do
+    step drv_strip_$i 120 $DRV
+    PXA_TUNE=0=1 step drv_tile_$i 120 $DRV
+  done
+  step c5_strip 300 python3 bench.py --only c5
+  PXA_TUNE=0=1 step c5_tile 300 python3 bench.py --only c5
+  step c4096_strip 300 python3 bench.py --only c2_4096
+  PXA_TUNE=0=1 step c4096_tile 300 python3 bench.py --only c2_4096
+  step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"

@@ -5,7 +5,9 @@ The fused PGD tile kernel (csrc/pgd_tv2d.hip) against itself on its different co
   against the all-scalar path the kernel takes when the arrays are not 16-B aligned;
 * launches with and without the RelError partials;
 * the partials themselves against the separate RelError pass (pxa_relerr_stats) and the solver's
-  stop_rate = 1 path that consumes them (pxa_tile_partials_fold).
+  stop_rate = 1 path that consumes them (pxa_tile_partials_fold);
+* the strip kernel (a workgroup walks a column strip of tiles, keeping the 4R shared window rows in LDS and
+  prefetching the next tile's new rows) against the tile kernel, at every strip length.
 
 Every per-pixel fp32 operation is the same on every path, so x_new must agree BIT FOR BIT on every shape
 class: interior and edge tiles, ragged tile grids, fewer tiles than resident workgroups, stacks with shared
@@ -68,7 +70,7 @@ def _launch(s, x, xp, hty, a, parts=None):
     out = _dev.empty_like(x)
     _dev.pgd_tv2d_step(x, xp, hty, out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
                        p["h1"], p["lam"], p["mu"], a, m["tau"], p["prox"], m["tau"] * p["prox_scale"], partials=parts)
-    assert int(lib.pxa_pgd_tv2d_last_kernel()) == 1
+    assert int(lib.pxa_pgd_tv2d_last_kernel()) in (1, 2)  # tile or strip kernel (PXA_TUNE_PGD_KERNEL)
     return out
 
 
@@ -197,3 +199,67 @@ def test_wide_blur_warns_and_runs_generic_path():
 
     with pytest.warns(FusedPathWarning):
         _plan((64, 96), 1, 1, 3.0, "pos", fused=False)
+
+
+def _with_kernel(v, fn):
+    old = _dev.tuning(0, v)  # PXA_TUNE_PGD_KERNEL: 1 tile kernel, v >= 2 strip kernel of v tiles, 0 auto
+    try:
+        return fn()
+    finally:
+        _dev.tuning(0, old)
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}-sig{c[3]}-{c[4]}")
+def test_strip_kernel_matches_tile_kernel(case):
+    """The strip kernel (PXA_TUNE_PGD_KERNEL = strip length; opt-in, measured slower) against the tile kernel:
+    x_new and the RelError partials bit for bit, for strips of 2 and 3 tiles and whole-column strips (the top,
+    interior and bottom tiles of one strip, ragged last strips); radii 1..8; 0 (the default) is the tile kernel."""
+    sh, stack, y_images, sigma, g_kind = case
+    s = _plan(sh, stack, y_images, sigma, g_kind)
+    m, p = s._mstate, s._plan
+    x, xp, hty = m["x"], m["x_prev"], p["hty"]
+
+    def run(v):
+        parts = _parts(s)
+        out = _with_kernel(v, lambda: _launch(s, x, xp, hty, 0.37, parts))
+        kern = int(lib.pxa_pgd_tv2d_last_kernel())
+        torch.cuda.synchronize()
+        return to_NUMPY(out), to_NUMPY(parts), kern
+
+    ref, ref_parts, k1 = run(1)
+    assert k1 == 1
+    tiles0 = -(-sh[0] // 32)
+    for v in sorted({2, 3, max(2, tiles0), 0}):
+        got, got_parts, k = run(v)
+        assert k == (2 if v >= 2 and tiles0 >= 2 else 1), (v, k)  # a strip of one tile is the tile kernel
+        assert np.array_equal(got, ref), v
+        assert np.array_equal(got_parts, ref_parts), v
+
+
+@pytest.mark.parametrize("v", [2, 3])
+def test_strip_kernel_solver_trajectory_and_misaligned_fallback(v):
+    """30 PGD iterations through the solver (stop checks at stop_rate 1: the partials path) with the strip kernel
+    give the tile kernel's iterates bit for bit; misaligned arrays fall back to the tile kernel (the strip kernel's
+    prefetch moves whole 16-B vectors)."""
+    def traj(kv):
+        def go():
+            f, g, dim, rng = _problem((200, 260), 1, 2.0, "pos")
+            with pxrt.Precision(pxrt.Width.SINGLE):
+                sv = pxs.PGD(f=f, g=g, show_progress=False, stop_rate=1)
+                sv.fit(x0=to_device(rng.uniform(0, 1, dim).astype(np.float32)),
+                       stop_crit=pxst.MaxIter(30) | pxst.RelError(eps=1e-9), mode=pxa.Mode.MANUAL)
+                for _ in sv.steps():  # this thread launches the steps (pxa_pgd_tv2d_last_kernel is per thread)
+                    pass
+                return to_NUMPY(sv.solution()), int(lib.pxa_pgd_tv2d_last_kernel())
+        return _with_kernel(kv, go)
+
+    (xt, kt), (xs_, ks) = traj(1), traj(v)
+    assert kt == 1 and ks == 2
+    assert np.array_equal(xt, xs_)
+    s = _plan((200, 260), 1, 1, 2.0, "pos")
+    m, p = s._mstate, s._plan
+    out = _with_kernel(2, lambda: _launch(s, _misaligned(m["x"]), _misaligned(m["x_prev"]), _misaligned(p["hty"]), 0.37))
+    assert int(lib.pxa_pgd_tv2d_last_kernel()) == 1
+    ref = _with_kernel(1, lambda: _launch(s, m["x"], m["x_prev"], p["hty"], 0.37))
+    torch.cuda.synchronize()
+    assert np.array_equal(to_NUMPY(out), to_NUMPY(ref))
