@@ -98,7 +98,10 @@ extern "C" {
                                    separable-axis passes (pxa_stencil_axis / _sep) use the scalar kernel instead of
                                    the vector / LDS-tiled ones, bit 2 turns off the LDS-tiled off-last-axis pass
                                    (same sums either way) */
-#define PXA_TUNE_COUNT 11
+#define PXA_TUNE_DUAL_ROWS 11 /* A/B of the PDS dual-update kernel C (pxa_tv_dual_update, the three-launch step): rows of w
+                                * per thread, 0 / 1 the one-row kernel, 2 or 4 the row-blocked kernel (a thread's row + 1
+                                * neighbours are its own rows).  Same bits. */
+#define PXA_TUNE_COUNT 12
 
 /* Row reductions (pxa_row_reduce). */
 #define PXA_RED_SUMSQ 0  /* sum x^2            : SquaredL2Norm.apply, norm(ord=2)^2   (norm.py:91-94) */

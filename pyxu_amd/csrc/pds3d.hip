@@ -178,9 +178,149 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
   }
 }
 
+// Row-blocked form (RB >= 2 rows per thread): a thread owns NV positions of RB consecutive rows, so the row + 1
+// neighbour of every row but its last is its own next row (already in registers at this plane) and only one
+// neighbour row per RB rows is read from another thread's rows: w is read 1 + 1 / RB times per voxel instead of
+// twice, and the HBM over-fetch of the neighbour rows that another workgroup has not kept in L2 shrinks with it
+// (1024^3: 1.107 x compulsory with RB = 1; profiles/r06*_k4_rows.txt).  Same per-element expressions: the same bits.
+template <typename T, int NV, int RB, bool ISO, bool PD3O, bool NT>
+__global__ void __launch_bounds__(kBlock) pds_dual_rows_kernel(PdsC<T> p, const T* __restrict__ w,
+                                                               const T* __restrict__ z, T* __restrict__ zo) {
+  const PdsGeom<T> g = p.g;
+  const T sigma = p.sigma, lam = p.lam, rho = p.rho, omr = p.omr;
+  const int n0 = g.n0, n1 = g.n1, n2 = g.n2, D = g.D;
+  const int64_t M = (int64_t)n1 * n2, N = M * n0;
+  const int a_first = 3 - D;
+  const int cgs = (n2 + NV - 1) / NV;  // column groups per row
+  const unsigned blk = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t t = (int64_t)blk * kBlock + threadIdx.x;
+  const int64_t rg = t / cgs;
+  if (rg * RB >= n1) return;  // no barriers below
+  const int r = (int)(rg * RB), c = (int)(t - rg * cgs) * NV;
+  const int nr = n1 - r < RB ? n1 - r : RB;  // rows of this thread inside the plane
+  const int64_t s = blockIdx.z;
+  const int pb = blockIdx.y * p.seg;
+  const int pe = pb + p.seg < n0 ? pb + p.seg : n0;
+  const int64_t j0 = (int64_t)r * n2 + c;
+  const T* ws = w + s * N + j0;
+  const T* zs = z + s * (int64_t)D * N + j0;
+  T* zos = zo + s * (int64_t)D * N + j0;
+  const bool row_nb = r + RB < n1, col_nb = c + NV < n2;
+  T wcur[RB][NV];  // w at the current plane, rows r .. r + RB - 1 (carried from the previous step)
+#pragma unroll
+  for (int i = 0; i < RB; ++i) {
+    if (i < nr) {
+      ldv<T, NV>(ws + (int64_t)pb * M + (int64_t)i * n2, wcur[i]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) wcur[i][e] = T(0);
+    }
+  }
+  for (int pl = pb; pl < pe; ++pl) {
+    const int64_t off = (int64_t)pl * M;
+    T wnext[RB][NV], wrow[NV];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      if (pl + 1 < n0 && i < nr) {
+        ldv<T, NV>(ws + off + M + (int64_t)i * n2, wnext[i]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) wnext[i][e] = T(0);
+      }
+    }
+    if (row_nb) {
+      ldv<T, NV>(ws + off + (int64_t)RB * n2, wrow);
+    } else {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) wrow[e] = T(0);
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      if (i >= nr) continue;
+      const int64_t ro = off + (int64_t)i * n2;
+      T zin[3][NV], zc[3][NV];
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        if (ax < a_first) continue;
+        T wn[NV];
+        if (ax == 0) {
+#pragma unroll
+          for (int e = 0; e < NV; ++e) wn[e] = wnext[i][e];
+        } else if (ax == 1) {
+#pragma unroll
+          for (int e = 0; e < NV; ++e) wn[e] = i + 1 < RB ? wcur[i + 1 < RB ? i + 1 : i][e] : wrow[e];
+          if (i + 1 < RB && i + 1 >= nr) {  // the plane's last row inside this thread's block: zero neighbour
+#pragma unroll
+            for (int e = 0; e < NV; ++e) wn[e] = T(0);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e + 1 < NV; ++e) wn[e] = wcur[i][e + 1];
+          wn[NV - 1] = col_nb ? ws[ro + NV] : T(0);
+        }
+        if (NT)
+          ldn_nt<T, NV>(zs + (int64_t)(ax - a_first) * N + ro, zc[ax]);
+        else
+          ldv<T, NV>(zs + (int64_t)(ax - a_first) * N + ro, zc[ax]);
+#pragma unroll
+        for (int e = 0; e < NV; ++e) zin[ax][e] = dual_in<T>(zc[ax][e], wcur[i][e], wn[e], g.c0[ax], g.c1[ax], sigma);
+      }
+      T zo3[3][NV];
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        T zc1[3], zi1[3], zn1[3];
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+          zc1[ax] = ax < a_first ? T(0) : zc[ax][e];
+          zi1[ax] = ax < a_first ? T(0) : zin[ax][e];
+        }
+        dual_out<T, ISO, PD3O>(zc1, zi1, a_first, lam, rho, omr, zn1);
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) zo3[ax][e] = zn1[ax];
+      }
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        if (ax < a_first) continue;
+        T zn[NV];
+#pragma unroll
+        for (int e = 0; e < NV; ++e) zn[e] = zo3[ax][e];
+        T* zq = zos + (int64_t)(ax - a_first) * N + ro;
+        if (NT)
+          stn_nt<T, NV>(zq, zn);
+        else if constexpr (NV == kVecN<T>)
+          *reinterpret_cast<typename Vec4<T>::type*>(zq) = *reinterpret_cast<const typename Vec4<T>::type*>(zn);
+        else
+          zq[0] = zn[0];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int e = 0; e < NV; ++e) wcur[i][e] = wnext[i][e];
+  }
+}
+
+template <typename T, int NV, int RB, bool PD3O>
+int launch_c_rows(const PdsC<T>& pc, bool iso, int nseg, const void* w, const void* z, void* zo, hipStream_t st) {
+  const int64_t items = (int64_t)((pc.g.n1 + RB - 1) / RB) * ((pc.g.n2 + NV - 1) / NV);
+  const int64_t blocks = (items + kBlock - 1) / kBlock;
+  dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pc.g.stack);
+  if (iso)
+    hipLaunchKernelGGL((pds_dual_rows_kernel<T, NV, RB, true, PD3O, true>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+                       (const T*)z, (T*)zo);
+  else
+    hipLaunchKernelGGL((pds_dual_rows_kernel<T, NV, RB, false, PD3O, true>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+                       (const T*)z, (T*)zo);
+  return last_launch_status();
+}
+
 template <typename T, int NV, bool PD3O>
 int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, const void* z, void* zo,
              hipStream_t st) {
+  // rows per thread (PXA_TUNE_DUAL_ROWS): 1 the one-row kernel, 2 / 4 the row-blocked kernel
+  const int64_t rb = tuning(PXA_TUNE_DUAL_ROWS);
+  if (rb == 2) return launch_c_rows<T, NV, 2, PD3O>(pc, iso, nseg, w, z, zo, st);
+  if (rb == 4) return launch_c_rows<T, NV, 4, PD3O>(pc, iso, nseg, w, z, zo, st);
   const int64_t blocks = (M + (int64_t)kBlock * NV - 1) / ((int64_t)kBlock * NV);
   dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pc.g.stack);
   // z / z_out non-temporal (read / written once): w's row + 1 neighbours stay in L2 (1024^3, r04b: fetch 22.5
@@ -210,7 +350,8 @@ int run_c(const PdsGeom<T>& g, T sigma, T lam, T rho, T omr, bool pd3o, bool iso
   pc.omr = omr;
   const bool vec = (g.n2 % V == 0) && aligned16(w) && aligned16(z) && aligned16(z_out);
   const int nv = vec ? V : 1;
-  const int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv - 1) / ((int64_t)kBlock * nv));
+  const int64_t rbk = tuning(PXA_TUNE_DUAL_ROWS) == 2 ? 2 : tuning(PXA_TUNE_DUAL_ROWS) == 4 ? 4 : 1;
+  const int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv * rbk - 1) / ((int64_t)kBlock * nv * rbk));
   const int64_t target = tuning(PXA_TUNE_DUAL_WGS) > 0 ? tuning(PXA_TUNE_DUAL_WGS) : 2048;  // A/B knob
   int cseg = (int)((target + blocks - 1) / blocks);
   if (cseg > g.n0) cseg = g.n0;

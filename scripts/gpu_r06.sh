@@ -50,6 +50,20 @@ if [ "$S" = "strip" ]; then
   PXA_TUNE=0=1 step c4096_tile 300 python3 bench.py --only c2_4096
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
 fi
+if [ "$S" = "k4" ]; then
+  step k4tests 600 $PT -m gpu tests/test_gpu_pds_fused.py -k "tv_dual"
+  for i in 1 2; do
+    for v in 0 2 4; do PXA_TUNE=11=$v step k4_rows${v}_$i 300 python3 bench.py --only k4; done
+  done
+  K4="python3 bench.py --only k4 --k4-which 3d"
+  for v in 0 2 4; do
+    PXA_TUNE=11=$v step k4fetch$v 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/k4fetch$v -o run --output-format csv -- $K4
+    PXA_TUNE=11=$v step k4write$v 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/k4write$v -o run --output-format csv -- $K4
+  done
+  python3 scripts/pmc_traffic.py $P/k4fetch0 $P/k4write0 "pds_dual_kernel" pds_dual_kernel@1024x1024x1024 $P/traffic_k4.json $T || true
+  python3 scripts/pmc_traffic.py $P/k4fetch2 $P/k4write2 "pds_dual_rows_kernel<float, 4, 2," pds_dual_rows_kernel_rb2@1024x1024x1024 $P/traffic_k4.json $T || true
+  python3 scripts/pmc_traffic.py $P/k4fetch4 $P/k4write4 "pds_dual_rows_kernel<float, 4, 4," pds_dual_rows_kernel_rb4@1024x1024x1024 $P/traffic_k4.json $T || true
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"

@@ -287,6 +287,32 @@ def test_tv_dual_update_vs_oracle(dt, h_kind, sh, relax):
     assert rel_err(out, ref) <= TOL[dt], rel_err(out, ref)
 
 
+@pytest.mark.parametrize("rows", [2, 4])
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("h_kind", ["l1", "iso"])
+@pytest.mark.parametrize("sh,stack", [((67, 129), 1), ((9, 33, 70), 1), ((5, 64, 128), 3), ((7, 37, 1024), 1),
+                                      ((3, 1, 64), 2)], ids=lambda s: "x".join(map(str, s)) if isinstance(s, tuple) else str(s))
+def test_tv_dual_update_row_blocked_bit_exact(rows, dt, h_kind, sh, stack):
+    """Kernel C with `rows` rows of w per thread (PXA_TUNE_DUAL_ROWS: a thread's row + 1 neighbours are its own rows)
+    gives the one-row kernel's bits: odd row counts (the last block's missing rows), a single row, stacks, 2-D and
+    3-D, both relaxations."""
+    rng = np.random.default_rng(5)
+    N = int(np.prod(sh))
+    Dd = len(sh)
+    w = rng.standard_normal(stack * N).astype(dt)
+    z = (0.05 * rng.standard_normal(stack * Dd * N)).astype(dt)
+    geom = (stack, 1, *sh, 2) if Dd == 2 else (stack, *sh, 3)
+    for relax in (0, 1):
+        args = (D(w), D(z), geom, [-1.0] * 3, [1.0] * 3, 0.37, 0.05, 0.7, 0 if h_kind == "l1" else 1)
+        ref = to_NUMPY(_dev.tv_dual_update(*args, relax=relax))
+        prev = _dev.tuning(_dev.TUNE_DUAL_ROWS, rows)
+        try:
+            got = to_NUMPY(_dev.tv_dual_update(*args, relax=relax))
+        finally:
+            _dev.tuning(_dev.TUNE_DUAL_ROWS, prev)
+        assert np.array_equal(got, ref), (relax, rows)
+
+
 @pytest.mark.parametrize("algo", ["pd3o", "cv"])
 def test_pds_lookahead_persistent_grid_bit_exact(algo):
     """Kernel D on a persistent grid (PXA_TUNE_PDS_MARCH bit 1: workgroups loop over the (segment, block) units)
