@@ -64,6 +64,24 @@ if [ "$S" = "k4" ]; then
   python3 scripts/pmc_traffic.py $P/k4fetch2 $P/k4write2 "pds_dual_rows_kernel<float, 4, 2," pds_dual_rows_kernel_rb2@1024x1024x1024 $P/traffic_k4.json $T || true
   python3 scripts/pmc_traffic.py $P/k4fetch4 $P/k4write4 "pds_dual_rows_kernel<float, 4, 4," pds_dual_rows_kernel_rb4@1024x1024x1024 $P/traffic_k4.json $T || true
 fi
+if [ "$S" = "c3prof" ]; then
+  step c3 600 python3 bench.py --only c3
+  step c3trace 600 rocprofv3 --kernel-trace --stats -d $P/c3trace -o run --output-format csv -- python3 bench.py --only c3
+  step k4 300 python3 bench.py --only k4
+  step k4trace 300 rocprofv3 --kernel-trace --stats -d $P/k4trace -o run --output-format csv -- python3 bench.py --only k4
+  B3="python3 bench.py --only c3 --c3-steps 3"
+  step fetchc3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetchc3 -o run --output-format csv -- $B3
+  step writec3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writec3 -o run --output-format csv -- $B3
+  for k in "pds_plane_kernel<float, 6, 0>:pds_plane_kernel_pd3o@1024^3" "pds_plane_kernel<float, 6, 2>:pds_plane_kernel_cv@1024^3" \
+           "pds_march_kernel<float, 6, 1, true, false, true, true>:pds_march_kernel_pd3o@1024^3" \
+           "pds_march_kernel<float, 6, 1, false, false, true, true>:pds_march_kernel_cv@1024^3"; do
+    python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "${k%%:*}" "${k##*:}" $P/traffic_c3.json $T || true
+  done
+  K42="python3 bench.py --only k4 --k4-which 2d"
+  step fetchk4 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetchk4 -o run --output-format csv -- $K42
+  step writek4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writek4 -o run --output-format csv -- $K42
+  python3 scripts/pmc_traffic.py $P/fetchk4 $P/writek4 "pds_dual_kernel" pds_dual_kernel@2048x2048 $P/traffic_c3.json $T || true
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
