@@ -498,6 +498,23 @@ int pxa_pgd_tv2d_plan_step(void* plan, double a, double tau, double prox_w, cons
 int pxa_pgd_tv2d_plan_step_fold(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
                                 const void* hty, void* x_new, double* partials, const void* x_ref, double* rel_values,
                                 uint32_t* rel_flags, uint32_t seq, void* stream);
+/* pxa_pgd_tv2d_plan_step with the RelError statistics of the PREVIOUS iterate pair (the stop check that precedes
+ * this launch at stop_rate 1, opt/stop.py:353-382): the launch's partials are (sum (x - x_prev)^2, sum x_prev^2) per
+ * (tile, wave), taken from the window loads it makes anyway (no load of x beyond them), and a fold launch behind it
+ * publishes them as pxa_tile_partials_fold does into rel_values / rel_flags (seq).  Used by the solver's lagged
+ * stop checks (pyxu_amd/abc/solver.py), which resolve a check after the next step has run. */
+int pxa_pgd_tv2d_plan_step_wfold(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
+                                 const void* hty, void* x_new, double* partials, double* rel_values, uint32_t* rel_flags,
+                                 uint32_t seq, void* stream);
+/* pxa_pgd_tv2d_plan_step with window partials (as pxa_pgd_tv2d_plan_step_wfold: the statistics of the (x, x_prev)
+ * pair it reads, into `partials`), and with prev_partials != NULL one extra workgroup that folds prev_partials -- the
+ * partials of the previous such launch, complete by now -- exactly as pxa_tile_partials_fold does (same bits) into
+ * rel_values[(2, rows)] and then sets rel_flags[q] = seq: a stop check's statistics are published by the launch
+ * after the one that computed them, with no fold launch of their own (the solver's lagged stop checks resolve a
+ * check two launches later).  partials and prev_partials must differ (two buffers, alternately). */
+int pxa_pgd_tv2d_plan_step_wpub(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
+                                const void* hty, void* x_new, double* partials, const double* prev_partials,
+                                double* rel_values, uint32_t* rel_flags, uint32_t seq, void* stream);
 int pxa_pgd_tv2d_plan_free(void* plan);
 int pxa_pgd_tv2d_last_kernel(void);
 /* Diagnostics: s_memtime stamps of the tile kernel's last launch under PXA_TUNE_PGD_DIAG bit 5

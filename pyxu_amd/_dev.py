@@ -614,6 +614,12 @@ def tile_partials_fold(parts, rows, per_row, out):
     return out
 
 
+def tile_partials_publish(parts, rows, per_row, fb, seq):
+    """pxa_tile_partials_fold of `parts` into HostFlagBuffer `fb` under an existing publication number `seq`."""
+    check(lib.pxa_tile_partials_fold(int(rows), int(per_row), parts.data_ptr(), fb.vptr, fb.fptr, int(seq), stream()),
+          "pxa_tile_partials_fold")
+
+
 class FlagWaitError(RuntimeError):
     """A HostFlagBuffer publication never landed although its stream is idle."""
 
@@ -1012,6 +1018,36 @@ class PgdPlan:
                      sink.fptr if sink is not None else None, int(seq), stream())
         if r:
             check(r, "pxa_pgd_tv2d_plan_step")
+        if ev is not None:
+            _TIMER.end(ev)
+        return x_new
+
+    def step_wpub(self, x, x_prev, hty, x_new, a, tau, prox_w, partials, prev=None):
+        """One iteration with window partials into `partials`; `prev` = (partials of the previous such launch,
+        HostFlagBuffer, seq): folded and published by an extra workgroup of this launch
+        (pxa_pgd_tv2d_plan_step_wpub)."""
+        ev = _TIMER.begin() if _TIMER is not None else None
+        pp, fb, seq = prev if prev is not None else (None, None, 0)
+        r = lib.pxa_pgd_tv2d_plan_step_wpub(self._h, float(a), float(tau), float(prox_w), x.data_ptr(), x_prev.data_ptr(),
+                                            hty.data_ptr(), x_new.data_ptr(), partials.data_ptr(),
+                                            pp.data_ptr() if pp is not None else None, fb.vptr if fb is not None else None,
+                                            fb.fptr if fb is not None else None, int(seq), stream())
+        if r:
+            check(r, "pxa_pgd_tv2d_plan_step_wpub")
+        if ev is not None:
+            _TIMER.end(ev)
+        return x_new
+
+    def step_window(self, x, x_prev, hty, x_new, a, tau, prox_w, partials, sink, seq):
+        """One iteration whose partials are the RelError statistics of the (x, x_prev) pair it reads -- the stop
+        check before it -- folded into `sink` under publication `seq` by a fold launch behind it
+        (pxa_pgd_tv2d_plan_step_wfold)."""
+        ev = _TIMER.begin() if _TIMER is not None else None
+        r = lib.pxa_pgd_tv2d_plan_step_wfold(self._h, float(a), float(tau), float(prox_w), x.data_ptr(), x_prev.data_ptr(),
+                                             hty.data_ptr(), x_new.data_ptr(), partials.data_ptr(), sink.vptr, sink.fptr,
+                                             int(seq), stream())
+        if r:
+            check(r, "pxa_pgd_tv2d_plan_step_wfold")
         if ev is not None:
             _TIMER.end(ev)
         return x_new

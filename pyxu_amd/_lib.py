@@ -89,6 +89,8 @@ EXPORTS = {
                                 ct.POINTER(vp)]),
     "pxa_pgd_tv2d_plan_step": (i32, [vp, f64, f64, f64, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp]),
     "pxa_pgd_tv2d_plan_step_fold": (i32, [vp, f64, f64, f64, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp]),
+    "pxa_pgd_tv2d_plan_step_wfold": (i32, [vp, f64, f64, f64, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp]),
+    "pxa_pgd_tv2d_plan_step_wpub": (i32, [vp, f64, f64, f64, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp]),
     "pxa_pgd_tv2d_plan_free": (i32, [vp]),
     "pxa_pgd_tv2d_step": (
         i32,

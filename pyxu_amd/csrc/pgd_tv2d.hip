@@ -91,6 +91,17 @@ struct PgdParams {
   int64_t fold_rows, fold_per_row;
   // strip kernel (pgd_strip_kernel): tiles per strip, strip groups per tile column of an image, strips in all
   unsigned slen, sgroups, nstrips;
+  // window partials (pxa_pgd_tv2d_plan_step_wfold): the per-(tile, wave) partials are (sum (x - x_prev)^2, sum x_prev^2)
+  // over the tile, from the window loads -- the RelError statistics of the PREVIOUS step's check -- instead of the
+  // epilogue's (x_new - x_ref) statistics: no extra load of x
+  int win_part;
+  // publication of the PREVIOUS launch's partials (pxa_pgd_tv2d_plan_step_wpub): one extra workgroup (block ntiles)
+  // folds pub_src as pxa_tile_partials_fold does (same bits) into pub_vals and sets pub_flags[q] = pub_seq, beside
+  // the tile workgroups -- no fold launch, no cross-workgroup hand-off (pub_src is complete at launch)
+  const double* pub_src;
+  double* pub_vals;
+  unsigned* pub_flags;
+  unsigned pub_seq;
 };
 
 // Round 3 also measured a variant that carried yk as solver state (the epilogue writing the next
@@ -697,14 +708,36 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
   if (kProbes && (p.diag & 128)) {  // timing probe only (WRONG results): no window loads, yk = 0
     for (int i = tid; i < L::AR * L::AP; i += kThreads) A[i] = T(0);
   } else {
-    load_window<T, R, EDGE>(p, A, ty0, tx0, xs, xps);
+    Window<T, R> w;
+    win_issue<T, R, EDGE>(p, ty0, tx0, xs, xps, w, tid);
+    win_store<T, R>(p, A, w, tid);
+    if (p.win_part && partials != nullptr) {  // the previous check's RelError statistics over this tile's pixels
+      double part_d = 0.0, part_x = 0.0;
+#pragma unroll
+      for (int k = 0; k < Window<T, R>::K0; ++k) {
+        const int it = tid + k * kThreads;
+        if (it < L::N0) {
+          const int r = it / L::NGA, g = it - r * L::NGA;
+          if (r >= 2 * R && r < 2 * R + TY && L::V * g >= L::CA && L::V * g < L::CA + TX) {
+#pragma unroll
+            for (int v = 0; v < L::V; ++v) {  // (outside the image both are 0: no contribution)
+              const double dd = (double)w.xv[k][v] - (double)w.pv[k][v];
+              part_d = fma(dd, dd, part_d);
+              part_x = fma((double)w.pv[k][v], (double)w.pv[k][v], part_x);
+            }
+          }
+        }
+      }
+      wave_partials(part_d, part_x, partials, tile * kPartWaves + (tid >> 6));
+    }
   }
 #if PXA_PGD_PRIO
   __builtin_amdgcn_s_setprio(0);
 #endif
   tmark(1);
   __syncthreads();
-  pgd_tile_body<T, R, EDGE, PXA_PGD_SWEEP_DEPTH>(p, smem, tile, ty0, tx0, bs, xns, partials, xrs, nullptr, NoHook{}, tid);
+  pgd_tile_body<T, R, EDGE, PXA_PGD_SWEEP_DEPTH>(p, smem, tile, ty0, tx0, bs, xns, p.win_part ? nullptr : partials, xrs,
+                                                 nullptr, NoHook{}, tid);
 }
 
 // (Opt-in: PXA_RELERR_SINK=1; gfx950-specific.)  The hand-off below uses no release / acquire: it is the first row
@@ -747,11 +780,34 @@ __device__ inline void tail_fold(const PgdParams<T>& p, const double* __restrict
   }
 }
 
+// The extra workgroup of a pxa_pgd_tv2d_plan_step_wpub launch: the previous launch's partials folded in the order of
+// pxa_tile_partials_fold (fold_tile_stat: same sum order, same bits; the narrow load form, so that this branch adds
+// no registers to the tile kernel's allocation), the values stored write-through to host memory
+// (system-scope relaxed atomic stores), then -- once they have completed -- the flags.
+template <typename T>
+__device__ inline void publish_prev(const PgdParams<T>& p) {
+  __shared__ double red[kThreads / 64];
+  for (int64_t q = 0; q < 2 * p.fold_rows; ++q) {
+    const int64_t stat = q / p.fold_rows, r = q - stat * p.fold_rows;
+    const double t = fold_tile_stat<false>(p.pub_src + 2 * r * p.fold_per_row + stat, p.fold_per_row, red);
+    if (threadIdx.x == 0) __hip_atomic_store(p.pub_vals + q, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the values have reached host memory before the flags
+    for (int64_t q = 0; q < 2 * p.fold_rows; ++q)
+      __hip_atomic_store(p.pub_flags + q, p.pub_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <typename T, int R>
 __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, const T* __restrict__ x,
                                                             const T* __restrict__ xp, const T* __restrict__ b,
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
+  if (p.pub_src != nullptr && blockIdx.x == p.ntiles) {  // (no barrier shared with the tile workgroups)
+    publish_prev<T>(p);
+    return;
+  }
   extern __shared__ __align__(16) unsigned char smem_raw[];
   if (kProbes && p.stagger && blockIdx.x < p.round1) {
     const unsigned sel = (unsigned)p.stagger >> 8, b = blockIdx.x >> 3;  // b: index within the XCD
@@ -985,8 +1041,8 @@ int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void*
                               (int)(kGhOff<T, R> + kGhBytes<T, R> + 256));
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(p.ntiles), dim3(kThreads), smem, s, p, (const T*)x, (const T*)xp, (const T*)b,
-                     (T*)xn, partials);
+  hipLaunchKernelGGL(kern, dim3(p.ntiles + (p.pub_src != nullptr ? 1u : 0u)), dim3(kThreads), smem, s, p, (const T*)x,
+                     (const T*)xp, (const T*)b, (T*)xn, partials);
   return last_launch_status();
 }
 
@@ -1050,7 +1106,8 @@ int pgd_params(int64_t stack, int64_t y_images, int64_t n0, int64_t n1, int nt0,
 template <typename T>
 int pgd_run(PgdParams<T> p, int R, double a, double tau, double prox_w, const void* x, const void* x_prev,
             const void* hty, void* x_new, double* partials, const void* x_ref, double* rel_values, uint32_t* rel_flags,
-            uint32_t seq, unsigned* counter, hipStream_t s) {
+            uint32_t seq, unsigned* counter, hipStream_t s, int win_part = 0, const double* pub_src = nullptr,
+            double* pub_vals = nullptr, uint32_t* pub_flags = nullptr, uint32_t pub_seq = 0) {
   PXA_CHECK_ARG(x && x_prev && hty && x_new);
   PXA_CHECK_ARG(x_new != x && x_new != x_prev && x_new != x_ref);
   PXA_CHECK_ARG(rel_values == nullptr || (partials != nullptr && rel_flags != nullptr && counter != nullptr));
@@ -1071,6 +1128,13 @@ int pgd_run(PgdParams<T> p, int R, double a, double tau, double prox_w, const vo
   // slots of one image, hence of one row, are contiguous
   p.fold_rows = p.stack / p.y_images;
   p.fold_per_row = (int64_t)p.ntiles * (kThreads / 64) / p.fold_rows;
+  p.win_part = win_part;
+  PXA_CHECK_ARG(!win_part || (partials != nullptr && rel_values == nullptr));
+  PXA_CHECK_ARG(pub_src == nullptr || (pub_vals != nullptr && pub_flags != nullptr && pub_src != partials));
+  p.pub_src = pub_src;
+  p.pub_vals = pub_vals;
+  p.pub_flags = (unsigned*)pub_flags;
+  p.pub_seq = (unsigned)pub_seq;
   // kernel choice (PXA_TUNE_PGD_KERNEL): 0 / 1 the tile kernel (default); v >= 2 the strip kernel with strips of v
   // tiles (A/B and tests: measured slower, see the strip kernel's comment)
   {
@@ -1083,7 +1147,7 @@ int pgd_run(PgdParams<T> p, int R, double a, double tau, double prox_w, const vo
     p.sgroups = (unsigned)((p.tiles0 + sl - 1) / sl);
     const int64_t ns = p.stack * (int64_t)p.sgroups * p.tiles1;
     p.nstrips = (unsigned)ns;
-    if (ns > 0x7fffffff) p.slen = 1;
+    if (ns > 0x7fffffff || win_part || pub_src) p.slen = 1;  // (window partials / publication: the tile kernel)
   }
   int st;
   switch (R) {
@@ -1194,6 +1258,38 @@ int pxa_pgd_tv2d_plan_step_fold(void* plan, double a, double tau, double prox_w,
                                        0, stream);
   if (e != PXA_OK) return e;
   return pxa_tile_partials_fold(rows, per_row, partials, rel_values, rel_flags, seq, stream);
+}
+
+int pxa_pgd_tv2d_plan_step_wfold(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
+                                 const void* hty, void* x_new, double* partials, double* rel_values, uint32_t* rel_flags,
+                                 uint32_t seq, void* stream) {
+  PXA_CHECK_ARG(plan != nullptr && partials != nullptr && rel_values != nullptr && rel_flags != nullptr);
+  const PgdPlan* pl = (const PgdPlan*)plan;
+  const int64_t stack = pl->dtype == PXA_F32 ? pl->pf.stack : pl->pd.stack;
+  const int64_t rows = stack / (pl->dtype == PXA_F32 ? pl->pf.y_images : pl->pd.y_images);
+  const int64_t per_row = (int64_t)(pl->dtype == PXA_F32 ? pl->pf.ntiles : pl->pd.ntiles) * (kThreads / 64) / rows;
+  int e;
+  if (pl->dtype == PXA_F32)
+    e = pgd_run<float>(pl->pf, pl->R, a, tau, prox_w, x, x_prev, hty, x_new, partials, nullptr, nullptr, nullptr, 0,
+                       pl->counter, as_stream(stream), 1);
+  else
+    e = pgd_run<double>(pl->pd, pl->R, a, tau, prox_w, x, x_prev, hty, x_new, partials, nullptr, nullptr, nullptr, 0,
+                        pl->counter, as_stream(stream), 1);
+  if (e != PXA_OK) return e;
+  return pxa_tile_partials_fold(rows, per_row, partials, rel_values, rel_flags, seq, stream);
+}
+
+int pxa_pgd_tv2d_plan_step_wpub(void* plan, double a, double tau, double prox_w, const void* x, const void* x_prev,
+                                const void* hty, void* x_new, double* partials, const double* prev_partials,
+                                double* rel_values, uint32_t* rel_flags, uint32_t seq, void* stream) {
+  PXA_CHECK_ARG(plan != nullptr && partials != nullptr);
+  PXA_CHECK_ARG(prev_partials == nullptr || (rel_values != nullptr && rel_flags != nullptr));
+  const PgdPlan* pl = (const PgdPlan*)plan;
+  if (pl->dtype == PXA_F32)
+    return pgd_run<float>(pl->pf, pl->R, a, tau, prox_w, x, x_prev, hty, x_new, partials, nullptr, nullptr, nullptr, 0,
+                          pl->counter, as_stream(stream), 1, prev_partials, rel_values, rel_flags, seq);
+  return pgd_run<double>(pl->pd, pl->R, a, tau, prox_w, x, x_prev, hty, x_new, partials, nullptr, nullptr, nullptr, 0,
+                         pl->counter, as_stream(stream), 1, prev_partials, rel_values, rel_flags, seq);
 }
 
 int pxa_pgd_tv2d_plan_free(void* plan) {

@@ -104,6 +104,9 @@ class PGD(pxa.Solver):
             # the solver never writes a tensor it has published as x (outputs go to fresh or recycled
             # buffers nobody else references), so stop criteria may keep references instead of copies
             mst["__immutable__"] = frozenset({"x"})
+            # the step can compute the RelError statistics of the (x, x_prev) pair it reads (pxa_pgd_tv2d_plan_step_wfold):
+            # offered to the criterion under the lagged engine, which resolves a check after the next step ran
+            mst["__window_ok__"] = True
 
     # publish the fused step's per-tile RelError partials to the stop criteria (False: A/B and parity tests)
     _fused_relerr = True
@@ -126,10 +129,50 @@ class PGD(pxa.Solver):
         self._spare = None
         self._spec_refs = 0
 
+    # lagged stop checks (abc/solver.py _lag_loop): a check's state is (x, x_prev); dropping the steps launched after
+    # it means restoring that pair and returning their momentum values (the fused path only: its steps write a
+    # buffer that is neither x nor x_prev, and one the solver holds no other reference to)
+    _LAG_PUB = os.environ.get("PXA_LAG_PUB", "1") == "1"
+
+    def _lag_supported(self):
+        return self._plan is not None and self._fused_relerr and not _NO_SPEC
+
+    def _lag_flush(self):
+        """Publish the window statistics still waiting for the next launch's extra workgroup (the run will not
+        launch again): one fold launch."""
+        pend = getattr(self, "_wpub_pending", None)
+        self._wpub_pending = None
+        if pend is not None:
+            p = self._plan
+            _dev.tile_partials_publish(pend[0], p["rows"], p["tiles_per_row"], pend[1], pend[2])
+
+    def _lag_snapshot(self):
+        mst = self._mstate
+        return (mst["x"], mst["x_prev"])
+
+    def _lag_restore(self, snap, undone):
+        mst = self._mstate
+        mst["x"], mst["x_prev"] = snap
+        hist = list(getattr(self, "_a_hist", ()))
+        for v in reversed(hist[len(hist) - undone:] if undone > 0 else []):  # next() returns the earliest first
+            mst["a"].push(v)
+        mst.pop("__relerr__", None)
+        mst.pop("__relerr_sink__", None)
+        mst.pop("__relerr_window__", None)
+        self._wpub_pending = None
+        self._spare = None
+        self._x_check = None
+
     def m_step(self):
         mst = self._mstate
         a = next(mst["a"])
         self._last_a = a
+        ah = self.__dict__.get("_a_hist")
+        if ah is None:
+            import collections
+
+            ah = self._a_hist = collections.deque(maxlen=256)
+        ah.append(a)
         if self._plan is not None:
             p = self._plan
             mst.pop("__relerr__", None)  # (holds x_prev: drop it before the buffer-recycling refcount below)
@@ -138,6 +181,28 @@ class PGD(pxa.Solver):
             if out is None or out is x or out is xp:
                 out = _dev.empty_like(x)
             tau = mst["tau"]
+            wnd = mst.pop("__relerr_window__", None)
+            if wnd is not None:
+                # (lagged engine) this launch computes the statistics of the check before it from its window loads,
+                # and an extra workgroup of it publishes those of the check before that (two partials buffers,
+                # alternately): no fold launch (PXA_LAG_PUB=0: a fold launch behind the step instead)
+                if self._LAG_PUB:
+                    wp = p.get("wparts")
+                    if wp is None:
+                        wp = p["wparts"] = (p["parts"], _dev.empty_f64(p["parts"].shape, x))
+                    self._wpar_i = getattr(self, "_wpar_i", 0) ^ 1
+                    cur = wp[self._wpar_i]
+                    p["plan"].step_wpub(x, xp, p["hty"], out, a, tau, tau * p["prox_scale"], cur,
+                                        getattr(self, "_wpub_pending", None))
+                    self._wpub_pending = (cur, wnd[0], wnd[1])
+                else:
+                    p["plan"].step_window(x, xp, p["hty"], out, a, tau, tau * p["prox_scale"], p["parts"], wnd[0], wnd[1])
+                mst["x_prev"], mst["x"] = x, out
+                refs = 2 + getattr(self, "_spec_refs", 0)
+                self._spec_refs = 0
+                self._spare = xp if (sys.getrefcount(xp) == refs and xp.data_ptr() != x.data_ptr()
+                                     and _dev.storage_exclusive(xp)) else None
+                return
             # RelError partials only for the launch right before a stop check (the engine advances idx
             # before m_step: the next check runs at idx when idx % stop_rate == 0).  RelError compares with
             # the iterate of the PREVIOUS check (opt/stop.py:353-382), which the criterion keeps: x itself at

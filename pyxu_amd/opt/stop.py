@@ -327,6 +327,7 @@ class RelError(pxa.StoppingCriterion):
         copy of x are enqueued now; the returned callable waits for them only and decides.  Same
         kernels, same bits, same decision, same info() as stop()."""
         x = state[self._var]
+        self._last_async = ("sync", None)  # (kind, readiness probe) of this check's statistics: the lagged engine
         if (isinstance(x, numbers.Real) or self._x_prev is None or self._reduce is not None
                 or self._f is not _identity or self._norm != 2):
             return super().stop_async(state)
@@ -335,6 +336,28 @@ class RelError(pxa.StoppingCriterion):
         rows = x.numel() // x.shape[-1]
         if not (0 < rows <= 65535 and x.dtype == self._x_prev.dtype):
             return super().stop_async(state)
+        if (getattr(self, "_window_stats", False) and hasattr(state, "__setitem__") and state.get("__window_ok__")
+                and state.get("x_prev") is self._x_prev):
+            # (the solver's lagged engine) the NEXT step computes this check's statistics from the (x, x_prev) pair
+            # it reads anyway and folds them into a ring buffer: this check is resolved after that step has run
+            nb = max(2, int(getattr(self, "_nbufs", 2)))
+            bufs = getattr(self, "_flag_bufs", None)
+            if bufs is None or bufs[0].rows != rows or len(bufs) != nb:
+                bufs = self._flag_bufs = tuple(_dev.HostFlagBuffer(rows) for _ in range(nb))
+            self._win_i = (getattr(self, "_win_i", -1) + 1) % nb
+            fb = bufs[self._win_i]
+            seq = fb.next_seq()
+            state["__relerr_window__"] = (fb, seq)
+            state.pop("__relerr_sink__", None)
+            self._x_prev = x
+            shape = x.shape[:-1]
+
+            def resolve_window():
+                fb.wait(seq)
+                return self._decide(_finish(fb.stats.copy(), self._norm), shape)
+
+            self._last_async = ("fused", lambda: bool((fb.flags == seq).all()))
+            return resolve_window
         h = self._fused(state, x)
         if h is not None:
             # the step's own per-tile partials, folded straight into coherent host memory with a completion flag
@@ -343,17 +366,21 @@ class RelError(pxa.StoppingCriterion):
             # iterate's buffer.  Two buffers, alternately: this check reads one while the launch behind it
             # (enqueued before the decision) may fold into the other -- the solver finds that one as the
             # "__relerr_sink__" of its state, and then the fold is part of its launch (h[6] = (buffer, seq))
+            # a ring of _nbufs buffers (2: this check's and the next launch's; the solver's lagged engine keeps
+            # several checks unresolved and asks for more, abc/solver.py _lag_loop)
+            nb = max(2, int(getattr(self, "_nbufs", 2)))
             bufs = getattr(self, "_flag_bufs", None)
-            if bufs is None or bufs[0].rows != rows:
-                bufs = self._flag_bufs = (_dev.HostFlagBuffer(rows), _dev.HostFlagBuffer(rows))
+            if bufs is None or bufs[0].rows != rows or len(bufs) != nb:
+                bufs = self._flag_bufs = tuple(_dev.HostFlagBuffer(rows) for _ in range(nb))
             folded = h[6] if len(h) > 6 else None
-            if folded is not None and folded[0] in bufs:
+            if folded is not None and any(folded[0] is b for b in bufs):
                 fb, seq = folded
             else:
                 fb = bufs[0]
                 seq = fb.fold(h[3], h[5])
             if self._offer_sink and hasattr(state, "__setitem__"):
-                state["__relerr_sink__"] = (self._var, bufs[1] if fb is bufs[0] else bufs[0], self._in_kernel_fold)
+                nxt = bufs[(next(i for i, b in enumerate(bufs) if b is fb) + 1) % nb]
+                state["__relerr_sink__"] = (self._var, nxt, self._in_kernel_fold)
             self._x_prev = x
             shape = x.shape[:-1]
 
@@ -361,6 +388,7 @@ class RelError(pxa.StoppingCriterion):
                 fb.wait(seq)
                 return self._decide(_finish(fb.stats.copy(), self._norm), shape)  # (2, rows) view
 
+            self._last_async = ("fused", lambda: bool((fb.flags == seq).all()))
             return resolve_flags
         # one device / pinned-host statistics pair and one event per criterion, reused: a check is
         # resolved before the next one is issued
@@ -377,6 +405,7 @@ class RelError(pxa.StoppingCriterion):
             x_copy = x
         _dev.record_event(ev)
         shape = x.shape[:-1]
+        self._last_async = ("event", ev.query)  # (one buffer: resolved before the next check is issued)
 
         def resolve():
             _dev.wait_event(ev)

@@ -82,6 +82,10 @@ if [ "$S" = "c3prof" ]; then
   step writek4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writek4 -o run --output-format csv -- $K42
   python3 scripts/pmc_traffic.py $P/fetchk4 $P/writek4 "pds_dual_kernel" pds_dual_kernel@2048x2048 $P/traffic_c3.json $T || true
 fi
+if [ "$S" = "lag" ]; then
+  step lagtests 900 $PT -m gpu tests/test_gpu_solver_lag.py tests/test_gpu_solver_engine.py tests/test_gpu_pgd_variants.py -k "lag or speculative or fold or relerr or async or objective"
+  step sr1ab 600 python3 scripts/sr1_lag_ab.py 400
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"

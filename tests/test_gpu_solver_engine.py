@@ -108,8 +108,11 @@ def test_speculative_stop_checks_match_synchronous(stop_rate, mode, monkeypatch)
     momentum and history as the synchronous checks of the reference order (solver.py:588-652)."""
     res = {}
     for spec in (True, False):
-        if not spec:
+        if not spec:  # the synchronous reference order: neither speculative nor lagged checks
             monkeypatch.setattr(pxs.PGD, "_spec_supported", lambda self: False)
+            monkeypatch.setattr(pxs.PGD, "_lag_supported", lambda self: False)
+        else:  # the speculative path itself (at stop_rate 1 the lagged engine would take over)
+            monkeypatch.setattr(pxs.PGD, "_lag_supported", lambda self: False)
         with pxrt.Precision(pxrt.Width.SINGLE):
             f, g, N = _pgd_problem()
             s = pxs.PGD(f=f, g=g, show_progress=False, stop_rate=stop_rate)
