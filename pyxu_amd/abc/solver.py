@@ -568,6 +568,7 @@ class Solver:
     # same terms in another order, so the RelError values may differ from the synchronous path's in the last bits
     # (PXA_LAG_WINDOW=0: the epilogue statistics, bit-identical history)
     _LAG_WINDOW = os.environ.get("PXA_LAG_WINDOW", "1") == "1"
+    _LAG_RECORDS = 4  # deferred history records written per batch by the lagged engine
 
     def _lag_supported(self) -> bool:
         return False
@@ -632,8 +633,6 @@ class Solver:
         try:
             while True:
                 idx = ast["idx"]
-                if ast["pending"] and idx - ast["pending"][0][0] >= self._RECORD_LAG:
-                    self._flush_records()
                 e = Solver._LagCheck()
                 e.idx, e.snap, e.rel_prev = idx, self._lag_snapshot(), rel._x_prev
                 # window statistics need a next launch: not for the check at which MaxIter ends the run
@@ -655,7 +654,20 @@ class Solver:
                     self.m_step()
                     e.post = {k: mst.get(k) for k in ast["log_var"]}
                     drain = 0
-                while pend and (drain > 0 or len(pend) > depth or (pend[0].ready is not None and pend[0].ready())):
+                    # deferred records, a few per launch (one batch of _RECORD_LAG would stall a queue that a host
+                    # synchronisation has just drained: ~0.1 ms of host work against one step of device work)
+                    if len(ast["pending"]) >= self._LAG_RECORDS:
+                        with ast["lock"]:
+                            items = ast["pending"][: self._LAG_RECORDS]
+                            del ast["pending"][: self._LAG_RECORDS]
+                            n = ast.get("unflushed", 0) + len(items)
+                            ast["unflushed"] = 0 if n >= self._RECORD_LAG else n
+                            self._record_batch(items, flush=n >= self._RECORD_LAG)
+                free = 1  # at most one ready check per launch beyond the forced ones: the device queue stays fed (a run
+                # of ready checks resolved back to back, e.g. after a host synchronisation, would leave it idle)
+                while pend and (drain > 0 or len(pend) > depth or (free > 0 and pend[0].ready is not None and pend[0].ready())):
+                    if drain <= 0 and len(pend) <= depth:
+                        free -= 1
                     drain -= 1
                     c = pend.popleft()
                     stopped = c.resolve()

@@ -86,6 +86,11 @@ if [ "$S" = "lag" ]; then
   step lagtests 900 $PT -m gpu tests/test_gpu_solver_lag.py tests/test_gpu_solver_engine.py tests/test_gpu_pgd_variants.py -k "lag or speculative or fold or relerr or async or objective"
   step sr1ab 600 python3 scripts/sr1_lag_ab.py 400
 fi
+if [ "$S" = "sr1" ]; then
+  step striptest 300 $PT -m gpu tests/test_gpu_pgd_variants.py -k "strip_kernel_solver"
+  SR1_ARMS=short step sr1_20 300 python3 scripts/sr1_lag_ab.py 20
+  SR1_ARMS=short step sr1_100 300 python3 scripts/sr1_lag_ab.py 100
+fi
 if [ "$S" = "full" ]; then
   step pytest 1200 $PT tests -m gpu
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"

@@ -19,7 +19,9 @@ import pyxu_amd.opt.solver as pxs  # noqa: E402
 
 # (depth, in-kernel fold, window statistics, publication by the next launch)
 arms = [(0, False, False, True), (8, False, True, True), (8, False, True, False), (8, False, False, True),
-        (16, False, True, True), (4, False, True, True)]
+        (4, False, True, True), (2, False, True, True)]
+if os.environ.get("SR1_ARMS") == "short":
+    arms = [(0, False, False, True), (8, False, True, True), (4, False, True, True), (2, False, True, True)]
 res = {}
 for rep in range(2):
     for depth, ink, win, pub in arms:

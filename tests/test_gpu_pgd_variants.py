@@ -241,6 +241,9 @@ def test_strip_kernel_solver_trajectory_and_misaligned_fallback(v):
     """30 PGD iterations through the solver (stop checks at stop_rate 1: the partials path) with the strip kernel
     give the tile kernel's iterates bit for bit; misaligned arrays fall back to the tile kernel (the strip kernel's
     prefetch moves whole 16-B vectors)."""
+    pxa.Solver._LAG, lag0 = 0, pxa.Solver._LAG  # the speculative engine (the lagged one uses the window-partials launch,
+    # which the strip kernel does not implement: it falls back to the tile kernel)
+
     def traj(kv):
         def go():
             f, g, dim, rng = _problem((200, 260), 1, 2.0, "pos")
@@ -253,7 +256,10 @@ def test_strip_kernel_solver_trajectory_and_misaligned_fallback(v):
                 return to_NUMPY(sv.solution()), int(lib.pxa_pgd_tv2d_last_kernel())
         return _with_kernel(kv, go)
 
-    (xt, kt), (xs_, ks) = traj(1), traj(v)
+    try:
+        (xt, kt), (xs_, ks) = traj(1), traj(v)
+    finally:
+        pxa.Solver._LAG = lag0
     assert kt == 1 and ks == 2
     assert np.array_equal(xt, xs_)
     s = _plan((200, 260), 1, 1, 2.0, "pos")
