@@ -569,6 +569,7 @@ class Solver:
     # (PXA_LAG_WINDOW=0: the epilogue statistics, bit-identical history)
     _LAG_WINDOW = os.environ.get("PXA_LAG_WINDOW", "1") == "1"
     _LAG_RECORDS = 4  # deferred history records written per batch by the lagged engine
+    _LAG_MAX_BYTES = int(float(os.environ.get("PXA_LAG_MAX_BYTES", str(16 * 2**30))))  # iterates held in flight
 
     def _lag_supported(self) -> bool:
         return False
@@ -609,6 +610,11 @@ class Solver:
             return None
         r = rels[0]
         if r._var not in ast["log_var"] or r._norm != 2 or r._f is not pxst._identity or r._reduce is not None:
+            return None
+        # the held states of the checks in flight: at most ~(_LAG + 3) iterates of the size of `var` at once
+        v = self._mstate.get(r._var)
+        nbytes = int(v.numel()) * int(v.element_size()) if hasattr(v, "numel") else 0
+        if nbytes * (self._LAG + 3) > self._LAG_MAX_BYTES:
             return None
         return r, maxs
 

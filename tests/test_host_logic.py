@@ -612,3 +612,50 @@ def test_profile_hooks_wrap_m_step(monkeypatch):
     s.m_step()
     assert calls == ["step"]
     assert profile._roctx().roctxRangePushA(b"x") >= 0 and profile._roctx().roctxRangePop() >= -1  # loads here
+
+
+def test_lagged_stop_check_eligibility():
+    """abc/solver.py _lag_plan: the lagged engine (round 6) applies only to stop_rate 1, BLOCK / MANUAL mode, no
+    checkpoints / objective tracking, an OR of MaxIter and exactly one plain RelError on a logged variable, a solver
+    that supports it, and iterates small enough to hold ~_LAG + 3 of (host logic only; the GPU tests pin the engine's
+    results, tests/test_gpu_solver_lag.py)."""
+    import pyxu_amd.distributed as pd
+
+    class _S(pxa.Solver):
+        def _lag_supported(self):
+            return True
+
+    class _Iterate:  # the size of a float32 iterate (no allocation)
+        def __init__(self, n):
+            self.n = n
+
+        def numel(self):
+            return self.n
+
+        def element_size(self):
+            return 4
+
+    def plan(crit, stop_rate=1, mode=pxa.Mode.BLOCK, wb=None, track=False, n=16, supported=True):
+        s = _S(show_progress=False, stop_rate=stop_rate, log_var=("x",), _internal=False)
+        s._astate.update(stop_crit=crit, mode=mode, wb_rate=wb, track_objective=track)
+        s._mstate["x"] = _Iterate(n)
+        if not supported:
+            s._lag_supported = lambda: False
+        return s._lag_plan()
+
+    ok = plan(pxst.MaxIter(10) | pxst.RelError(eps=1e-3))
+    assert ok is not None and type(ok[0]) is pxst.RelError and len(ok[1]) == 1
+    assert plan(pxst.RelError(eps=1e-3)) is not None
+    assert plan(pxst.MaxIter(3) | (pxst.RelError(eps=1e-3) | pxst.MaxIter(5)))[1][1]._n == 5
+    assert plan(pxst.MaxIter(10) | pxst.RelError(eps=1e-3), mode=pxa.Mode.MANUAL) is not None
+    for bad in (dict(stop_rate=2), dict(mode=pxa.Mode.ASYNC), dict(wb=1), dict(track=True), dict(supported=False)):
+        assert plan(pxst.MaxIter(10) | pxst.RelError(eps=1e-3), **bad) is None, bad
+    assert plan(pxst.MaxIter(10) & pxst.RelError(eps=1e-3)) is None  # AND: the decision is not RelError's alone
+    assert plan(pxst.AbsError(eps=1e-3) | pxst.RelError(eps=1e-3)) is None
+    assert plan(pxst.RelError(eps=1e-3) | pxst.RelError(eps=1e-2)) is None
+    assert plan(pxst.RelError(eps=1e-3, var="y")) is None  # not a logged variable
+    assert plan(pxst.RelError(eps=1e-3, norm=1)) is None
+    assert plan(pxst.RelError(eps=1e-3, f=lambda v: v)) is None
+    assert plan(pd.ShardedRelError(eps=1e-3)) is None  # its all-reduce per check is a collective: not lagged
+    big = int(_S._LAG_MAX_BYTES // 4 // (_S._LAG + 3)) + 1
+    assert plan(pxst.RelError(eps=1e-3), n=big) is None  # the held iterates would not fit the budget
