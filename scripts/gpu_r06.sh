@@ -31,6 +31,8 @@ pmc_pgd() {  # the headline's PGD counters, one pass each (separate runs: FETCH 
   step pgdwrite 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/pgdwrite -o run --output-format csv -- $DRV
   step pgdsq 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS --kernel-trace -d $P/pgdsq -o run --output-format csv -- $DRV
   step pgdsq2 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES --kernel-trace -d $P/pgdsq2 -o run --output-format csv -- $DRV
+  python3 scripts/pmc_traffic.py $P/pgdfetch $P/pgdwrite "pgd_tv2d_kernel<float, 6>" pgd_tv2d_kernel@2048x2048 $P/traffic_pgd.json $T || true
+  python3 scripts/pmc_sum.py "pgd_tv2d_kernel<float, 6>" $P/pgdfetch $P/pgdwrite $P/pgdsq $P/pgdsq2 > $O/pmc_summary.txt 2>&1 || true
 }
 if [ "$S" = "new" ]; then
   step newtests 900 $PT -m gpu tests/test_gpu_rccl.py tests/test_gpu_fft.py tests/test_gpu_solver_engine.py \
