@@ -61,8 +61,9 @@ SURVEY_BYTES_PER_PIXEL = 48  # 8 reads + 4 writes of fp32 p
 MFMA_F32_PEAK_TF = 157.3  # dense fp32 MFMA peak (MI355X_MICROARCH.md, Matrix cores: = the f32 vector peak)
 CPU_THREADS_MAX = 16  # the GPU box's CPU share per GPU (gpurun: 16)
 # pxa_pgd_tv2d_last_kernel() -> (mode name, own compulsory bytes per pixel): the arrays the launch reads / writes
-PGD_MODES = {1: ("x, x_prev, H^T y -> x_new (tile kernel)", 16), 2: ("x, x_prev, H^T y -> x_new (strip kernel)", 16)}
-PGD_KERNELS = {1: "pgd_tv2d_kernel", 2: "pgd_strip_kernel"}  # the rocprof name of each mode's kernel
+PGD_MODES = {1: ("x, x_prev, H^T y -> x_new (tile kernel)", 16), 2: ("x, x_prev, H^T y -> x_new (strip kernel)", 16),
+             3: ("x, x_prev, H^T y -> x_new (pipelined kernel)", 16)}
+PGD_KERNELS = {1: "pgd_tv2d_kernel", 2: "pgd_strip_kernel", 3: "pgd_pipe_kernel"}  # the rocprof name of each mode's kernel
 
 
 # ----------------------------------------------------------------------------- launcher (no GPU here)

@@ -101,7 +101,11 @@ extern "C" {
 #define PXA_TUNE_DUAL_ROWS 11 /* A/B of the PDS dual-update kernel C (pxa_tv_dual_update, the three-launch step): rows of w
                                 * per thread, 0 / 1 the one-row kernel, 2 or 4 the row-blocked kernel (a thread's row + 1
                                 * neighbours are its own rows).  Same bits. */
-#define PXA_TUNE_COUNT 12
+#define PXA_TUNE_PGD_PIPE 12 /* A/B of the fused PGD step: 1 the pipelined kernel (two resident workgroups per CU, each
+                               * walking its XCD's tiles, the next tile's x / x_prev window fetched by LDS-DMA into a
+                               * staging area during the current tile; fp32, 16-B aligned rows, R <= 7).  Same bits;
+                               * measured slower (profiles/r06n_pgd_pipe_ab.txt). */
+#define PXA_TUNE_COUNT 13
 
 /* Row reductions (pxa_row_reduce). */
 #define PXA_RED_SUMSQ 0  /* sum x^2            : SquaredL2Norm.apply, norm(ord=2)^2   (norm.py:91-94) */
@@ -473,7 +477,8 @@ int pxa_dir_contract(int dtype, int64_t S, int64_t G, int64_t J, int64_t K, int6
  * iterate of the previous check (opt/stop.py:353-382) — pxa_pgd_tv2d_partials_count() gives the
  * number of slots (tiles x 4; the slots of one image are contiguous).  prox codes: 0 none, 1 positive
  * orthant, 2 l1 with weight prox_w.  pxa_pgd_tv2d_last_kernel() is the kernel the calling thread launched
- * last: 1 the tile kernel, 2 the strip kernel (PXA_TUNE_PGD_KERNEL), 0 none yet.
+ * last: 1 the tile kernel, 2 the strip kernel (PXA_TUNE_PGD_KERNEL), 3 the pipelined kernel (PXA_TUNE_PGD_PIPE), 0 none
+ * yet.
  * ------------------------------------------------------------------------------------------- */
 int pxa_pgd_tv2d_partials_count(int64_t stack, int64_t n0, int64_t n1);
 /* Prepared form of pxa_pgd_tv2d_step for a solver's iterations (replaces the same call per PGD.m_step,

@@ -218,6 +218,7 @@ TUNE_PDS_MARCH = 7  # PXA_TUNE_PDS_MARCH: kernel D A/B (bit 0: two positions per
 TUNE_FFT_KERNEL = 8  # PXA_TUNE_FFT_KERNEL: 0 in-place register-staged FFT kernel, 1 the ping-pong Stockham kernel
 TUNE_GRAD_KERNEL = 9  # PXA_TUNE_GRAD_KERNEL: 0 axis-0 march gradient kernels, 1 the row kernels (same bits)
 TUNE_STENCIL_ND = 10  # PXA_TUNE_STENCIL_ND: 0 LDS-tiled N-D stencil where it applies, 1 the generic kernel (same sums)
+TUNE_PGD_PIPE = 12  # PXA_TUNE_PGD_PIPE: 1 the pipelined PGD kernel (LDS-DMA window prefetch; same bits, slower)
 TUNE_DUAL_ROWS = 11  # PXA_TUNE_DUAL_ROWS: kernel C rows per thread (0 / 1 one-row kernel, 2 or 4 row-blocked; same bits)
 
 

@@ -91,6 +91,8 @@ struct PgdParams {
   int64_t fold_rows, fold_per_row;
   // strip kernel (pgd_strip_kernel): tiles per strip, strip groups per tile column of an image, strips in all
   unsigned slen, sgroups, nstrips;
+  // pipelined kernel (pgd_pipe_kernel): resident tile workgroups (0: not that kernel)
+  unsigned pipe_wgs;
   // window partials (pxa_pgd_tv2d_plan_step_wfold): the per-(tile, wave) partials are (sum (x - x_prev)^2, sum x_prev^2)
   // over the tile, from the window loads -- the RelError statistics of the PREVIOUS step's check -- instead of the
   // epilogue's (x_new - x_ref) statistics: no extra load of x
@@ -559,10 +561,23 @@ struct NoHook {
   __device__ void operator()() const {}
 };
 
+// Workgroup barrier of a tile body.  RB: the raw form (LDS operations complete, then s_barrier) for the pipelined
+// kernel, whose next window is in flight by LDS-DMA during the body -- __syncthreads()'s fence would wait for it
+// (an LDS-DMA is a pending LDS write on the VM counter) at every barrier.  The body's own global loads land in
+// registers, which the compiler waits for at their use, so the raw form orders everything the body shares.
+template <bool RB>
+__device__ inline void body_sync() {
+  if constexpr (RB) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else {
+    __syncthreads();
+  }
+}
+
 // The phases of one output tile once its window is in A (behind a barrier): pass A, [ghost columns], pass B
 // (parked in registers), the H^T y / x loads, O staging, row-major epilogue, [RelError partials].  `mid` runs at the
 // strip kernel's prefetch point; `xarea23`: see tv_exchange (nullptr in the tile kernel).
-template <typename T, int R, bool EDGE, int D, typename Mid>
+template <typename T, int R, bool EDGE, int D, bool RB, typename Mid>
 __device__ inline void pgd_tile_body(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
                                      const T* __restrict__ bs, T* __restrict__ xns, double* __restrict__ partials,
                                      const T* __restrict__ xrs, T* xarea23, Mid&& mid, const int tid) {
@@ -588,11 +603,11 @@ __device__ inline void pgd_tile_body(const PgdParams<T>& p, unsigned char* smem,
   const bool skip_passes = kProbes && (p.diag & 64) != 0;  // timing probe only (WRONG results)
   if (!skip_passes) pass_a<T, R, EDGE, D>(p, A, PT, KT, ty0, tid);
   tmark(3);
-  __syncthreads();
+  body_sync<RB>();
   if (PXA_PGD_STRIP_ISSUE == 0) mid();
   if (edge_cols) {
     ghost_cols_coop<T, R>(p.k1, PT, GH, tx0, n1, tid);
-    __syncthreads();
+    body_sync<RB>();
   }
   tmark(4);
   T st[KB][V][CW];
@@ -627,7 +642,7 @@ __device__ inline void pgd_tile_body(const PgdParams<T>& p, unsigned char* smem,
 #endif
   }
   tmark(5);
-  __syncthreads();  // every G1 sweep is done with PT: O may overwrite it
+  body_sync<RB>();  // every G1 sweep is done with PT: O may overwrite it
   T* O = PT;
 #pragma unroll
   for (int k = 0; k < KB; ++k) {
@@ -651,7 +666,7 @@ __device__ inline void pgd_tile_body(const PgdParams<T>& p, unsigned char* smem,
   // x (RelError partials only) is loaded once pass B's parked results are out of the registers
   if (want_part) load_staged<T, R, EDGE>(p, ty0, tx0, xrs, hb.x, tid);
   if (PXA_PGD_STRIP_ISSUE != 0) mid();
-  __syncthreads();
+  body_sync<RB>();
   tmark(6);
 #if PXA_PGD_PRIO_FIN
   __builtin_amdgcn_s_setprio(PXA_PGD_PRIO_FIN);  // A/B builds: the finishing stores ahead of other passes
@@ -683,6 +698,30 @@ __device__ inline void pgd_tile_body(const PgdParams<T>& p, unsigned char* smem,
 }
 
 
+// The previous check's RelError statistics over this tile's pixels, from its window (win_part): sum (x - x_prev)^2,
+// sum x_prev^2 per wave (outside the image both are 0: no contribution).
+template <typename T, int R>
+__device__ inline void win_partials(const Window<T, R>& w, double* __restrict__ partials, unsigned tile, const int tid) {
+  using L = Layout<T, R>;
+  double part_d = 0.0, part_x = 0.0;
+#pragma unroll
+  for (int k = 0; k < Window<T, R>::K0; ++k) {
+    const int it = tid + k * kThreads;
+    if (it < L::N0) {
+      const int r = it / L::NGA, g = it - r * L::NGA;
+      if (r >= 2 * R && r < 2 * R + TY && L::V * g >= L::CA && L::V * g < L::CA + TX) {
+#pragma unroll
+        for (int v = 0; v < L::V; ++v) {
+          const double dd = (double)w.xv[k][v] - (double)w.pv[k][v];
+          part_d = fma(dd, dd, part_d);
+          part_x = fma((double)w.pv[k][v], (double)w.pv[k][v], part_x);
+        }
+      }
+    }
+  }
+  wave_partials(part_d, part_x, partials, tile * kPartWaves + (tid >> 6));
+}
+
 // One output tile of the tile kernel: phase 0 (window) into A, then the body.
 template <typename T, int R, bool EDGE>
 __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsigned tile, int ty0, int tx0,
@@ -711,32 +750,14 @@ __device__ inline void pgd_tile(const PgdParams<T>& p, unsigned char* smem, unsi
     Window<T, R> w;
     win_issue<T, R, EDGE>(p, ty0, tx0, xs, xps, w, tid);
     win_store<T, R>(p, A, w, tid);
-    if (p.win_part && partials != nullptr) {  // the previous check's RelError statistics over this tile's pixels
-      double part_d = 0.0, part_x = 0.0;
-#pragma unroll
-      for (int k = 0; k < Window<T, R>::K0; ++k) {
-        const int it = tid + k * kThreads;
-        if (it < L::N0) {
-          const int r = it / L::NGA, g = it - r * L::NGA;
-          if (r >= 2 * R && r < 2 * R + TY && L::V * g >= L::CA && L::V * g < L::CA + TX) {
-#pragma unroll
-            for (int v = 0; v < L::V; ++v) {  // (outside the image both are 0: no contribution)
-              const double dd = (double)w.xv[k][v] - (double)w.pv[k][v];
-              part_d = fma(dd, dd, part_d);
-              part_x = fma((double)w.pv[k][v], (double)w.pv[k][v], part_x);
-            }
-          }
-        }
-      }
-      wave_partials(part_d, part_x, partials, tile * kPartWaves + (tid >> 6));
-    }
+    if (p.win_part && partials != nullptr) win_partials<T, R>(w, partials, tile, tid);
   }
 #if PXA_PGD_PRIO
   __builtin_amdgcn_s_setprio(0);
 #endif
   tmark(1);
   __syncthreads();
-  pgd_tile_body<T, R, EDGE, PXA_PGD_SWEEP_DEPTH>(p, smem, tile, ty0, tx0, bs, xns, p.win_part ? nullptr : partials, xrs,
+  pgd_tile_body<T, R, EDGE, PXA_PGD_SWEEP_DEPTH, false>(p, smem, tile, ty0, tx0, bs, xns, p.win_part ? nullptr : partials, xrs,
                                                  nullptr, NoHook{}, tid);
 }
 
@@ -785,8 +806,7 @@ __device__ inline void tail_fold(const PgdParams<T>& p, const double* __restrict
 // no registers to the tile kernel's allocation), the values stored write-through to host memory
 // (system-scope relaxed atomic stores), then -- once they have completed -- the flags.
 template <typename T>
-__device__ inline void publish_prev(const PgdParams<T>& p) {
-  __shared__ double red[kThreads / 64];
+__device__ inline void publish_prev(const PgdParams<T>& p, double* red) {
   for (int64_t q = 0; q < 2 * p.fold_rows; ++q) {
     const int64_t stat = q / p.fold_rows, r = q - stat * p.fold_rows;
     const double t = fold_tile_stat<false>(p.pub_src + 2 * r * p.fold_per_row + stat, p.fold_per_row, red);
@@ -805,7 +825,8 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
   if (p.pub_src != nullptr && blockIdx.x == p.ntiles) {  // (no barrier shared with the tile workgroups)
-    publish_prev<T>(p);
+    __shared__ double red[kThreads / 64];
+    publish_prev<T>(p, red);
     return;
   }
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -996,9 +1017,9 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_strip_kernel(PgdParams<T> p, 
     // (issued for the last tile of the strip too, clamped into the image, so that no branch guards the loads)
     auto issue = [&]() { rows_issue<T, R>(p, ty0 + TY, tx0, xs, xps, nw, ltid); };
     if (cols_in && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0)
-      pgd_tile_body<T, R, false, PXA_PGD_STRIP_DEPTH>(p, smem_raw, tile, ty0, tx0, bs, xns, partials, xrs, X23, issue, ltid);
+      pgd_tile_body<T, R, false, PXA_PGD_STRIP_DEPTH, false>(p, smem_raw, tile, ty0, tx0, bs, xns, partials, xrs, X23, issue, ltid);
     else
-      pgd_tile_body<T, R, true, PXA_PGD_STRIP_DEPTH>(p, smem_raw, tile, ty0, tx0, bs, xns, partials, xrs, X23, issue, ltid);
+      pgd_tile_body<T, R, true, PXA_PGD_STRIP_DEPTH, false>(p, smem_raw, tile, ty0, tx0, bs, xns, partials, xrs, X23, issue, ltid);
     if (more) {
       __syncthreads();  // every read of this window is done
       window_advance<T, R>(p, A, nw, ltid);
@@ -1022,10 +1043,201 @@ int launch_pgd_strip(const PgdParams<T>& p, const void* x, const void* xp, const
   return last_launch_status();
 }
 
+// ---- pipelined kernel (PXA_TUNE_PGD_KERNEL = -1): a resident grid of two workgroups per CU, each walking the tiles of
+// its XCD's band (i = blockIdx.x, + grid, ...: the same XCD every time).  The raw x / x_prev window of the NEXT tile is
+// fetched by LDS-DMA (global_load_lds_dwordx4: no VGPR destination, so nothing is held through the passes) into a
+// staging area beside the tile carve while the current tile runs passes A / B and its epilogue; then one pass turns
+// the staged window into yk in A (win_store's arithmetic: the same bits as the tile kernel's phase 0).  The body
+// uses raw barriers (body_sync<true>) so that the fetch stays in flight through them.  LDS: carve 36.4 KB + staging
+// 40 KB = 75.5 KB per workgroup (fp32, R = 6), two per CU; edge tiles are fetched with clamped addresses and their
+// outside vectors zeroed (vec_ok: a 16-B vector lies wholly inside or outside the image).
+template <typename T, int R>
+constexpr int kPipeChunks = cdiv(Layout<T, R>::N0, 64);  // one LDS-DMA wave-instruction = 64 window vectors
+template <typename T, int R>
+constexpr size_t kPipeArr = (size_t)kPipeChunks<T, R> * 64 * 16;  // bytes of one staged window array
+template <typename T, int R>
+constexpr size_t kPipeRawOff = (kGhOff<T, R> + kGhBytes<T, R> + 15) / 16 * 16;
+template <typename T, int R>
+constexpr size_t kPipeBytes = kPipeRawOff<T, R> + 2 * kPipeArr<T, R>;
+
+template <typename T, int R>
+__device__ inline void pipe_issue(const PgdParams<T>& p, unsigned char* raw, int ty0, int tx0, const T* __restrict__ xs,
+                                  const T* __restrict__ xps, const int tid) {
+  using L = Layout<T, R>;
+  constexpr int V = L::V;
+  constexpr int NW = kThreads / 64;
+  static_assert(V * sizeof(T) == 16, "one 16-B vector per lane");
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int n0 = p.n0, n1 = p.n1;
+#pragma unroll
+  for (int k = 0; k < cdiv(kPipeChunks<T, R>, NW); ++k) {
+    const int c = wv + NW * k;
+    if (c < kPipeChunks<T, R>) {
+      int it = c * 64 + lane;
+      if (it >= L::N0) it = L::N0 - 1;  // (the last piece's surplus lanes fill the staging padding)
+      const int r = it / L::NGA, g = it - r * L::NGA;
+      int gr = ty0 - 2 * R + r, gc = tx0 - L::CA + V * g;
+      gr = gr < 0 ? 0 : gr >= n0 ? n0 - 1 : gr;
+      gc = gc < 0 ? 0 : gc > n1 - V ? n1 - V : gc;
+      const int64_t off = (int64_t)gr * n1 + gc;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xs + off),
+                                       (__attribute__((address_space(3))) void*)(raw + (size_t)c * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xps + off),
+                                       (__attribute__((address_space(3))) void*)(raw + kPipeArr<T, R> + (size_t)c * 1024),
+                                       16, 0, 0);
+    }
+  }
+}
+
+// staged window -> yk in A (and the window partials), behind a barrier after every wave's pieces have landed
+template <typename T, int R>
+__device__ inline void pipe_window(const PgdParams<T>& p, T* A, const unsigned char* raw, int ty0, int tx0,
+                                   double* __restrict__ partials, unsigned tile, const int tid) {
+  using L = Layout<T, R>;
+  constexpr int V = L::V;
+  const int n0 = p.n0, n1 = p.n1;
+  const T* rx = reinterpret_cast<const T*>(raw);
+  const T* rp = reinterpret_cast<const T*>(raw + kPipeArr<T, R>);
+  Window<T, R> w;
+#pragma unroll
+  for (int k = 0; k < Window<T, R>::K0; ++k) {
+    const int it = tid + k * kThreads;
+    if (it < L::N0) {
+      const int r = it / L::NGA, g = it - r * L::NGA;
+      const int gr = ty0 - 2 * R + r, gc = tx0 - L::CA + V * g;
+      ld_vec<T, V>(rx + V * it, w.xv[k]);
+      ld_vec<T, V>(rp + V * it, w.pv[k]);
+      if (!(gr >= 0 && gr < n0 && gc >= 0 && gc < n1)) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) w.xv[k][v] = w.pv[k][v] = T(0);
+      }
+    }
+  }
+  win_store<T, R>(p, A, w, tid);
+  if (p.win_part && partials != nullptr) win_partials<T, R>(w, partials, tile, tid);
+}
+
+template <typename T, int R>
+__global__ void __launch_bounds__(kThreads, 2) pgd_pipe_kernel(PgdParams<T> p, const T* __restrict__ x,
+                                                            const T* __restrict__ xp, const T* __restrict__ b,
+                                                            T* __restrict__ xn, double* __restrict__ partials) {
+  using L = Layout<T, R>;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const unsigned nw = p.pipe_wgs;
+  if (p.pub_src != nullptr && blockIdx.x == nw) {  // the publishing workgroup (its reduction area: the carve's start)
+    publish_prev<T>(p, reinterpret_cast<double*>(smem_raw));
+    return;
+  }
+  T* A = reinterpret_cast<T*>(smem_raw);
+  T* KT = A + L::AR * L::AP + L::AC * L::PTP;
+  unsigned char* raw = smem_raw + kPipeRawOff<T, R>;
+  const int tid = threadIdx.x;
+  if (tid < 2 * R + 1) {
+    KT[tid] = p.k0[tid];
+    KT[kKT + tid] = p.k1[tid];
+  }
+  const unsigned tpi = (unsigned)p.tiles0 * (unsigned)p.tiles1;
+  const int64_t img = (int64_t)p.n0 * p.n1;
+  // virtual block index -> (tile, image, tile origin), as the tile kernel maps its block index (XCD band, the last
+  // band backwards)
+  auto locate = [&](unsigned i, unsigned& tile, unsigned& si, int& ty0, int& tx0) {
+    tile = xcd_tile(i, p.ntiles);
+    const unsigned nb = p.ntiles, q8 = nb >> 3, r8 = nb & 7u, g8 = i & 7u;
+    if (g8 == 7u) {
+      const unsigned lo = 7u * q8 + (r8 < 7u ? r8 : 7u), len = q8 + (7u < r8 ? 1u : 0u);
+      tile = lo + (len - 1u - (tile - lo));
+    }
+    si = tile / tpi;
+    const unsigned tr = tile - si * tpi, trow = tr / (unsigned)p.tiles1;
+    ty0 = (int)trow * TY;
+    tx0 = (int)(tr - trow * (unsigned)p.tiles1) * TX;
+  };
+  unsigned i = blockIdx.x, tile, si;
+  int ty0, tx0;
+  locate(i, tile, si, ty0, tx0);
+  pipe_issue<T, R>(p, raw, ty0, tx0, x + (int64_t)si * img, xp + (int64_t)si * img, tid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  body_sync<true>();
+  pipe_window<T, R>(p, A, raw, ty0, tx0, partials, tile, tid);
+  using KP = const __attribute__((address_space(4))) PgdParams<T>*;
+  for (;;) {
+    // the parameters re-read (scalar loads from the kernel-argument segment) per tile: hoisted out of the loop, the
+    // taps and geometry stay live across it and spill
+    KP kp = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    const PgdParams<T>& p = *(const PgdParams<T>*)kp;
+    body_sync<true>();  // A holds this tile's window; the staging area is free
+    const unsigned inext = i + nw;
+    const bool more = inext < p.ntiles;
+    unsigned tile_n = 0, si_n = 0;
+    int ty0n = 0, tx0n = 0;
+    if (more) {
+      locate(inext, tile_n, si_n, ty0n, tx0n);
+      pipe_issue<T, R>(p, raw, ty0n, tx0n, x + (int64_t)si_n * img, xp + (int64_t)si_n * img, tid);
+    }
+    const T* bs = b + (int64_t)(si % (unsigned)p.y_images) * img;
+    T* xns = xn + (int64_t)si * img;
+    const T* xrs = (p.xref != nullptr ? p.xref : x) + (int64_t)si * img;
+    const bool interior = img <= 0x7fffffff && ty0 - 2 * R >= 0 && ty0 + TY + 2 * R <= p.n0 && tx0 - L::CA >= 0 &&
+                          tx0 + TX + L::CA <= p.n1;
+    double* bp = p.win_part ? nullptr : partials;
+    if (interior)
+      pgd_tile_body<T, R, false, PXA_PGD_SWEEP_DEPTH, true>(p, smem_raw, tile, ty0, tx0, bs, xns, bp, xrs, nullptr,
+                                                            NoHook{}, tid);
+    else
+      pgd_tile_body<T, R, true, PXA_PGD_SWEEP_DEPTH, true>(p, smem_raw, tile, ty0, tx0, bs, xns, bp, xrs, nullptr,
+                                                           NoHook{}, tid);
+    if (!more) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of the next window have landed
+    body_sync<true>();                                 // ... every wave's, and every read of A by this tile is done
+    pipe_window<T, R>(p, A, raw, ty0n, tx0n, partials, tile_n, tid);
+    i = inext;
+    tile = tile_n;
+    si = si_n;
+    ty0 = ty0n;
+    tx0 = tx0n;
+  }
+}
+
+// resident workgroups per CU of the pipelined kernel, and the CU count of the current device (cached per device)
+constexpr int kPipePerCu = 2;
+inline int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+template <typename T, int R>
+int launch_pgd_pipe(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
+                    hipStream_t s) {
+  const size_t smem = kPipeBytes<T, R>;
+  auto kern = pgd_pipe_kernel<T, R>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(p.pipe_wgs + (p.pub_src != nullptr ? 1u : 0u)), dim3(kThreads), smem, s, p, (const T*)x,
+                     (const T*)xp, (const T*)b, (T*)xn, partials);
+  return last_launch_status();
+}
+
 template <typename T, int R>
 int launch_pgd(const PgdParams<T>& p, const void* x, const void* xp, const void* b, void* xn, double* partials,
                hipStream_t s) {
   constexpr bool strip_fits = kStripXOff<T, R> + kStripXBytes <= (size_t)160 * 1024;  // (fp64 at large R: no)
+  constexpr bool pipe_fits = sizeof(T) == 4 && kPipeBytes<T, R> * kPipePerCu <= (size_t)160 * 1024;
+  if (pipe_fits && p.pipe_wgs > 0) {
+    const int e = launch_pgd_pipe<T, R>(p, x, xp, b, xn, partials, s);
+    if (e == PXA_OK) g_last_pgd_kernel = 3;
+    return e;
+  }
   if (strip_fits && p.slen >= 2) {
     const int e = launch_pgd_strip<T, R>(p, x, xp, b, xn, partials, s);
     if (e == PXA_OK) g_last_pgd_kernel = 2;
@@ -1148,6 +1360,15 @@ int pgd_run(PgdParams<T> p, int R, double a, double tau, double prox_w, const vo
     const int64_t ns = p.stack * (int64_t)p.sgroups * p.tiles1;
     p.nstrips = (unsigned)ns;
     if (ns > 0x7fffffff || win_part || pub_src) p.slen = 1;  // (window partials / publication: the tile kernel)
+    // PXA_TUNE_PGD_PIPE = 1: the pipelined kernel (whole 16-B vectors only; not with the last-workgroup fold)
+    p.pipe_wgs = 0;
+    if (tuning(PXA_TUNE_PGD_PIPE) == 1 && p.vec_ok && rel_values == nullptr) {
+      const unsigned cap = (unsigned)(kPipePerCu * device_cus());
+      unsigned nw = p.ntiles < cap ? p.ntiles : cap;
+      if (nw >= 8) nw -= nw % 8;  // a multiple of 8: every workgroup stays on its XCD's band
+      p.pipe_wgs = nw;
+      p.slen = 1;
+    }
   }
   int st;
   switch (R) {

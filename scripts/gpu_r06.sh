@@ -52,6 +52,13 @@ if [ "$S" = "strip" ]; then
   PXA_TUNE=0=1 step c4096_tile 300 python3 bench.py --only c2_4096
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
 fi
+if [ "$S" = "pipe" ]; then  # the pipelined PGD kernel (PXA_TUNE 12=1) against the tile kernel (default)
+  step pipetests 600 $PT -m gpu tests/test_gpu_pgd_variants.py
+  for i in 1 2; do
+    PXA_TUNE=12=1 step drv_pipe_$i 120 $DRV
+    step drv_tile_$i 120 $DRV
+  done
+fi
 if [ "$S" = "k4" ]; then
   step k4tests 600 $PT -m gpu tests/test_gpu_pds_fused.py -k "tv_dual"
   for i in 1 2; do

@@ -70,7 +70,7 @@ def _launch(s, x, xp, hty, a, parts=None):
     out = _dev.empty_like(x)
     _dev.pgd_tv2d_step(x, xp, hty, out, p["stack"], p["B"], p["n0"], p["n1"], p["taps0"], p["taps1"], p["h0"],
                        p["h1"], p["lam"], p["mu"], a, m["tau"], p["prox"], m["tau"] * p["prox_scale"], partials=parts)
-    assert int(lib.pxa_pgd_tv2d_last_kernel()) in (1, 2)  # tile or strip kernel (PXA_TUNE_PGD_KERNEL)
+    assert int(lib.pxa_pgd_tv2d_last_kernel()) in (1, 2, 3)  # tile, strip or pipelined kernel (PXA_TUNE_PGD_KERNEL)
     return out
 
 
@@ -269,3 +269,80 @@ def test_strip_kernel_solver_trajectory_and_misaligned_fallback(v):
     ref = _with_kernel(1, lambda: _launch(s, m["x"], m["x_prev"], p["hty"], 0.37))
     torch.cuda.synchronize()
     assert np.array_equal(to_NUMPY(out), to_NUMPY(ref))
+
+
+def _with_pipe(on, fn):
+    old = _dev.tuning(_dev.TUNE_PGD_PIPE, 1 if on else 0)
+    try:
+        return fn()
+    finally:
+        _dev.tuning(_dev.TUNE_PGD_PIPE, old)
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0][0]}x{c[0][1]}-s{c[1]}-y{c[2]}-sig{c[3]}-{c[4]}")
+def test_pipe_kernel_matches_tile_kernel(case):
+    """The pipelined kernel (PXA_TUNE_PGD_PIPE = 1; opt-in, measured slower: resident workgroups, the next tile's window
+    fetched by LDS-DMA during the current tile) against the tile kernel: x_new and the RelError partials bit for bit,
+    with and without partials, on every shape class (edge tiles fetched clamped and zeroed, fewer tiles than
+    workgroups, stacks); misaligned arrays and R = 8 (its LDS would not fit twice per CU) keep the tile kernel."""
+    sh, stack, y_images, sigma, g_kind = case
+    s = _plan(sh, stack, y_images, sigma, g_kind)
+    m, p = s._mstate, s._plan
+    x, xp, hty = m["x"], m["x_prev"], p["hty"]
+
+    def run(on, with_parts=True):
+        parts = _parts(s) if with_parts else None
+        out = _with_pipe(on, lambda: _launch(s, x, xp, hty, 0.37, parts))
+        kern = int(lib.pxa_pgd_tv2d_last_kernel())
+        torch.cuda.synchronize()
+        return to_NUMPY(out), (to_NUMPY(parts) if with_parts else None), kern
+
+    ref, ref_parts, k1 = run(False)
+    got, got_parts, k = run(True)
+    assert (k1, k) == (1, 1 if sigma == 2.5 else 3)  # (sigma 2.5: R = 8)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(got_parts, ref_parts)
+    got2, _, _ = run(True, with_parts=False)
+    assert np.array_equal(got2, ref)
+    if sh == (300, 260):
+        out = _with_pipe(True, lambda: _launch(s, _misaligned(x), _misaligned(xp), _misaligned(hty), 0.37))
+        assert int(lib.pxa_pgd_tv2d_last_kernel()) == 1
+        torch.cuda.synchronize()
+        assert np.array_equal(to_NUMPY(out), ref)
+
+
+@pytest.mark.parametrize("lag", [0, 8])
+def test_pipe_kernel_solver_trajectory(lag):
+    """PGD iterations through the solver at stop_rate 1 with the pipelined kernel give the tile kernel's iterates,
+    stop iteration and RelError history bit for bit: through the speculative engine (lag 0: epilogue partials + fold
+    launch) and the lagged one (lag 8: window partials, publication by the extra workgroup).  eps is set from a
+    first run so that RelError stops the solve mid-run."""
+    pxa.Solver._LAG, lag0 = lag, pxa.Solver._LAG
+
+    def traj(on, eps):
+        def go():
+            f, g, dim, rng = _problem((260, 300), 1, 2.0, "pos")
+            with pxrt.Precision(pxrt.Width.SINGLE):
+                sv = pxs.PGD(f=f, g=g, show_progress=False, stop_rate=1)
+                sv.fit(x0=to_device(rng.uniform(0, 1, dim).astype(np.float32)),
+                       stop_crit=pxst.MaxIter(60) | pxst.RelError(eps=eps), mode=pxa.Mode.MANUAL)
+                for _ in sv.steps():
+                    pass
+                hist = sv.stats()[1]
+                return (to_NUMPY(sv.solution()), int(lib.pxa_pgd_tv2d_last_kernel()), int(sv._astate["idx"]),
+                        {k: np.asarray(hist[k]) for k in hist.dtype.names})
+        return _with_pipe(on, go)
+
+    try:
+        _, _, _, h0 = traj(False, 1e-30)
+        key = next(k for k in h0 if k.startswith("RelError"))
+        eps = float(h0[key][25]) * (1 + 1e-9)
+        (xt, kt, it_t, ht), (xp_, kp, it_p, hp) = traj(False, eps), traj(True, eps)
+    finally:
+        pxa.Solver._LAG = lag0
+    assert kt == 1 and kp == 3
+    assert it_t == it_p and 1 < it_t < 59
+    assert np.array_equal(xt, xp_)
+    assert ht.keys() == hp.keys()
+    for k in ht:
+        assert np.array_equal(ht[k], hp[k]), k
