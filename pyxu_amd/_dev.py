@@ -632,7 +632,10 @@ def wait_flags(flags, seq, spin_s, stream_idle):
     look will never change: raise FlagWaitError (the wait used to spin forever there)."""
     import time
 
-    if (flags == seq).all():
+    if len(flags) == 2:  # (one row: two flags, compared as scalars -- ~20x cheaper than the array compare)
+        if flags[0] == seq and flags[1] == seq:
+            return
+    elif (flags == seq).all():
         return
     t_end = time.perf_counter() + spin_s
     while not (flags == seq).all():
@@ -670,6 +673,13 @@ class HostFlagBuffer:
     @property
     def stats(self):
         return self.values.reshape(2, self.rows)
+
+    def landed(self, seq):
+        """Whether every flag of publication `seq` is set (no wait)."""
+        f = self.flags
+        if len(f) == 2:
+            return bool(f[0] == seq and f[1] == seq)
+        return bool((f == seq).all())
 
     def next_seq(self):
         """A new publication number, for a kernel about to be launched on the CURRENT stream: that stream is

@@ -636,13 +636,17 @@ class Solver:
         prec = pxrt.getPrecision().value
         pend = collections.deque()
         ast["lag"] = pend
+        win = self._LAG_WINDOW
         try:
             while True:
                 idx = ast["idx"]
                 e = Solver._LagCheck()
                 e.idx, e.snap, e.rel_prev = idx, self._lag_snapshot(), rel._x_prev
                 # window statistics need a next launch: not for the check at which MaxIter ends the run
-                rel._window_stats = self._LAG_WINDOW and not any(m._i + 1 > m._n for m in maxs)
+                last = False  # MaxIter ends the run at this check
+                for m in maxs:
+                    last = last or m._i + 1 > m._n
+                rel._window_stats = win and not last
                 e.resolve = crit.stop_async(mst)
                 e.pre = crit.info()  # MaxIter counts of this check (the RelError value is filled in when resolved)
                 e.counts = [m._i for m in maxs]
@@ -651,8 +655,7 @@ class Solver:
                 e.stamp, e.log = dt.datetime.now(), (idx % ast["log_rate"] == 0) and log_on
                 e.post = e.info = None
                 pend.append(e)
-                host_stop = any(m._i > m._n for m in maxs)  # MaxIter ends the run at this check (OR composite)
-                if kind == "event" or host_stop:
+                if kind == "event" or last:  # (OR composite: MaxIter's stop() above returned True exactly when `last`)
                     self._lag_flush()
                     drain = len(pend)  # a one-buffer statistic, or the last check: resolve everything now
                 else:

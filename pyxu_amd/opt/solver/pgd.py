@@ -162,6 +162,35 @@ class PGD(pxa.Solver):
         self._wpub_pending = None
         self._spare = None
         self._x_check = None
+        self.__dict__.pop("_pool", None)
+
+    # Output buffers under the lagged engine: the held check states keep the old x_prev referenced, so the refcount
+    # recycling below never finds it free and every step would allocate (torch.empty_like: several us of host time
+    # per step at stop_rate 1, where the host sets the pace).  Retired iterates wait in a small pool instead and are
+    # reused once nothing references them (the same refcount + storage test: a held state, a steps() item or a user
+    # view keeps a buffer out of reuse).
+    _POOL_MAX = 16
+
+    def _pool_take(self, x, xp):
+        pool = self.__dict__.get("_pool")
+        if pool:
+            for i in range(len(pool)):
+                b = pool[i]
+                # references: the pool's, b, getrefcount's argument
+                if (sys.getrefcount(b) == 3 and b is not x and b is not xp and b.shape == x.shape and b.dtype == x.dtype
+                        and _dev.storage_exclusive(b)):
+                    del pool[i]
+                    return b
+        return _dev.empty_like(x)
+
+    def _pool_put(self, b):
+        if self._astate.get("lag") is None:  # (only while the lagged engine runs; emptied when it ends)
+            self.__dict__.pop("_pool", None)
+            return
+        pool = self.__dict__.setdefault("_pool", [])
+        pool.append(b)
+        if len(pool) > self._POOL_MAX:
+            del pool[0]
 
     def m_step(self):
         mst = self._mstate
@@ -179,7 +208,7 @@ class PGD(pxa.Solver):
             x, xp = mst["x"], mst["x_prev"]
             out = self._spare
             if out is None or out is x or out is xp:
-                out = _dev.empty_like(x)
+                out = self._pool_take(x, xp)
             tau = mst["tau"]
             wnd = mst.pop("__relerr_window__", None)
             if wnd is not None:
@@ -202,6 +231,8 @@ class PGD(pxa.Solver):
                 self._spec_refs = 0
                 self._spare = xp if (sys.getrefcount(xp) == refs and xp.data_ptr() != x.data_ptr()
                                      and _dev.storage_exclusive(xp)) else None
+                if self._spare is None:
+                    self._pool_put(xp)
                 return
             # RelError partials only for the launch right before a stop check (the engine advances idx
             # before m_step: the next check runs at idx when idx % stop_rate == 0).  RelError compares with

@@ -5,6 +5,7 @@ Norms are evaluated on the device (``pxa_row_reduce``, double accumulation) and 
 scalars cross to the host — the single device->host sync of a stop check (stop.py:381).
 """
 import datetime as dt
+import math
 import numbers
 import os
 
@@ -258,13 +259,17 @@ class RelError(pxa.StoppingCriterion):
             return None
         return h
 
+    def _decide1(self, n, d, shape):
+        """_decide for one row from the two finished statistics as host floats."""
+        decision = n <= self._eps * d
+        v = n / d if d != 0 else (np.inf if n > 0 else 0.0)
+        v = np.array([0.0 if v != v else v])
+        self._val = v if len(shape) == 0 else v.reshape(*shape, 1)
+        return bool(decision)
+
     def _decide(self, st, shape):
         if st.shape[-1] == 1:  # one row: the same decision and value in host floats (no numpy temporaries)
-            n, d = float(st[0, 0]), float(st[1, 0])
-            decision = n <= self._eps * d
-            v = n / d if d != 0 else (np.inf if n > 0 else 0.0)
-            self._val = np.reshape(np.float64(0.0 if v != v else v), (*shape, 1))
-            return bool(decision)
+            return self._decide1(float(st[0, 0]), float(st[1, 0]), shape)
         num = st[0].reshape(*shape, 1)
         den = st[1].reshape(*shape, 1)
         rule = np.all if self._satisfy_all else np.any
@@ -352,11 +357,18 @@ class RelError(pxa.StoppingCriterion):
             self._x_prev = x
             shape = x.shape[:-1]
 
-            def resolve_window():
-                fb.wait(seq)
-                return self._decide(_finish(fb.stats.copy(), self._norm), shape)
+            if rows == 1:  # (the statistics as host floats: sqrt is _finish's numpy power 0.5, exactly rounded)
+                vals = fb.values
 
-            self._last_async = ("fused", lambda: bool((fb.flags == seq).all()))
+                def resolve_window():
+                    fb.wait(seq)
+                    return self._decide1(math.sqrt(vals[0]), math.sqrt(vals[1]), shape)
+            else:
+                def resolve_window():
+                    fb.wait(seq)
+                    return self._decide(_finish(fb.stats.copy(), self._norm), shape)
+
+            self._last_async = ("fused", lambda: fb.landed(seq))
             return resolve_window
         h = self._fused(state, x)
         if h is not None:
@@ -388,7 +400,7 @@ class RelError(pxa.StoppingCriterion):
                 fb.wait(seq)
                 return self._decide(_finish(fb.stats.copy(), self._norm), shape)  # (2, rows) view
 
-            self._last_async = ("fused", lambda: bool((fb.flags == seq).all()))
+            self._last_async = ("fused", lambda: fb.landed(seq))
             return resolve_flags
         # one device / pinned-host statistics pair and one event per criterion, reused: a check is
         # resolved before the next one is issued
@@ -417,7 +429,7 @@ class RelError(pxa.StoppingCriterion):
 
     def info(self):
         if self._val.size == 1:
-            return {f"RelError[{self._var}]": float(self._val.max())}
+            return {f"RelError[{self._var}]": float(self._val.item())}
         return {f"RelError[{self._var}]_min": float(self._val.min()), f"RelError[{self._var}]_max": float(self._val.max())}
 
     def clear(self):

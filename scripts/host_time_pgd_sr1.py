@@ -14,7 +14,8 @@ import pyxu_amd.opt.stop as pxst  # noqa: E402
 import pyxu_amd.runtime as pxrt  # noqa: E402
 from pyxu_amd import _dev  # noqa: E402
 
-f, g, _ = bench.build_problem(2048, 2048, seed=1)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+f, g, _ = bench.build_problem(N, N, seed=1)
 with pxrt.Precision(pxrt.Width.SINGLE):
     like = torch.empty((1,), dtype=torch.float32, device="cuda")
     for sr, crit in ((1, "rel"), (1, "maxiter"), (50, "rel")):
