@@ -126,6 +126,9 @@ def coerce(x):
     if not _state["coerce"]:
         return x
     width = _state["width"]
+    t = type(x)
+    if t is float or t is int:  # (the common case, without the ABC instance checks below: same value)
+        return np.dtype(width.value).type(x)
     if isinstance(x, (numbers.Real, np.number)) and not isinstance(x, (np.complexfloating, complex)):
         return np.array(x, dtype=width.value)[()]
     if _is_tensor(x):

@@ -20,4 +20,5 @@ with pxrt.Precision(pxrt.Width.SINGLE):
     for _ in range(300): next(gen)
     torch.cuda.synchronize(); pr.disable(); dt = time.perf_counter() - t0
     print("us/step", 1e6 * dt / 300)
-    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(45)
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
