@@ -59,6 +59,14 @@ if [ "$S" = "pipe" ]; then  # the pipelined PGD kernel (PXA_TUNE 12=1) against t
     step drv_tile_$i 120 $DRV
   done
 fi
+if [ "$S" = "subtraffic" ]; then  # round-current traffic passes of the c2_4096 and c5 sub-records
+  for leg in c2_4096:pgd_tv2d_kernel@4096x4096 c5:pgd_tv2d_kernel@512x512x512; do
+    o=${leg%%:*}; key=${leg##*:}
+    step fetch_$o 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetch_$o -o run --output-format csv -- python3 bench.py --only $o
+    step write_$o 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/write_$o -o run --output-format csv -- python3 bench.py --only $o
+    python3 scripts/pmc_traffic.py $P/fetch_$o $P/write_$o "pgd_tv2d_kernel<float, 6>" $key $P/traffic_sub.json $T || true
+  done
+fi
 if [ "$S" = "k4" ]; then
   step k4tests 600 $PT -m gpu tests/test_gpu_pds_fused.py -k "tv_dual"
   for i in 1 2; do
