@@ -782,9 +782,12 @@ def bench_c4(ctx, args):
                         "note": "whole CG iteration (operator + CG vector updates + the outer iteration amortised)"}}
     if normal_ms is not None:  # the fused operator reads K once: its own roofline against one pass
         one = (hi - lo) * N * 4
-        rec["normal_operator"] = {"kernel": "normal_rows_kernel + normal_sum/final", "kernel_ms": round(normal_ms, 4),
+        tr, src = measured_traffic("normal_group_kernel", f"{hi - lo}x{N}")
+        rec["normal_operator"] = {"kernel": "normal_group_kernel + normal_sum/final", "kernel_ms": round(normal_ms, 4),
                                   "achieved": round(one / (normal_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(one / (normal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  "traffic": tr, "traffic_source": src,
+                                  "traffic_note": "HBM bytes of the operator pass kernel (normal_group_kernel) per launch",
                                   "note": "K^T K p + p/tau in ONE pass over K (pxa_dense_normal), alg bytes = M N 4"}
     del s, K, Kr
     torch.cuda.empty_cache()

@@ -67,6 +67,13 @@ if [ "$S" = "subtraffic" ]; then  # round-current traffic passes of the c2_4096 
     python3 scripts/pmc_traffic.py $P/fetch_$o $P/write_$o "pgd_tv2d_kernel<float, 6>" $key $P/traffic_sub.json $T || true
   done
 fi
+if [ "$S" = "c4mfma" ]; then  # round-current PMC passes of the c4 operator kernel and the dense MFMA kernels
+  step fetch_c4 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetch_c4 -o run --output-format csv -- python3 bench.py --only c4
+  step write_c4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/write_c4 -o run --output-format csv -- python3 bench.py --only c4
+  python3 scripts/pmc_traffic.py $P/fetch_c4 $P/write_c4 "normal_group_kernel" normal_group_kernel@8192x65536 $P/traffic_c4.json $T || true
+  step mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $P/mfma -o run --output-format csv -- python3 bench.py --only dense_mfma
+  python3 scripts/pmc_mfma.py $P/mfma $P/mfma_busy.json $T > $O/mfma.txt 2>&1 || true
+fi
 if [ "$S" = "k4" ]; then
   step k4tests 600 $PT -m gpu tests/test_gpu_pds_fused.py -k "tv_dual"
   for i in 1 2; do
