@@ -100,7 +100,9 @@ extern "C" {
                                    (same sums either way) */
 #define PXA_TUNE_DUAL_ROWS 11 /* A/B of the PDS dual-update kernel C (pxa_tv_dual_update, the three-launch step): rows of w
                                 * per thread, 0 / 1 the one-row kernel, 2 or 4 the row-blocked kernel (a thread's row + 1
-                                * neighbours are its own rows).  Same bits. */
+                                * neighbours are its own rows), 8 the plane-block kernel (3-D fp32 16-B vectors: an 8 x 128
+                                * block of each plane staged in LDS with its halo row / column; 9: the same with z loaded one plane ahead).  Same
+                                * bits. */
 #define PXA_TUNE_PGD_PIPE 12 /* A/B of the fused PGD step: 1 the pipelined kernel (two resident workgroups per CU, each
                                * walking its XCD's tiles, the next tile's x / x_prev window fetched by LDS-DMA into a
                                * staging area during the current tile; fp32, 16-B aligned rows, R <= 7).  Same bits;

@@ -300,6 +300,155 @@ __global__ void __launch_bounds__(kBlock) pds_dual_rows_kernel(PdsC<T> p, const 
   }
 }
 
+// Plane-block form (3-D, 16-B vectors; PXA_TUNE_DUAL_ROWS = 8): a workgroup owns a block of kLdsRB rows x kLdsC columns
+// of the plane and marches its axis-0 segment; at each plane every thread stores its own w vector into an LDS image
+// of the block (double-buffered by plane parity), the block's halo -- the row below it and the column right of it,
+// fetched one plane ahead -- goes in beside it, and the row + 1 / column + 1 neighbours are read from LDS: a w row is
+// fetched from memory by its own workgroup only, plus once more as the halo of the block above it (1 + 1 / kLdsRB
+// reads per voxel instead of up to 2 with the one-row kernel, whose neighbour rows other workgroups fetch at their
+// own pace).  One barrier per plane.  Same per-element expressions: the same bits.
+constexpr int kLdsRB = 8;    // rows per block
+constexpr int kLdsC = 128;   // columns per block (32 threads x 4)
+constexpr int kLdsP = kLdsC + 4;  // LDS pitch (floats): the halo column's vector at kLdsC
+
+template <bool ISO, bool PD3O, bool ZA>
+__global__ void __launch_bounds__(kBlock) pds_dual_lds_kernel(PdsC<float> p, const float* __restrict__ w,
+                                                              const float* __restrict__ z, float* __restrict__ zo,
+                                                              int tiles2) {
+  static_assert(kBlock == kLdsRB * kLdsC / 4, "one 4-vector per thread");
+  __shared__ __align__(16) float img[2][kLdsRB + 1][kLdsP];
+  const PdsGeom<float> g = p.g;
+  const float sigma = p.sigma, lam = p.lam, rho = p.rho, omr = p.omr;
+  const int n0 = g.n0, n1 = g.n1, n2 = g.n2;
+  const int64_t M = (int64_t)n1 * n2, N = M * n0;
+  const unsigned blk = xcd_tile(blockIdx.x, gridDim.x);
+  const int tr = (int)(blk / (unsigned)tiles2), tc = (int)(blk - (unsigned)tr * (unsigned)tiles2);
+  const int t = threadIdx.x, lr = t >> 5, lc = 4 * (t & 31);
+  const int r = tr * kLdsRB + lr, c = tc * kLdsC + lc;
+  const bool live = r < n1 && c < n2;  // (n2 % 4 == 0: a vector is wholly inside or outside)
+  const int64_t s = blockIdx.z;
+  const int pb = blockIdx.y * p.seg;
+  const int pe = pb + p.seg < n0 ? pb + p.seg : n0;
+  const int64_t j0 = (int64_t)r * n2 + c;
+  const float* wb = w + s * N;
+  const float* zs = z + s * (int64_t)3 * N + j0;
+  float* zos = zo + s * (int64_t)3 * N + j0;
+  // halo lanes: threads 0..31 the row below the block (4 columns each), 32..39 the column right of it (one row each)
+  const int hr = tr * kLdsRB + kLdsRB, hc = tc * kLdsC + lc;        // row halo position (t < 32)
+  const int vr = tr * kLdsRB + (t - 32), vc = tc * kLdsC + kLdsC;   // column halo position (32 <= t < 40)
+  const bool hrow = t < 32, hcol = t >= 32 && t < 32 + kLdsRB;
+  const bool hin = hrow ? (hr < n1 && hc < n2) : hcol ? (vr < n1 && vc < n2) : false;
+  const int64_t hoff = hrow ? (int64_t)hr * n2 + hc : (int64_t)vr * n2 + vc;
+  auto load_w = [&](int pl, float (&v)[4]) {
+    if (live && pl < n0) {
+      ldv<float, 4>(wb + (int64_t)pl * M + j0, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = 0.f;
+    }
+  };
+  auto load_h = [&](int pl, float (&v)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = 0.f;
+    if (hin && pl < n0) {
+      if (hrow)
+        ldv<float, 4>(wb + (int64_t)pl * M + hoff, v);
+      else
+        v[0] = wb[(int64_t)pl * M + hoff];
+    }
+  };
+  float wc[4], wp[4], hc4[4], hn4[4];
+  load_w(pb, wc);
+  load_h(pb, hc4);
+  float zn[3][4];  // z of the next plane (ZA: loaded one plane ahead)
+  auto load_z = [&](int pl, float (&v)[3][4]) {
+    if (live && pl < pe) {
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) ldn_nt<float, 4>(zs + (int64_t)ax * N + (int64_t)pl * M, v[ax]);
+    }
+  };
+  if (ZA) load_z(pb, zn);
+  for (int pl = pb; pl < pe; ++pl) {
+    const int par = pl & 1;
+    const int64_t off = (int64_t)pl * M;
+    float zc[3][4];
+    if (ZA) {
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zc[ax][e] = zn[ax][e];
+    }
+    load_w(pl + 1, wp);  // next plane: own vector and halo, in flight through this plane
+    load_h(pl + 1, hn4);
+    if (ZA)
+      load_z(pl + 1, zn);
+    else
+      load_z(pl, zc);
+    // this plane's w image: own vectors, the halo row / column (zeros outside the image)
+    *reinterpret_cast<float4*>(&img[par][lr][lc]) = make_float4(wc[0], wc[1], wc[2], wc[3]);
+    if (hrow) *reinterpret_cast<float4*>(&img[par][kLdsRB][lc]) = make_float4(hc4[0], hc4[1], hc4[2], hc4[3]);
+    if (hcol) img[par][t - 32][kLdsC] = hc4[0];
+    __syncthreads();  // (double buffer: the next plane writes the other image, so one barrier per plane)
+    if (live) {
+      float wr[4];
+      const float4 q = *reinterpret_cast<const float4*>(&img[par][lr + 1][lc]);
+      wr[0] = q.x, wr[1] = q.y, wr[2] = q.z, wr[3] = q.w;
+      const float wcol = img[par][lr][lc + 4];
+      float zin[3][4];
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        float wn[4];
+        if (ax == 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) wn[e] = wp[e];
+        } else if (ax == 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) wn[e] = r + 1 < n1 ? wr[e] : 0.f;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 3; ++e) wn[e] = wc[e + 1];
+          wn[3] = c + 4 < n2 ? wcol : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zin[ax][e] = dual_in<float>(zc[ax][e], wc[e], wn[e], g.c0[ax], g.c1[ax], sigma);
+      }
+      float zo3[3][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float zc1[3], zi1[3], zn1[3];
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+          zc1[ax] = zc[ax][e];
+          zi1[ax] = zin[ax][e];
+        }
+        dual_out<float, ISO, PD3O>(zc1, zi1, 0, lam, rho, omr, zn1);
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) zo3[ax][e] = zn1[ax];
+      }
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) stn_nt<float, 4>(zos + (int64_t)ax * N + off, zo3[ax]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      wc[e] = wp[e];
+      hc4[e] = hn4[e];
+    }
+  }
+}
+
+template <bool PD3O, bool ZA>
+int launch_c_lds(const PdsC<float>& pc, bool iso, int nseg, const void* w, const void* z, void* zo, hipStream_t st) {
+  const int tiles1 = (pc.g.n1 + kLdsRB - 1) / kLdsRB, tiles2 = (pc.g.n2 + kLdsC - 1) / kLdsC;
+  dim3 grid((unsigned)((int64_t)tiles1 * tiles2), (unsigned)nseg, (unsigned)pc.g.stack);
+  if (iso)
+    hipLaunchKernelGGL((pds_dual_lds_kernel<true, PD3O, ZA>), grid, dim3(kBlock), 0, st, pc, (const float*)w, (const float*)z,
+                       (float*)zo, tiles2);
+  else
+    hipLaunchKernelGGL((pds_dual_lds_kernel<false, PD3O, ZA>), grid, dim3(kBlock), 0, st, pc, (const float*)w, (const float*)z,
+                       (float*)zo, tiles2);
+  return last_launch_status();
+}
+
 template <typename T, int NV, int RB, bool PD3O>
 int launch_c_rows(const PdsC<T>& pc, bool iso, int nseg, const void* w, const void* z, void* zo, hipStream_t st) {
   const int64_t items = (int64_t)((pc.g.n1 + RB - 1) / RB) * ((pc.g.n2 + NV - 1) / NV);
@@ -319,6 +468,10 @@ int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, co
              hipStream_t st) {
   // rows per thread (PXA_TUNE_DUAL_ROWS): 1 the one-row kernel, 2 / 4 the row-blocked kernel
   const int64_t rb = tuning(PXA_TUNE_DUAL_ROWS);
+  if constexpr (sizeof(T) == 4 && NV == 4) {
+    if (rb == 8 && pc.g.D == 3) return launch_c_lds<PD3O, false>(pc, iso, nseg, w, z, zo, st);
+    if (rb == 9 && pc.g.D == 3) return launch_c_lds<PD3O, true>(pc, iso, nseg, w, z, zo, st);
+  }
   if (rb == 2) return launch_c_rows<T, NV, 2, PD3O>(pc, iso, nseg, w, z, zo, st);
   if (rb == 4) return launch_c_rows<T, NV, 4, PD3O>(pc, iso, nseg, w, z, zo, st);
   const int64_t blocks = (M + (int64_t)kBlock * NV - 1) / ((int64_t)kBlock * NV);
@@ -350,8 +503,11 @@ int run_c(const PdsGeom<T>& g, T sigma, T lam, T rho, T omr, bool pd3o, bool iso
   pc.omr = omr;
   const bool vec = (g.n2 % V == 0) && aligned16(w) && aligned16(z) && aligned16(z_out);
   const int nv = vec ? V : 1;
-  const int64_t rbk = tuning(PXA_TUNE_DUAL_ROWS) == 2 ? 2 : tuning(PXA_TUNE_DUAL_ROWS) == 4 ? 4 : 1;
-  const int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv * rbk - 1) / ((int64_t)kBlock * nv * rbk));
+  const int64_t rbt = tuning(PXA_TUNE_DUAL_ROWS);
+  const int64_t rbk = rbt == 2 ? 2 : rbt == 4 ? 4 : 1;
+  int64_t blocks = g.stack * ((M + (int64_t)kBlock * nv * rbk - 1) / ((int64_t)kBlock * nv * rbk));
+  if ((rbt == 8 || rbt == 9) && vec && g.D == 3 && sizeof(T) == 4)  // (the plane-block kernel's block count)
+    blocks = g.stack * (int64_t)((g.n1 + kLdsRB - 1) / kLdsRB) * ((g.n2 + kLdsC - 1) / kLdsC);
   const int64_t target = tuning(PXA_TUNE_DUAL_WGS) > 0 ? tuning(PXA_TUNE_DUAL_WGS) : 2048;  // A/B knob
   int cseg = (int)((target + blocks - 1) / blocks);
   if (cseg > g.n0) cseg = g.n0;

@@ -126,4 +126,17 @@ if [ "$S" = "prof" ]; then
   step trace 120 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $DRV
   pmc_pgd
 fi
+
+if [ "$S" = "k4lds" ]; then  # plane-block kernel C (PXA_TUNE 11=8) against the one-row kernel
+  step k4tests 600 $PT -m gpu tests/test_gpu_pds_fused.py -k "tv_dual"
+  for i in 1 2; do
+    step k4_one_$i 300 python3 bench.py --only k4 --k4-which 3d
+    PXA_TUNE=11=8 step k4_lds_$i 300 python3 bench.py --only k4 --k4-which 3d
+    PXA_TUNE=11=9 step k4_ldsz_$i 300 python3 bench.py --only k4 --k4-which 3d
+  done
+  K4="python3 bench.py --only k4 --k4-which 3d"
+  PXA_TUNE=11=8 step k4fetch8 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/k4fetch8 -o run --output-format csv -- $K4
+  PXA_TUNE=11=8 step k4write8 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/k4write8 -o run --output-format csv -- $K4
+  python3 scripts/pmc_traffic.py $P/k4fetch8 $P/k4write8 "pds_dual_lds_kernel" pds_dual_lds_kernel@1024x1024x1024 $P/traffic_k4.json $T || true
+fi
 echo done
