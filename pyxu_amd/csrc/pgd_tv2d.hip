@@ -140,8 +140,42 @@ template <typename T, int R>
 struct Window {
   using L = Layout<T, R>;
   static constexpr int K0 = cdiv(L::N0, kThreads);
+  // the tile's own vectors come first (thread-uniform: items k < KI of every thread), then the halo
+  static constexpr int NI = TY * (TX / L::V);
+  static constexpr int KI = NI / kThreads;
+  static_assert(NI % kThreads == 0, "every thread loads KI of the tile's own vectors");
   T xv[K0][L::V], pv[K0][L::V];
 };
+
+// Window vector `it` (0 .. N0) -> window row r, vector column g.  Items 0 .. NI - 1 are the tile's own TY x TX pixels
+// (row-major), the rest the halo: the top 2R rows, then the CA / V vectors left and right of each tile row, then the
+// bottom 2R rows.  So the RelError window partials (the tile's pixels only) are items k < KI of every thread: no
+// divergent double-precision code (the row-major order spread them over all K0 items, exec-masked).  Any bijection
+// gives the same A (each vector's yk is computed alone): the order only moves work between threads.
+template <typename T, int R>
+__device__ inline void win_rg(int it, int& r, int& g) {
+  using L = Layout<T, R>;
+  constexpr int TV = TX / L::V, CV = L::CA / L::V, NI = Window<T, R>::NI;
+  constexpr int TOP = 2 * R * L::NGA, MID = TY * 2 * CV;
+  if (it < NI) {
+    r = 2 * R + it / TV;
+    g = CV + it % TV;
+    return;
+  }
+  const int h = it - NI;
+  if (h < TOP) {
+    r = h / L::NGA;
+    g = h - r * L::NGA;
+  } else if (h < TOP + MID) {
+    const int m = h - TOP, q = m % (2 * CV);
+    r = 2 * R + m / (2 * CV);
+    g = q < CV ? q : q + TV;
+  } else {
+    const int b = h - TOP - MID, rb = b / L::NGA;
+    r = 2 * R + TY + rb;
+    g = b - rb * L::NGA;
+  }
+}
 
 template <typename T, int R, bool EDGE>
 __device__ inline void win_issue(const PgdParams<T>& p, int ty0, int tx0, const T* __restrict__ xs,
@@ -154,7 +188,8 @@ __device__ inline void win_issue(const PgdParams<T>& p, int ty0, int tx0, const 
   for (int k = 0; k < Window<T, R>::K0; ++k) {
     const int it = lt + k * kThreads;
     if (it < L::N0) {
-      const int r = it / L::NGA, g = it - r * L::NGA;
+      int r, g;
+      win_rg<T, R>(it, r, g);
       const int gr = ty0 - 2 * R + r, gc = tx0 - CA + V * g;
       if (!EDGE) {
         const unsigned off = (unsigned)(gr * n1 + gc);
@@ -188,7 +223,8 @@ __device__ inline void win_store(const PgdParams<T>& p, T* A, const Window<T, R>
   for (int k = 0; k < Window<T, R>::K0; ++k) {
     const int it = lt + k * kThreads;
     if (it < L::N0) {
-      const int r = it / L::NGA, g = it - r * L::NGA;
+      int r, g;
+      win_rg<T, R>(it, r, g);
       T out[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) out[v] = fma(w.xv[k][v] - w.pv[k][v], p.a, w.xv[k][v]);  // one rounding site
@@ -705,18 +741,12 @@ __device__ inline void win_partials(const Window<T, R>& w, double* __restrict__ 
   using L = Layout<T, R>;
   double part_d = 0.0, part_x = 0.0;
 #pragma unroll
-  for (int k = 0; k < Window<T, R>::K0; ++k) {
-    const int it = tid + k * kThreads;
-    if (it < L::N0) {
-      const int r = it / L::NGA, g = it - r * L::NGA;
-      if (r >= 2 * R && r < 2 * R + TY && L::V * g >= L::CA && L::V * g < L::CA + TX) {
+  for (int k = 0; k < Window<T, R>::KI; ++k) {  // (items k < KI: the tile's own vectors, win_rg)
 #pragma unroll
-        for (int v = 0; v < L::V; ++v) {
-          const double dd = (double)w.xv[k][v] - (double)w.pv[k][v];
-          part_d = fma(dd, dd, part_d);
-          part_x = fma((double)w.pv[k][v], (double)w.pv[k][v], part_x);
-        }
-      }
+    for (int v = 0; v < L::V; ++v) {
+      const double dd = (double)w.xv[k][v] - (double)w.pv[k][v];
+      part_d = fma(dd, dd, part_d);
+      part_x = fma((double)w.pv[k][v], (double)w.pv[k][v], part_x);
     }
   }
   wave_partials(part_d, part_x, partials, tile * kPartWaves + (tid >> 6));
@@ -824,11 +854,16 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
                                                             const T* __restrict__ xp, const T* __restrict__ b,
                                                             T* __restrict__ xn, double* __restrict__ partials) {
   using L = Layout<T, R>;
-  if (p.pub_src != nullptr && blockIdx.x == p.ntiles) {  // (no barrier shared with the tile workgroups)
+  // the publishing workgroup is block 0: dispatched in the first round, its fold is done long before the last tiles
+  // (as the last block it ran beside the second round and could outlast it); the tile workgroups' index is shifted by
+  // one, which rotates the XCD bands by one XCD and keeps each band on one XCD
+  const unsigned pub = p.pub_src != nullptr ? 1u : 0u;
+  if (pub && blockIdx.x == 0) {  // (no barrier shared with the tile workgroups)
     __shared__ double red[kThreads / 64];
     publish_prev<T>(p, red);
     return;
   }
+  const unsigned vb = blockIdx.x - pub;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   if (kProbes && p.stagger && blockIdx.x < p.round1) {
     const unsigned sel = (unsigned)p.stagger >> 8, b = blockIdx.x >> 3;  // b: index within the XCD
@@ -836,10 +871,10 @@ __global__ void __launch_bounds__(kThreads, 4) pgd_tv2d_kernel(PgdParams<T> p, c
     if (late)
       for (int i = 0; i < (p.stagger & 255); ++i) __builtin_amdgcn_s_sleep(16);
   }
-  unsigned tile = xcd_tile(blockIdx.x, p.ntiles);
+  unsigned tile = xcd_tile(vb, p.ntiles);
   {  // the last XCD band walks backwards: an image's bottom-edge tiles (slower: boundary corrections)
      // are dispatched first instead of last, longest-first scheduling (2048^2: 29.2-29.3 -> 28.9-29.0 us)
-    const unsigned nb = p.ntiles, q8 = nb >> 3, r8 = nb & 7u, g8 = blockIdx.x & 7u;
+    const unsigned nb = p.ntiles, q8 = nb >> 3, r8 = nb & 7u, g8 = vb & 7u;
     if (g8 == 7u) {
       const unsigned lo = 7u * q8 + (r8 < 7u ? r8 : 7u), len = q8 + (7u < r8 ? 1u : 0u);
       tile = lo + (len - 1u - (tile - lo));
@@ -1075,7 +1110,8 @@ __device__ inline void pipe_issue(const PgdParams<T>& p, unsigned char* raw, int
     if (c < kPipeChunks<T, R>) {
       int it = c * 64 + lane;
       if (it >= L::N0) it = L::N0 - 1;  // (the last piece's surplus lanes fill the staging padding)
-      const int r = it / L::NGA, g = it - r * L::NGA;
+      int r, g;
+      win_rg<T, R>(it, r, g);
       int gr = ty0 - 2 * R + r, gc = tx0 - L::CA + V * g;
       gr = gr < 0 ? 0 : gr >= n0 ? n0 - 1 : gr;
       gc = gc < 0 ? 0 : gc > n1 - V ? n1 - V : gc;
@@ -1103,7 +1139,8 @@ __device__ inline void pipe_window(const PgdParams<T>& p, T* A, const unsigned c
   for (int k = 0; k < Window<T, R>::K0; ++k) {
     const int it = tid + k * kThreads;
     if (it < L::N0) {
-      const int r = it / L::NGA, g = it - r * L::NGA;
+      int r, g;
+      win_rg<T, R>(it, r, g);
       const int gr = ty0 - 2 * R + r, gc = tx0 - L::CA + V * g;
       ld_vec<T, V>(rx + V * it, w.xv[k]);
       ld_vec<T, V>(rp + V * it, w.pv[k]);

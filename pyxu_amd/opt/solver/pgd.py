@@ -192,6 +192,27 @@ class PGD(pxa.Solver):
         if len(pool) > self._POOL_MAX:
             del pool[0]
 
+    def _rel_on_x(self):
+        """Whether the run's stop criterion holds a RelError on x (the statistics the fused step's partials feed):
+        without one, the check steps skip the partials (an extra read of x per launch)."""
+        crit = self._astate.get("stop_crit")
+        key = id(crit)
+        cached = self.__dict__.get("_rel_on_x_cache")
+        if cached is not None and cached[0] == key and cached[1] is crit:
+            return cached[2]
+        from pyxu_amd.abc.solver import _StoppingCriteriaComposition
+        from pyxu_amd.opt.stop import RelError
+
+        todo, found = [crit], False
+        while todo:
+            c = todo.pop()
+            if isinstance(c, _StoppingCriteriaComposition):
+                todo += [c._lhs, c._rhs]
+            elif isinstance(c, RelError) and c._var == "x":
+                found = True
+        self._rel_on_x_cache = (key, crit, found)
+        return found
+
     def m_step(self):
         mst = self._mstate
         a = next(mst["a"])
@@ -242,7 +263,7 @@ class PGD(pxa.Solver):
             sr = ast.get("stop_rate")
             if sr is not None and (ast["idx"] - 1) % sr == 0:
                 self._x_check = x  # a check ran right before this step, on this x
-            want = self._fused_relerr and sr is not None and ast["idx"] % sr == 0
+            want = self._fused_relerr and sr is not None and ast["idx"] % sr == 0 and self._rel_on_x()
             parts = p["parts"] if want else None
             xref = self._x_check if want else None
             if xref is None:

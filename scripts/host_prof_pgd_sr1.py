@@ -17,8 +17,9 @@ with pxrt.Precision(pxrt.Width.SINGLE):
     for _ in range(50): next(gen)
     torch.cuda.synchronize()
     pr = cProfile.Profile(); t0 = time.perf_counter(); pr.enable()
-    for _ in range(300): next(gen)
+    NS = int(sys.argv[2]) if len(sys.argv) > 2 else 300
+    for _ in range(NS): next(gen)
     torch.cuda.synchronize(); pr.disable(); dt = time.perf_counter() - t0
-    print("us/step", 1e6 * dt / 300)
+    print("us/step", 1e6 * dt / NS)
     pstats.Stats(pr).sort_stats("tottime").print_stats(45)
     pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
