@@ -663,15 +663,16 @@ class Solver:
                     self.m_step()
                     e.post = {k: mst.get(k) for k in ast["log_var"]}
                     drain = 0
-                    # deferred records, a few per launch (one batch of _RECORD_LAG would stall a queue that a host
-                    # synchronisation has just drained: ~0.1 ms of host work against one step of device work)
-                    if len(ast["pending"]) >= self._LAG_RECORDS:
-                        with ast["lock"]:
-                            items = ast["pending"][: self._LAG_RECORDS]
-                            del ast["pending"][: self._LAG_RECORDS]
-                            n = ast.get("unflushed", 0) + len(items)
-                            ast["unflushed"] = 0 if n >= self._RECORD_LAG else n
-                            self._record_batch(items, flush=n >= self._RECORD_LAG)
+                    # deferred records: written while the host would otherwise spin on the oldest check (the queue is
+                    # full and its statistics have not landed), else a few per launch once a backlog builds up (one
+                    # batch of _RECORD_LAG would stall a queue that a host synchronisation has just drained: ~0.1 ms of
+                    # host work against one step of device work)
+                    npr = len(ast["pending"])
+                    if npr > 0:
+                        if len(pend) > depth and pend[0].ready is not None and not pend[0].ready():
+                            self._lag_records(min(npr, 2 * self._LAG_RECORDS))
+                        elif npr >= 4 * self._LAG_RECORDS:
+                            self._lag_records(self._LAG_RECORDS)
                 free = 1  # at most one ready check per launch beyond the forced ones: the device queue stays fed (a run
                 # of ready checks resolved back to back, e.g. after a host synchronisation, would leave it idle)
                 while pend and (drain > 0 or len(pend) > depth or (free > 0 and pend[0].ready is not None and pend[0].ready())):
@@ -699,6 +700,16 @@ class Solver:
             self._on_exception(err)
         finally:
             rel._window_stats = False
+
+    def _lag_records(self, k):
+        """Write the oldest k deferred records (flushing the log every _RECORD_LAG records)."""
+        ast = self._astate
+        with ast["lock"]:
+            items = ast["pending"][:k]
+            del ast["pending"][:k]
+            n = ast.get("unflushed", 0) + len(items)
+            ast["unflushed"] = 0 if n >= self._RECORD_LAG else n
+            self._record_batch(items, flush=n >= self._RECORD_LAG)
 
     def _lag_end(self, c, rel, maxs, pend, prec):
         """Check c said stop: drop the launches after it, restore its state, write its record, end the run."""

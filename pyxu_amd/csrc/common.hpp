@@ -52,6 +52,31 @@ int resident_grid(const void* kernel, int threads, size_t lds);
 template <typename T>
 constexpr int kVecN = 16 / sizeof(T);
 
+// DPP operand of one double (two 32-bit halves through the same lane permutation)
+template <int CTRL>
+__device__ inline double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum of a double over the 64 lanes of a wave, the same value in every lane, in a fixed order: within each
+// 16-lane row by DPP (quad butterfly, then row rotations by 4 and 8), then the four row sums read from
+// lanes 0, 16, 32, 48 and added in ascending order.  No LDS round trips (a __shfl_down ladder is six
+// ds_bpermute pairs in series).
+__device__ inline double wave_sum_f64(double d) {
+  d += dpp_f64<0xB1>(d);   // quad_perm [1,0,3,2]
+  d += dpp_f64<0x4E>(d);   // quad_perm [2,3,0,1]: every lane holds its quad's sum
+  d += dpp_f64<0x124>(d);  // row_ror 4
+  d += dpp_f64<0x128>(d);  // row_ror 8: lane 16 r holds row r's sum
+  double r[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    r[q] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(d), 16 * q),
+                            __builtin_amdgcn_readlane(__double2loint(d), 16 * q));
+  return ((r[0] + r[1]) + r[2]) + r[3];
+}
+
 // One RelError statistic of the fused PGD step's per-(tile, wavefront) partials, by a whole kBlock-thread
 // workgroup: thread t sums pr[2 k] for k = t, t + kBlock, ... in order, the wavefront folds by a shuffle-down
 // tree, then thread 0 adds the kBlock / 64 wave results in order (`red`: kBlock / 64 doubles of LDS).  The

@@ -540,30 +540,7 @@ struct NormPlan {
   static constexpr size_t LDS = (size_t)NL * kNormThreads * 16 + 2 * (kNormThreads / 64) * sizeof(double);
 };
 
-// DPP operand of one double (two 32-bit halves through the same lane permutation)
-template <int CTRL>
-__device__ inline double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
-// Sum of a double over the 64 lanes of a wave, the same value in every lane, in a fixed order: within each
-// 16-lane row by DPP (quad butterfly, then row rotations by 4 and 8), then the four row sums read from
-// lanes 0, 16, 32, 48 and added in ascending order.  No LDS round trips (a __shfl_down ladder is six
-// ds_bpermute pairs in series).
-__device__ inline double wave_sum_f64(double d) {
-  d += dpp_f64<0xB1>(d);   // quad_perm [1,0,3,2]
-  d += dpp_f64<0x4E>(d);   // quad_perm [2,3,0,1]: every lane holds its quad's sum
-  d += dpp_f64<0x124>(d);  // row_ror 4
-  d += dpp_f64<0x128>(d);  // row_ror 8: lane 16 r holds row r's sum
-  double r[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    r[q] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(d), 16 * q),
-                            __builtin_amdgcn_readlane(__double2loint(d), 16 * q));
-  return ((r[0] + r[1]) + r[2]) + r[3];
-}
+// dpp_f64 / wave_sum_f64: common.hpp
 
 // Sum over the 16 doubles the waves of a workgroup left in red[0..15]: lanes 0..15 of every wave read one
 // each, a DPP reduction within lane row 0 (fixed order), the total read from lane 0 -- the same bits in

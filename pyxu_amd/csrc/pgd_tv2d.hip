@@ -749,7 +749,15 @@ __device__ inline void win_partials(const Window<T, R>& w, double* __restrict__ 
       part_x = fma((double)w.pv[k][v], (double)w.pv[k][v], part_x);
     }
   }
-  wave_partials(part_d, part_x, partials, tile * kPartWaves + (tid >> 6));
+  // (DPP wave sums: the __shfl_down ladder of wave_partials is a chain of twelve LDS round trips, on the path to the
+  // window's barrier here; the window statistics only have to agree with the epilogue ones to rounding)
+  part_d = wave_sum_f64(part_d);
+  part_x = wave_sum_f64(part_x);
+  if ((tid & 63) == 0) {
+    const unsigned slot = tile * kPartWaves + (tid >> 6);
+    __hip_atomic_store(partials + 2 * slot, part_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partials + 2 * slot + 1, part_x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // One output tile of the tile kernel: phase 0 (window) into A, then the body.
