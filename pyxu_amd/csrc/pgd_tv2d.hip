@@ -152,9 +152,17 @@ struct Window {
 // bottom 2R rows.  So the RelError window partials (the tile's pixels only) are items k < KI of every thread: no
 // divergent double-precision code (the row-major order spread them over all K0 items, exec-masked).  Any bijection
 // gives the same A (each vector's yk is computed alone): the order only moves work between threads.
+#ifndef PXA_PGD_WIN_ROWMAJOR
+#define PXA_PGD_WIN_ROWMAJOR 0  // (A/B builds: the row-major window order of rounds 1-5)
+#endif
 template <typename T, int R>
 __device__ inline void win_rg(int it, int& r, int& g) {
   using L = Layout<T, R>;
+  if (PXA_PGD_WIN_ROWMAJOR) {
+    r = it / L::NGA;
+    g = it - r * L::NGA;
+    return;
+  }
   constexpr int TV = TX / L::V, CV = L::CA / L::V, NI = Window<T, R>::NI;
   constexpr int TOP = 2 * R * L::NGA, MID = TY * 2 * CV;
   if (it < NI) {
@@ -741,12 +749,20 @@ __device__ inline void win_partials(const Window<T, R>& w, double* __restrict__ 
   using L = Layout<T, R>;
   double part_d = 0.0, part_x = 0.0;
 #pragma unroll
-  for (int k = 0; k < Window<T, R>::KI; ++k) {  // (items k < KI: the tile's own vectors, win_rg)
+  for (int k = 0; k < (PXA_PGD_WIN_ROWMAJOR ? Window<T, R>::K0 : Window<T, R>::KI); ++k) {  // (items k < KI: the tile's own vectors, win_rg)
+    int r = 2 * R, g = L::CA / L::V;
+    if (PXA_PGD_WIN_ROWMAJOR) {
+      const int it = tid + k * kThreads;
+      if (it >= L::N0) continue;
+      win_rg<T, R>(it, r, g);
+    }
+    if (r >= 2 * R && r < 2 * R + TY && L::V * g >= L::CA && L::V * g < L::CA + TX) {
 #pragma unroll
-    for (int v = 0; v < L::V; ++v) {
-      const double dd = (double)w.xv[k][v] - (double)w.pv[k][v];
-      part_d = fma(dd, dd, part_d);
-      part_x = fma((double)w.pv[k][v], (double)w.pv[k][v], part_x);
+      for (int v = 0; v < L::V; ++v) {
+        const double dd = (double)w.xv[k][v] - (double)w.pv[k][v];
+        part_d = fma(dd, dd, part_d);
+        part_x = fma((double)w.pv[k][v], (double)w.pv[k][v], part_x);
+      }
     }
   }
   // (DPP wave sums: the __shfl_down ladder of wave_partials is a chain of twelve LDS round trips, on the path to the
