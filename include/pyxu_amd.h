@@ -245,6 +245,12 @@ int pxa_cg_update(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p,
 int pxa_cg_update_tail(int dtype, int64_t rows, int64_t n, void* x, void* r, void* p, const void* ap, const double* rr,
                        double* rr_out, double* rr_host, uint32_t* flags, uint32_t seq, void* work, void* stream);
 
+/* The CG tail's first half alone (pxa_cg_update_tail without the p update): x += alpha p, r -= alpha A p, and the
+ * ||r'||^2 partials at work + rows * 64 doubles, for a following pxa_dense_normal_pdot_pfold that forms p' = r' +
+ * beta p inside its operator pass (cg.py:125-153; same bits as pxa_cg_update_tail + pxa_dense_normal_pdot). */
+int pxa_cg_update_xr(int dtype, int64_t rows, int64_t n, void* x, void* r, const void* p, const void* ap, const double* rr,
+                     void* work, void* stream);
+
 /* RelError statistics from the fused PGD step's per-tile partials (pxa_pgd_tv2d_step[_y] with
  * `partials`): out[0 * rows + r] = sum (x_new - x)^2 and out[1 * rows + r] = sum x^2 over the per_row
  * consecutive tiles of stack row r, fixed summation order.  At stop_rate 1 the criterion's stored x_prev
@@ -388,6 +394,15 @@ int pxa_dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, 
  * head of its workspace.  Same bits as pxa_dense_normal followed by pxa_cg_update. */
 int pxa_dense_normal_pdot(int dtype, int64_t M, int64_t N, const void* A, const void* X, double s, double d, void* Y,
                           void* work, double* pdot, void* stream);
+
+/* pxa_dense_normal_pdot with the CG's previous p update folded into the pass (one row, fp32, the split-row kernel):
+ * p' = r' + beta p with beta = ||r'||^2 / ||r||^2, ||r'||^2 folded from pxa_cg_update_xr's partials `part_rr`; p' is
+ * written to P_new (!= P) and used as the operand; ||r'||^2 goes to rr_out (device) and, with rr_host / flags, to
+ * coherent host memory with publication `seq`, as pxa_cg_update does.  Same bits as pxa_cg_update(_tail) followed
+ * by pxa_dense_normal_pdot on p'.  PXA_ERR_UNSUPPORTED under PXA_TUNE_NORMAL_KERNEL = 1. */
+int pxa_dense_normal_pdot_pfold(int dtype, int64_t M, int64_t N, const void* A, const void* R, const void* P, void* P_new,
+                                const double* rr, const double* part_rr, double* rr_out, double* rr_host, uint32_t* flags,
+                                uint32_t seq, double s, double d, void* Y, void* work, double* pdot, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Array primitives: the data movement of the operator algebra and the NumPy-named functions of the

@@ -606,6 +606,31 @@ def cg_update(x, r, p, ap, rr, rr_out, rr_host, work, have_pap=False):
     return seq
 
 
+def cg_update_xr(x, r, p, ap, rr, work):
+    """pxa_cg_update_xr: x += alpha p, r -= alpha A p and the ||r'||^2 partials (work + rows * 64 doubles), with the
+    <p, A p> partials already in `work` (dense_normal(..., pdot=work)); the p update is left to the next
+    dense_normal_pfold."""
+    rows, n = x.shape
+    check(lib.pxa_cg_update_xr(dtcode(x), rows, n, ptr(x), ptr(r), ptr(p), ptr(ap), rr.data_ptr(), work.data_ptr(),
+                               stream()), "pxa_cg_update_xr")
+
+
+def dense_normal_pfold(A, r, p, p_new, rr, rr_out, fb, seq, s, d, work, pdot):
+    """pxa_dense_normal_pdot_pfold: p_new = r + beta p (the CG's previous p update, beta from cg_update_xr's ||r'||^2
+    partials at pdot + 64 doubles and `rr`), then Y = s A^T (A p_new) + d p_new and the <p_new, Y> partials into
+    pdot; ||r'||^2 into rr_out (device) and HostFlagBuffer `fb` under publication `seq`.  Returns Y."""
+    M, N = A.shape
+    wsz = int(lib.pxa_dense_normal_workspace_bytes(dtcode(p), M, N, 1))
+    if wsz == 0 or work is None or work.numel() < wsz:
+        raise ValueError("pxa_dense_normal_pdot_pfold: unsupported operand or workspace")
+    Y = empty(p.shape, p)
+    check(lib.pxa_dense_normal_pdot_pfold(dtcode(p), M, N, ptr(A), ptr(r), ptr(p), ptr(p_new), rr.data_ptr(),
+                                          pdot.data_ptr() + 64 * 8, rr_out.data_ptr(), fb.vptr, fb.fptr, int(seq),
+                                          float(s), float(d), ptr(Y), ptr(work), pdot.data_ptr(), stream()),
+          "pxa_dense_normal_pdot_pfold")
+    return Y
+
+
 def tile_partials_fold(parts, rows, per_row, out):
     """RelError statistics from the fused PGD step's per-tile partials (pxa_tile_partials_fold):
     out (contiguous float64 (2, rows), device or pinned host) = per-row sum (x_new - x)^2, sum x^2."""

@@ -55,6 +55,7 @@ EXPORTS = {
     "pxa_cg_update_workspace_bytes": (sz, [i64]),
     "pxa_cg_update": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp, vp]),
     "pxa_cg_update_tail": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, vp, vp]),
+    "pxa_cg_update_xr": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp, vp]),
     "pxa_stencil_axis": (i32, [i32, i64, i32, P_i64, i32, i32, P_i32, P_f64, i32, vp, i64, vp, i64, f64, vp]),
     "pxa_stencil_sep_workspace_bytes": (sz, [i32, i64, i32, P_i64, P_int]),
     "pxa_stencil_sep": (i32, [i32, i64, i32, P_i64, P_int, P_i32, P_f64, vp, i64, vp, i64, f64, vp, vp]),
@@ -72,6 +73,8 @@ EXPORTS = {
     "pxa_dense_normal_workspace_bytes": (sz, [i32, i64, i64, i64]),
     "pxa_dense_normal": (i32, [i32, i64, i64, i64, vp, vp, f64, f64, vp, vp, vp]),
     "pxa_dense_normal_pdot": (i32, [i32, i64, i64, vp, vp, f64, f64, vp, vp, vp, vp]),
+    "pxa_dense_normal_pdot_pfold": (i32, [i32, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, ct.c_uint32, f64, f64, vp, vp,
+                                          vp, vp]),
     "pxa_copy2d": (i32, [i32, i64, i64, vp, i64, i64, vp, i64, i32, vp]),
     "pxa_unary": (i32, [i32, i32, i64, vp, vp, vp]),
     "pxa_binary": (i32, [i32, i32, i64, vp, f64, vp, f64, vp, vp]),

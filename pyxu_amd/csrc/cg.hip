@@ -187,4 +187,19 @@ int pxa_cg_update_tail(int dtype, int64_t rows, int64_t n, void* x, void* r, voi
   return cg_update(dtype, rows, n, x, r, p, ap, rr, rr_out, rr_host, flags, seq, work, true, stream);
 }
 
+int pxa_cg_update_xr(int dtype, int64_t rows, int64_t n, void* x, void* r, const void* p, const void* ap, const double* rr,
+                     void* work, void* stream) {
+  PXA_CHECK_ARG(rows >= 1 && rows <= 65535 && n >= 1);
+  PXA_CHECK_ARG(x && r && p && ap && rr && work);
+  hipStream_t st = as_stream(stream);
+  const int nb = cg_blocks(n);
+  double* part_pap = (double*)work;
+  double* part_rr = part_pap + rows * kCgBlocks;
+  PXA_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL((cg_xr_kernel<T>), dim3((unsigned)nb, (unsigned)rows), dim3(kBlock), 0, st, n, rr, part_pap,
+                       (const T*)p, (const T*)ap, (T*)x, (T*)r, part_rr);
+    return last_launch_status();
+  });
+}
+
 }  // extern "C"

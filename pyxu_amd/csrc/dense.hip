@@ -680,6 +680,24 @@ constexpr int kBufs = 4;
 constexpr int kGroupWaitTicks = 5000;  // 50 us of the 100 MHz clock
 constexpr int kGroupScratch = 2048;    // LDS bytes below the x part
 
+// The CG's p = r' + beta p of the previous step folded into this operator pass (pxa_dense_normal_pdot_pfold): each
+// workgroup forms its part of the direction from r' and p (cg_p_kernel's expressions: beta = (float)(||r'||^2 /
+// ||r||^2) with ||r'||^2 folded from pxa_cg_update_xr's partials in cg.hip's order, p' = fma(beta, p, r')) instead of
+// loading it, group 0's members store p', and workgroup 0 publishes ||r'||^2 as cg_p_kernel does.  Same bits as
+// pxa_cg_update followed by pxa_dense_normal_pdot on p'; one launch and one pass over r / p fewer per CG step.
+struct PFold {
+  const float* r;         // r' (nullptr: no fold, the pass reads x)
+  const float* p;         // p of the previous step
+  float* pn;              // p' (= the pass's x for the reductions after it)
+  const double* rr;       // ||r||^2 of the previous step (device)
+  const double* part_rr;  // the ||r'||^2 partials (cg_blocks(n) doubles)
+  int nb;
+  double* rr_out;         // ||r'||^2 (device): the next step's ||r||^2
+  double* rr_host;        // ... into coherent host memory (or nullptr)
+  unsigned* flags;        // ... and its completion flag (or nullptr)
+  unsigned seq;
+};
+
 template <int NVS>
 struct GroupPlan {
   static constexpr size_t LDS = (size_t)NVS * kNormThreads * 16 + kGroupScratch;
@@ -754,7 +772,8 @@ __global__ void __launch_bounds__(kNormThreads) normal_group_kernel(int64_t M, i
                                                                     float* __restrict__ part,
                                                                     unsigned long long* __restrict__ slots,
                                                                     int rows_per_group, unsigned tag, int solo,
-                                                                    unsigned long long* __restrict__ stats, int flav) {
+                                                                    unsigned long long* __restrict__ stats, int flav,
+                                                                    PFold pf) {
   extern __shared__ __align__(16) unsigned char nsm[];
   // LDS: scratch at the bottom (one base register + immediates): red[b][0, 16) the part-dot sums of buffer
   // b's row, red[3 + b][0, 16) those of a part-dot computed here in another member's place, exch[b][part]
@@ -777,7 +796,38 @@ __global__ void __launch_bounds__(kNormThreads) normal_group_kernel(int64_t M, i
   auto rsrc = [&](const float4* base, int w) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, w * 16, 0x00020000);
   };
-  {
+  const bool fold = pf.r != nullptr;
+  float beta = 0.f;
+  if (fold) {
+    double rn = 0.0;  // cg.hip fold(): 0 + part[0] + part[1] + ... in order
+    for (int j = 0; j < pf.nb; ++j) rn += pf.part_rr[j];
+    beta = (float)(rn / pf.rr[0]);
+    if (blockIdx.x == 0 && tid == 0) {  // cg_p_kernel's publication of ||r'||^2
+      pf.rr_out[0] = rn;
+      if (pf.rr_host) pf.rr_host[0] = rn;
+      if (pf.flags) {
+        __threadfence_system();
+        __hip_atomic_store(pf.flags, pf.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  const float4* r4 = reinterpret_cast<const float4*>(pf.r);
+  const float4* p4 = reinterpret_cast<const float4*>(pf.p);
+  // p' of part h, vector k: fma(beta, p, r') per element (cg_p_kernel's expression)
+  auto pfold = [&](int h, int wh, int k) {
+    const __amdgpu_buffer_rsrc_t rr_ = rsrc(r4 + h * q.P4, wh), pr_ = rsrc(p4 + h * q.P4, wh);
+    const float4 rv = buf_ld16<0>(rr_, voff, k * kNormThreads * 16), pv = buf_ld16<0>(pr_, voff, k * kNormThreads * 16);
+    return make_float4(fmaf(beta, pv.x, rv.x), fmaf(beta, pv.y, rv.y), fmaf(beta, pv.z, rv.z), fmaf(beta, pv.w, rv.w));
+  };
+  if (fold) {
+    float4* pn4 = reinterpret_cast<float4*>(pf.pn) + c0;
+#pragma unroll
+    for (int k = 0; k < NVS; ++k) {
+      const float4 v = live(k, W4) ? pfold(q.part, W4, k) : z4;
+      xs[k * kNormThreads + tid] = v;
+      if (q.group == 0 && live(k, W4)) pn4[tid + k * kNormThreads] = v;
+    }
+  } else {
     const __amdgpu_buffer_rsrc_t xr = rsrc(x4 + c0, W4);
 #pragma unroll
     for (int k = 0; k < NVS; ++k)
@@ -954,7 +1004,7 @@ __global__ void __launch_bounds__(kNormThreads) normal_group_kernel(int64_t M, i
 #pragma unroll
         for (int k = 0; k < NVS; ++k)
           e += (double)dot4(live(k, wh) ? buf_ld16<2>(ra, voff, k * kNormThreads * 16) : z4,
-                            live(k, wh) ? buf_ld16<0>(rx, voff, k * kNormThreads * 16) : z4);
+                            live(k, wh) ? (fold ? pfold(h, wh, k) : buf_ld16<0>(rx, voff, k * kNormThreads * 16)) : z4);
         const double dh = group_block_sum(e, red + (3 + (h & 1)) * 16);  // consecutive sums alternate scratch
         tot = h == 0 ? dh : tot + dh;
       }
@@ -1177,7 +1227,7 @@ int launch_normal(int64_t M, int64_t N, const float* A, const float* x, float s,
 
 template <int NVS>
 int launch_normal_group(int64_t M, int64_t N, const float* A, const float* x, float s, float d, float* Y, float* work,
-                        bool solo, double* pdot, hipStream_t st) {
+                        bool solo, double* pdot, hipStream_t st, const PFold& pf = PFold{}) {
   const size_t lds = GroupPlan<NVS>::LDS;
   static bool attr = false;
   if (!attr) {
@@ -1206,10 +1256,10 @@ int launch_normal_group(int64_t M, int64_t N, const float* A, const float* x, fl
   const int flav = kGroupProbes ? tuning(PXA_TUNE_NORMAL_KERNEL) : 0;
   if (P4 * kParts == N4 && P4 == NVS * kNormThreads)
     hipLaunchKernelGGL((normal_group_kernel<NVS, true>), dim3(kParts * C), dim3(kNormThreads), lds, st, M, N4, A, x,
-                       work, slots, rpg, tag, (int)solo, stats, flav);
+                       work, slots, rpg, tag, (int)solo, stats, flav, pf);
   else
     hipLaunchKernelGGL((normal_group_kernel<NVS, false>), dim3(kParts * C), dim3(kNormThreads), lds, st, M, N4, A, x,
-                       work, slots, rpg, tag, (int)solo, stats, flav);
+                       work, slots, rpg, tag, (int)solo, stats, flav, pf);
   const int e = last_launch_status();
   return e ? e : normal_reduce(C, N, x, s, d, Y, work, pdot, st);
 }
@@ -1283,7 +1333,7 @@ size_t pxa_dense_normal_workspace_bytes(int dtype, int64_t M, int64_t N, int64_t
 }
 
 static int dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* A, const void* X, double s, double d, void* Y,
-                 void* work, double* pdot, void* stream) {
+                 void* work, double* pdot, void* stream, const PFold& pf = PFold{}) {
   PXA_CHECK_ARG(M >= 1 && N >= 1 && B >= 0);
   if (B == 0) return PXA_OK;
   PXA_CHECK_ARG(A != nullptr && X != nullptr && Y != nullptr && Y != X);
@@ -1300,10 +1350,11 @@ static int dense_normal(int dtype, int64_t M, int64_t N, int64_t B, const void* 
   if (kern != 1) {  // split rows (2: without the exchange, every part-dot computed by every member; same bits)
     const int64_t nvs = ((N / 4 + kParts - 1) / kParts + kNormThreads - 1) / kNormThreads;  // vectors per part
     const bool solo = kern == 2;
-    if (nvs <= 1) return launch_normal_group<1>(M, N, a, x, fs, fd, y, w, solo, pdot, st);
-    if (nvs <= 2) return launch_normal_group<2>(M, N, a, x, fs, fd, y, w, solo, pdot, st);
-    return launch_normal_group<4>(M, N, a, x, fs, fd, y, w, solo, pdot, st);
+    if (nvs <= 1) return launch_normal_group<1>(M, N, a, x, fs, fd, y, w, solo, pdot, st, pf);
+    if (nvs <= 2) return launch_normal_group<2>(M, N, a, x, fs, fd, y, w, solo, pdot, st, pf);
+    return launch_normal_group<4>(M, N, a, x, fs, fd, y, w, solo, pdot, st, pf);
   }
+  if (pf.r != nullptr) return PXA_ERR_UNSUPPORTED;  // (the one-workgroup-per-row A/B kernel has no fold)
   const int64_t nv = (N / 4 + kNormThreads - 1) / kNormThreads;  // vectors per thread
   if (nv <= 1) return launch_normal<1>(M, N, a, x, fs, fd, y, w, pdot, st);
   if (nv <= 2) return launch_normal<2>(M, N, a, x, fs, fd, y, w, pdot, st);
@@ -1322,6 +1373,28 @@ int pxa_dense_normal_pdot(int dtype, int64_t M, int64_t N, const void* A, const 
                           void* work, double* pdot, void* stream) {
   PXA_CHECK_ARG(pdot != nullptr);
   return dense_normal(dtype, M, N, 1, A, X, s, d, Y, work, pdot, stream);
+}
+
+int pxa_dense_normal_pdot_pfold(int dtype, int64_t M, int64_t N, const void* A, const void* R, const void* P, void* P_new,
+                                const double* rr, const double* part_rr, double* rr_out, double* rr_host, uint32_t* flags,
+                                uint32_t seq, double s, double d, void* Y, void* work, double* pdot, void* stream) {
+  PXA_CHECK_ARG(pdot != nullptr && R != nullptr && P != nullptr && P_new != nullptr && rr != nullptr && part_rr != nullptr &&
+                rr_out != nullptr);
+  PXA_CHECK_ARG(P_new != P && P_new != R && P_new != Y && aligned16(R) && aligned16(P) && aligned16(P_new));
+  PXA_CHECK_ARG(dtype == PXA_F32 && rr_out != rr);
+  PFold pf;
+  pf.r = (const float*)R;
+  pf.p = (const float*)P;
+  pf.pn = (float*)P_new;
+  pf.rr = rr;
+  pf.part_rr = part_rr;
+  pf.nb = cg_blocks(N);
+  pf.rr_out = rr_out;
+  pf.rr_host = rr_host;
+  pf.flags = (unsigned*)flags;
+  pf.seq = (unsigned)seq;
+  // X = p': the reductions after the pass read it (d p', <p', A p'>); the pass itself forms its parts from r' and p
+  return dense_normal(dtype, M, N, 1, A, P_new, s, d, Y, work, pdot, stream, pf);
 }
 
 }  // extern "C"

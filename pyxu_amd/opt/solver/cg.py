@@ -1,4 +1,6 @@
 """Conjugate Gradient (mirrors reference opt/solver/cg.py:14-187)."""
+import os
+
 import numpy as np
 
 import pyxu_amd.abc as pxa
@@ -16,6 +18,9 @@ _ROWSTAT = "__rowstat__"
 # A p and the CG's <p, A p> partials from one set of launches when the operator can produce them
 # (pxa_dense_normal_pdot -> pxa_cg_update_tail; same bits either way).  Tests switch it off for the A/B.
 _FUSED_DOT = True
+# ... and the p update of a CG step formed inside the next step's operator pass (pxa_dense_normal_pdot_pfold), when
+# that pass is launched ahead of the stop check: one launch and one pass over r / p fewer per step, same bits
+_FOLD_P = os.environ.get("PXA_CG_FOLD_P", "1") == "1"  # (PXA_CG_FOLD_P=0: the separate p launch, for A/B)
 
 
 def _rows2d(x):
@@ -188,8 +193,14 @@ class CG(pxa.Solver):
                 return None
             return _dev.dense_normal(mat, v, s, d, work=workspace(v), pdot=pdot)
 
+        def apply_pfold(r, p, p_new, rr, rr_out, fb, seq, pdot):
+            return _dev.dense_normal_pfold(mat, r, p, p_new, rr, rr_out, fb, seq, s, d, workspace(p), pdot)
+
         apply.fused = True
         apply.pdot = apply_pdot
+        apply.mat = mat
+        if not sharded:
+            apply.pfold = apply_pfold
         return apply
 
     def _apply_p(self, p):
@@ -249,6 +260,23 @@ class CG(pxa.Solver):
         rr_host = rr.host()  # already waited for by the stop check of this iteration (same value)
         fast = (not np.any(rr_host <= eps) and self._astate["idx"] % mst["restart_rate"] != 0
                 and 0 < _rows2d(x).shape[0] <= 65535)
+        internal = self._astate.get("internal")
+        if (fast and internal and have_pap and _FOLD_P and _FUSED_DOT and p.dim() == 1
+                and getattr(self._apply, "pfold", None) is not None and _dev.dense_normal_supported(self._apply.mat, p)
+                and _dev.tuning(_dev.TUNE_NORMAL_KERNEL) & 15 != 1 and not self._predict_stop(rr_host)):
+            # x, r and the ||r'||^2 partials now (pxa_cg_update_xr); p' = r' + beta p, ||r'||^2's publication and
+            # A p' with its <p', A p'> partials in the next operator pass, launched ahead of the stop check
+            hr = self._rows_buffers(1)
+            _dev.cg_update_xr(_rows2d(x), _rows2d(r), _rows2d(p), _rows2d(Ap), rr.dev, self._cg_work)
+            pn = _dev.empty_like(p)
+            seq = hr[1].next_seq()
+            self._Ap_next = self._apply.pfold(r, p, pn, rr.dev, hr[0], hr[1], seq, self._cg_workspace(1))
+            self._pap_ready = self._Ap_next
+            hr = _KernelRows(hr[0], hr[1], seq)
+            self._rr = (hr, r)
+            mst[_ROWSTAT] = {"residual": (r, 2, hr)}
+            mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, pn
+            return
         if fast:
             # the whole tail in three launches (pxa_cg_update): alpha, x, r, ||r'||^2, beta, p; ||r'||^2 is
             # written straight into pinned host memory for the next stop check
@@ -257,9 +285,9 @@ class CG(pxa.Solver):
                                  have_pap=have_pap)
             hr = _KernelRows(hr[0], hr[1], seq)
             self._rr = (hr, r)
-            if self._astate.get("internal"):
+            if internal:
                 mst[_ROWSTAT] = {"residual": (r, 2, hr)}
-                if not self._predict_stop(rr_host):
+                if not self._predicted_stop(rr_host):
                     self._Ap_next = self._apply_p(p)
             mst["x"], mst["residual"], mst["conjugate_dir"] = x, r, p
             return
@@ -314,16 +342,26 @@ class CG(pxa.Solver):
                 found = float(c._eps)
         return found
 
+    def _predicted_stop(self, rr_host):
+        """_predict_stop of this step, evaluated at most once per step (the fold test above may have asked it)."""
+        got = self.__dict__.get("_pred_cache")
+        if got is not None and got[0] is rr_host:
+            return got[1]
+        return self._predict_stop(rr_host)
+
     def _predict_stop(self, rr_host):
         """Whether the NEXT stop check will probably end the solve, from the geometric rate of the last two
         ||r||^2: then A p' is not launched ahead (it would be dropped).  A wrong guess either way only
         moves where A p' is computed; the iterates are the same."""
         self._rr_hist = (self._rr_hist + [float(np.max(rr_host))])[-2:]
         if self._abs_eps is None or len(self._rr_hist) < 2 or self._rr_hist[0] <= 0:
-            return False
-        r0, r1 = self._rr_hist
-        pred = r1 * (r1 / r0)  # ||r_next||^2 at the current contraction rate
-        return pred <= self._abs_eps**2
+            out = False
+        else:
+            r0, r1 = self._rr_hist
+            pred = r1 * (r1 / r0)  # ||r_next||^2 at the current contraction rate
+            out = pred <= self._abs_eps**2
+        self._pred_cache = (rr_host, out)
+        return out
 
     def default_stop_crit(self):
         from pyxu_amd.opt.stop import AbsError

@@ -212,3 +212,44 @@ def test_fused_cg_dot_same_bits(M, N, mode):
         _dev.tuning(_dev.TUNE_NORMAL_KERNEL, old)
     assert res[True][0] == res[False][0] and res[True][0] >= 5
     assert np.array_equal(res[True][1].view(np.uint32), res[False][1].view(np.uint32))
+
+
+@pytest.mark.parametrize("M,N,mode", [(1024, 8192, 0), (256, 65536, 0), (64, 40000, 0), (512, 8192, 2)])
+def test_cg_p_fold_same_bits(M, N, mode):
+    """The CG's p' = r' + beta p formed inside the next operator pass (pxa_cg_update_xr, then
+    pxa_dense_normal_pdot_pfold, which also publishes ||r'||^2) against pxa_cg_update's own p launch: the same
+    solution, residual, direction and iteration count, bit for bit; the fold path is taken (mode 2: every member
+    forms the other parts' operand itself, from r' and p)."""
+    import pyxu_amd.opt.solver.cg as cgm
+
+    rng = np.random.default_rng(M + 3 * N)
+    A = (rng.standard_normal((M, N)) / np.sqrt(M)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    res, calls = {}, [0]
+    orig = _dev.dense_normal_pfold
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return orig(*a, **k)
+
+    old = _dev.tuning(_dev.TUNE_NORMAL_KERNEL, mode)
+    _dev.dense_normal_pfold = counted
+    try:
+        for fold in (True, False):
+            cgm._FOLD_P = fold
+            with pxrt.Precision(pxrt.Width.SINGLE):
+                K = pxa.LinOp.from_array(to_device(A))
+                q = pxa.QuadraticFunc(shape=(1, N), Q=K.T * K)
+                x = q.prox(to_device(b), 0.5)
+                slvr = q._prox_cg(np.float32(0.5))[0]
+                m = slvr._mstate
+                res[fold] = (slvr._astate["idx"], to_NUMPY(x), to_NUMPY(m["residual"]), to_NUMPY(m["conjugate_dir"]))
+            if fold:
+                assert calls[0] >= 3, calls
+    finally:
+        cgm._FOLD_P = True
+        _dev.dense_normal_pfold = orig
+        _dev.tuning(_dev.TUNE_NORMAL_KERNEL, old)
+    assert res[True][0] == res[False][0] and res[True][0] >= 5
+    for a_, b_ in zip(res[True][1:], res[False][1:]):
+        assert np.array_equal(a_.view(np.uint32), b_.view(np.uint32))
