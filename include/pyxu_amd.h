@@ -84,7 +84,9 @@ extern "C" {
                                 (default one); bit 1 a persistent grid of the resident capacity (default one
                                 workgroup per unit); bit 2 a soft progress coupling of row-neighbour workgroups
                                 (fp32, radius 6: each waits, boundedly, while a started neighbour lags more than
-                                2 + (value >> 3) planes); same bits */
+                                2 + (value >> 3) planes); bit 8 the march without its plane prefetch (the default
+                                issues every load of plane q + 1 before plane q is computed), bit 9 two planes
+                                ahead; same bits */
 #define PXA_TUNE_FFT_KERNEL 8 /* A/B of the in-LDS FFT (pxa_fft, lines that fit one workgroup): 0 in-place register-staged
                                  stages on padded lines with a twiddle table, 1 the ping-pong Stockham kernel of rounds
                                  1-3 (results equal up to rounding); bits 256 / 512 force 512- / 1024-thread

@@ -59,7 +59,18 @@ __device__ __forceinline__ void couple_step(unsigned* prog, unsigned tag, unsign
 
 // One work unit of kernel D: in-plane block `blk` (kAThreads * NP consecutive positions) of axis-0 segment `segi`
 // of volume `s`, marched over the segment's planes (+ the G0 halo planes).
-template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT, bool CP = false>
+// PF (PXA_TUNE_PDS_MARCH bit 8, DUAL only): every load of plane qp + 1 is issued before plane qp is computed (a
+// second register set of the plane's loads, PlaneLoads), so that each wave has two planes of loads in flight; the
+// arithmetic is the same expressions on the same values: the same bits.
+template <typename T, int NP>
+struct PlaneLoads {
+  T wf[NP], w1[NP], w2n, zc[3][NP];      // own_z: w at plane + 1, row + 1, the column after the block; z
+  T rw[NP], rz[3][NP], rw0[NP], rw2[NP];  // row - 1 neighbours: w, z, w at plane + 1, w at column + 1
+  T lw, lz[3], lw0, lw1;                  // column - 1 neighbour: w, z, w at plane + 1, w at row + 1
+  T u[NP];                                // u (PD3O) or x (Condat-Vu)
+};
+
+template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT, bool CP = false, int PF = 0>
 __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict__ w, const T* __restrict__ z,
                                            const T* __restrict__ src, T* __restrict__ zo, T* __restrict__ ao,
                                            T* __restrict__ q, unsigned blk, int segi, int64_t s) {
@@ -278,6 +289,170 @@ __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict
     return r;
   };
 
+  // PF: the loads of plane qp (the conditions of own_z / one_z / load_v), then the plane from them
+  auto issue = [&](int qp, PlaneLoads<T, NP>& L) __attribute__((always_inline)) {
+    const int64_t off = (int64_t)qp * M;
+    if (qp + 1 < n0) {
+      ldn<T, NP>(ws + off + M, L.wf);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) L.wf[k] = T(0);
+    }
+    if (row_nb) {
+      ldn<T, NP>(ws + off + n2, L.w1);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) L.w1[k] = T(0);
+    }
+    L.w2n = col_nb ? ws[off + NP] : T(0);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if (a < a_first) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) L.zc[a][k] = T(0);
+      } else {
+        ldn<T, NP>(zs + (int64_t)(a - a_first) * N + off, L.zc[a]);
+      }
+    }
+    if (a_first <= 1 && row > 0) {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int64_t o = off - n2 + k;
+        L.rw[k] = ws[o];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) L.rz[a][k] = a < a_first ? T(0) : zs[(int64_t)(a - a_first) * N + o];
+        L.rw0[k] = qp + 1 < n0 ? ws[o + M] : T(0);
+        L.rw2[k] = col + k + 1 < n2 ? ws[o + 1] : T(0);
+      }
+    }
+    if (col > 0) {
+      const int64_t o = off - 1;
+      L.lw = ws[o];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) L.lz[a] = a < a_first ? T(0) : zs[(int64_t)(a - a_first) * N + o];
+      L.lw0 = qp + 1 < n0 ? ws[o + M] : T(0);
+      L.lw1 = row + 1 < n1 ? ws[o + n2] : T(0);
+    }
+    if (NT)
+      ldn_nt<T, NP>(in + off, L.u);
+    else
+      ldn<T, NP>(in + off, L.u);
+  };
+  auto compute_v = [&](int qp, const PlaneLoads<T, NP>& L) __attribute__((always_inline)) -> VN {
+    const int64_t off = (int64_t)qp * M;
+    const bool mine = qp >= pb && qp < pe;
+    T zn[3][NP], zr1[NP], zl2;
+    T wc0[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) wc0[k] = wcar[k];
+    {  // own_z
+      T w2[NP];
+#pragma unroll
+      for (int k = 0; k + 1 < NP; ++k) w2[k] = wc0[k + 1];
+      w2[NP - 1] = L.w2n;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        T c3[3], i3[3], n3[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          const T wn = a == 0 ? L.wf[k] : (a == 1 ? L.w1[k] : w2[k]);
+          c3[a] = L.zc[a][k];
+          i3[a] = a < a_first ? T(0) : dual_in<T>(L.zc[a][k], wc0[k], wn, g.c0[a], g.c1[a], sigma);
+        }
+        dual_out<T, ISO, PD3O>(c3, i3, a_first, lam, rho, omr, n3);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) zn[a][k] = n3[a];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) wcar[k] = L.wf[k];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {  // one_z at row - 1 (back = 1: its row + 1 neighbour is the own w)
+      zr1[k] = T(0);
+      if (a_first <= 1 && row > 0) {
+        T c3[3], i3[3], n3[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          if (a < a_first) {
+            c3[a] = i3[a] = T(0);
+            continue;
+          }
+          c3[a] = L.rz[a][k];
+          const T wn = a == 1 ? wc0[k] : (a == 0 ? L.rw0[k] : L.rw2[k]);
+          i3[a] = dual_in<T>(c3[a], L.rw[k], wn, g.c0[a], g.c1[a], sigma);
+        }
+        dual_out<T, ISO, PD3O>(c3, i3, a_first, lam, rho, omr, n3);
+        zr1[k] = n3[1];
+      }
+    }
+    zl2 = T(0);
+    if (col > 0) {  // one_z at column - 1 (back = 2)
+      T c3[3], i3[3], n3[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        if (a < a_first) {
+          c3[a] = i3[a] = T(0);
+          continue;
+        }
+        c3[a] = L.lz[a];
+        const T wn = a == 2 ? wc0[0] : (a == 0 ? L.lw0 : L.lw1);
+        i3[a] = dual_in<T>(c3[a], L.lw, wn, g.c0[a], g.c1[a], sigma);
+      }
+      dual_out<T, ISO, PD3O>(c3, i3, a_first, lam, rho, omr, n3);
+      zl2 = n3[2];
+    }
+    if (mine) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        if (a < a_first) continue;
+        if (NT)
+          stn_nt<T, NP>(zw + (int64_t)(a - a_first) * N + off, zn[a]);
+        else
+          stn<T, NP>(zw + (int64_t)(a - a_first) * N + off, zn[a]);
+      }
+    }
+    T kt[NP];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if (a < a_first) continue;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const T zm = a == 0 ? zp0[k] : (a == 1 ? zr1[k] : (k == 0 ? zl2 : zn[2][k - 1]));
+        const T term = kt_term<T>(g.c1[a], zm, g.c0[a], zn[a][k]);
+        kt[k] = (a == a_first) ? term : kt[k] + term;
+      }
+      if (a == 0) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) zp0[k] = zn[0][k];
+      }
+    }
+    VN r;
+    T(&v)[NP] = r.v;
+    if constexpr (PD3O) {
+      const T one = T(1), mtau = -tau;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) v[k] = apply_prox<T>(prox, fma(mtau, kt[k], one * L.u[k]), pw);
+      if (mine) {
+        if (NT)
+          stn_nt<T, NP>(aw + off, v);
+        else
+          stn<T, NP>(aw + off, v);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) v[k] = L.u[k];
+      if (mine) {
+        if (NT)
+          stn_nt<T, NP>(aw + off, kt);
+        else
+          stn<T, NP>(aw + off, kt);
+      }
+    }
+    return r;
+  };
+  (void)issue;
+  (void)compute_v;
+
   if constexpr (R0 == 0) {
     for (int qp = pb; qp < pe; ++qp) (void)load_v(qp);
   } else {
@@ -292,6 +467,12 @@ __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict
     // rh[t] = (H0 v) at plane qp - 3 R0 + t.  (Static ring slots as in pds_axis0_kernel, i.e. the plane
     // body unrolled RING times, measured no faster: profiles/r03z_pds_march_ring_ab.txt.)
     const bool couple = CP && p.prog != nullptr;  // (CP: a separate instance, so the default keeps its SGPRs)
+    PlaneLoads<T, NP> cur, nxt, nx2;
+    if constexpr (PF > 0 && DUAL) {
+      const int q0 = first < 0 ? 0 : first;
+      if (q0 < n0 && q0 <= last) issue(q0, cur);
+      if (PF > 1 && q0 + 1 < n0 && q0 + 1 <= last) issue(q0 + 1, nxt);
+    }
     const int64_t cbase = (s * p.nseg + segi) * (int64_t)p.blocks;
     const int64_t cup = couple && blk >= (unsigned)p.bpr ? cbase + blk - p.bpr : -1;
     const int64_t cdn = couple && (int64_t)blk + p.bpr < p.blocks ? cbase + blk + p.bpr : -1;
@@ -303,7 +484,19 @@ __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict
 #pragma unroll
         for (int k = 0; k < NP; ++k) rv[t][k] = rv[t + 1][k];
       if (qp >= 0 && qp < n0) {
-        const VN r = load_v(qp);
+        VN r;
+        if constexpr (PF == 1 && DUAL) {
+          if (qp + 1 < n0 && qp + 1 <= last) issue(qp + 1, nxt);  // in flight while this plane is computed
+          r = compute_v(qp, cur);
+          cur = nxt;
+        } else if constexpr (PF == 2 && DUAL) {
+          if (qp + 2 < n0 && qp + 2 <= last) issue(qp + 2, nx2);  // two planes ahead
+          r = compute_v(qp, cur);
+          cur = nxt;
+          nxt = nx2;
+        } else {
+          r = load_v(qp);
+        }
 #pragma unroll
         for (int k = 0; k < NP; ++k) rv[RING - 1][k] = r.v[k];
       } else {
@@ -354,7 +547,7 @@ __device__ __forceinline__ void march_unit(const PdsD<T>& p, const T* __restrict
 // r05c): HBM fetch 25.7 -> 23.8 GiB per launch (1.29 -> 1.19 x compulsory), but kernel D 8.8 -> 11.0 ms (PD3O)
 // and 10.2 -> 12.0 ms (Condat-Vu): the marches running in lockstep cost more than the re-fetched rows, so the
 // default stays one workgroup per unit, dispatched as slots free up.
-template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT, bool CP = false>
+template <typename T, int R0, int NP, bool PD3O, bool ISO, bool DUAL, bool NT, bool CP = false, int PF = 0>
 __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T* __restrict__ w,
                                                               const T* __restrict__ z, const T* __restrict__ src,
                                                               T* __restrict__ zo, T* __restrict__ ao,
@@ -362,7 +555,7 @@ __global__ void __launch_bounds__(kAThreads) pds_march_kernel(PdsD<T> p, const T
                                                               unsigned units) {
   for (unsigned u = blockIdx.x; u < units; u += gridDim.x) {
     const unsigned r = u % blocks, rest = u / blocks;
-    march_unit<T, R0, NP, PD3O, ISO, DUAL, NT, CP>(p, w, z, src, zo, ao, q, xcd_tile(r, blocks), (int)(rest % nseg),
+    march_unit<T, R0, NP, PD3O, ISO, DUAL, NT, CP, PF>(p, w, z, src, zo, ao, q, xcd_tile(r, blocks), (int)(rest % nseg),
                                                (int64_t)(rest / nseg));
   }
 }
@@ -384,7 +577,16 @@ int launch_d(const PdsD<T>& pd, int np, int64_t M, int nseg, const void* w, cons
   const int64_t blocks = (M + (int64_t)kAThreads * np - 1) / ((int64_t)kAThreads * np);
   const int64_t units = blocks * nseg * pd.a.g.stack;
   PXA_CHECK_ARG(units <= 0x7fffffff);
+  // one position per thread: the plane-prefetching march (every load of plane q + 1 issued before plane q is computed;
+  // C3 1024^3, r06ao: kernel D 8.78-8.84 -> 8.22-8.23 ms PD3O, 9.74-9.86 -> 8.24-8.25 ms Condat-Vu; same bits).
+  // PXA_TUNE_PDS_MARCH bit 8: the march without it, bit 9: two planes ahead (A/B)
   auto kern = np == 2 ? pds_march_kernel<T, R0, 2, PD3O, ISO, DUAL, true> : pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true>;
+  if constexpr (DUAL) {
+    const int64_t tv = tuning(PXA_TUNE_PDS_MARCH);
+    if (np == 1 && !(tv & 256))
+      kern = (tv & 512) ? pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true, false, 2>
+                        : pds_march_kernel<T, R0, 1, PD3O, ISO, DUAL, true, false, 1>;
+  }
   // grid: one workgroup per unit (PXA_TUNE_PDS_MARCH bit 1: the resident capacity, persistent; see above)
   unsigned grid = (unsigned)units;
   PdsD<T> pdc = pd;

@@ -349,3 +349,25 @@ def test_pds_lookahead_coupled_march_bit_exact(algo, slack):
             _dev.tuning(_dev.TUNE_PDS_MARCH, prev)
         for k in a:
             assert np.array_equal(a[k], b[k]), (shape, k)
+
+
+@pytest.mark.parametrize("algo", ["pd3o", "cv"])
+@pytest.mark.parametrize("case", LA_CASES + [((40, 256, 512), 2.0, "iso", "pos", np.float32, False)],
+                         ids=lambda c: "x".join(map(str, c[0])) + f"-{c[2]}-{np.dtype(c[4]).name}" if isinstance(c, tuple) else str(c))
+def test_pds_lookahead_prefetch_march_bit_exact(algo, case):
+    """Kernel D with every load of plane q + 1 issued before plane q is computed (the default: two planes of loads in
+    flight per wave; PXA_TUNE_PDS_MARCH bit 9: three) gives the bits of the march without prefetch (bit 8): 2-D / 3-D,
+    iso / aniso, fp32 / fp64, batch-as-axis."""
+    N = int(np.prod(case[0]))
+    x0 = np.random.default_rng(9).uniform(0, 1, N).astype(case[4])
+    a = _run(algo, case, 5, True, x0)
+    res = {}
+    for v in (256, 512):
+        prev = _dev.tuning(_dev.TUNE_PDS_MARCH, v)
+        try:
+            res[v] = _run(algo, case, 5, True, x0)
+        finally:
+            _dev.tuning(_dev.TUNE_PDS_MARCH, prev)
+    for v, b in res.items():
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (v, k)
