@@ -101,7 +101,8 @@ extern "C" {
                                    the vector / LDS-tiled ones, bit 2 turns off the LDS-tiled off-last-axis pass
                                    (same sums either way) */
 #define PXA_TUNE_DUAL_ROWS 11 /* A/B of the PDS dual-update kernel C (pxa_tv_dual_update, the three-launch step): rows of w
-                                * per thread, 0 / 1 the one-row kernel, 2 or 4 the row-blocked kernel (a thread's row + 1
+                                * per thread, 0 the one-row kernel (the next plane's loads issued one plane early), 1 the
+                                * one-row kernel without that prefetch, 2 or 4 the row-blocked kernel (a thread's row + 1
                                 * neighbours are its own rows), 8 the plane-block kernel (3-D fp32 16-B vectors: an 8 x 128
                                 * block of each plane staged in LDS with its halo row / column; 9: the same with z loaded one plane ahead).  Same
                                 * bits. */

@@ -87,7 +87,10 @@ __device__ inline void ldv(const T* p, T (&v)[NV]) {
 // axis-0 forward neighbour w(p + 1) is loaded once and carried to the next step.  The in-plane block
 // index is XCD-banded (tile2d::xcd_tile) so that the row+1 neighbour is usually read from the L2 of the
 // same XCD, where the neighbouring block marches in step.
-template <typename T, int NV, bool ISO, bool PD3O, bool NT>
+// PF (the default; PXA_TUNE_DUAL_ROWS = 1 turns it off): z and the row + 1 / column + 1 neighbours of plane p + 1 are
+// loaded while plane p is computed (two planes of loads in flight per thread); the same values in the same expressions:
+// the same bits.
+template <typename T, int NV, bool ISO, bool PD3O, bool NT, bool PF = false>
 __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __restrict__ w,
                                                           const T* __restrict__ z, T* __restrict__ zo) {
   const PdsGeom<T> g = p.g;
@@ -108,6 +111,27 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
   const bool row_nb = r + 1 < n1, col_nb = c + NV < n2;
   T wn0[NV];  // w at the current plane (carried from the previous step)
   ldv<T, NV>(ws + (int64_t)pb * M, wn0);
+  // PF: the next plane's z, w row + 1 and w column + 1 (the loads below, one plane early)
+  T fz[3][NV], fr[NV], fcol;
+  auto fetch = [&](int pl) {
+    const int64_t off = (int64_t)pl * M;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      if (ax < a_first) continue;
+      if (NT)
+        ldn_nt<T, NV>(zs + (int64_t)(ax - a_first) * N + off, fz[ax]);
+      else
+        ldv<T, NV>(zs + (int64_t)(ax - a_first) * N + off, fz[ax]);
+    }
+    if (row_nb) {
+      ldv<T, NV>(ws + off + n2, fr);
+    } else {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) fr[e] = T(0);
+    }
+    fcol = col_nb ? ws[off + NV] : T(0);
+  };
+  if (PF) fetch(pb);
   for (int pl = pb; pl < pe; ++pl) {
     const int64_t off = (int64_t)pl * M;
     T wc[NV], wp[NV];
@@ -119,6 +143,17 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
 #pragma unroll
       for (int e = 0; e < NV; ++e) wp[e] = T(0);
     }
+    T cz[3][NV], cr[NV], ccol = T(0);
+    if (PF) {
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax)
+#pragma unroll
+        for (int e = 0; e < NV; ++e) cz[ax][e] = fz[ax][e];
+#pragma unroll
+      for (int e = 0; e < NV; ++e) cr[e] = fr[e];
+      ccol = fcol;
+      if (pl + 1 < pe) fetch(pl + 1);
+    }
     T zin[3][NV], zc[3][NV];
 #pragma unroll
     for (int ax = 0; ax < 3; ++ax) {
@@ -128,7 +163,10 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
 #pragma unroll
         for (int e = 0; e < NV; ++e) wn[e] = wp[e];
       } else if (ax == 1) {
-        if (row_nb) {
+        if (PF) {
+#pragma unroll
+          for (int e = 0; e < NV; ++e) wn[e] = cr[e];
+        } else if (row_nb) {
           ldv<T, NV>(ws + off + n2, wn);
         } else {
 #pragma unroll
@@ -137,9 +175,12 @@ __global__ void __launch_bounds__(kBlock) pds_dual_kernel(PdsC<T> p, const T* __
       } else {
 #pragma unroll
         for (int e = 0; e + 1 < NV; ++e) wn[e] = wc[e + 1];
-        wn[NV - 1] = col_nb ? ws[off + NV] : T(0);
+        wn[NV - 1] = PF ? ccol : (col_nb ? ws[off + NV] : T(0));
       }
-      if (NT)
+      if (PF) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) zc[ax][e] = cz[ax][e];
+      } else if (NT)
         ldn_nt<T, NV>(zs + (int64_t)(ax - a_first) * N + off, zc[ax]);
       else
         ldv<T, NV>(zs + (int64_t)(ax - a_first) * N + off, zc[ax]);
@@ -478,6 +519,15 @@ int launch_c(const PdsC<T>& pc, bool iso, int64_t M, int nseg, const void* w, co
   dim3 grid((unsigned)blocks, (unsigned)nseg, (unsigned)pc.g.stack);
   // z / z_out non-temporal (read / written once): w's row + 1 neighbours stay in L2 (1024^3, r04b: fetch 22.5
   // -> 19 B/voxel, 5.9 -> 5.1-5.7 ms)
+  if (rb != 1) {  // the next plane's loads one plane early (default; 1: without, A/B -- 1024^3 r06ar: 5.00 -> 4.94 ms)
+    if (iso)
+      hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O, true, true>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+                         (const T*)z, (T*)zo);
+    else
+      hipLaunchKernelGGL((pds_dual_kernel<T, NV, false, PD3O, true, true>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
+                         (const T*)z, (T*)zo);
+    return last_launch_status();
+  }
   if (iso)
     hipLaunchKernelGGL((pds_dual_kernel<T, NV, true, PD3O, true>), grid, dim3(kBlock), 0, st, pc, (const T*)w,
                        (const T*)z, (T*)zo);

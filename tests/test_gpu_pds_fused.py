@@ -287,13 +287,14 @@ def test_tv_dual_update_vs_oracle(dt, h_kind, sh, relax):
     assert rel_err(out, ref) <= TOL[dt], rel_err(out, ref)
 
 
-@pytest.mark.parametrize("rows", [2, 4, 8, 9])
+@pytest.mark.parametrize("rows", [1, 2, 4, 8, 9])
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
 @pytest.mark.parametrize("h_kind", ["l1", "iso"])
 @pytest.mark.parametrize("sh,stack", [((67, 129), 1), ((9, 33, 70), 1), ((5, 64, 128), 3), ((7, 37, 1024), 1),
                                       ((3, 1, 64), 2), ((6, 19, 260), 2)], ids=lambda s: "x".join(map(str, s)) if isinstance(s, tuple) else str(s))
 def test_tv_dual_update_row_blocked_bit_exact(rows, dt, h_kind, sh, stack):
-    """Kernel C with `rows` rows of w per thread (PXA_TUNE_DUAL_ROWS: a thread's row + 1 neighbours are its own rows;
+    """Kernel C with `rows` rows of w per thread (PXA_TUNE_DUAL_ROWS; 1: the one-row kernel without its next-plane
+    prefetch; 2, 4: a thread's row + 1 neighbours are its own rows;
     8: the plane-block kernel, whose row + 1 / column + 1 neighbours come from an LDS image of the block, 3-D fp32)
     gives the one-row kernel's bits: odd row counts (the last block's missing rows), partial column blocks, a single
     row, stacks, 2-D and 3-D, both relaxations."""
