@@ -78,6 +78,11 @@ class _PrimalDualSplitting(pxa.Solver):
         self._la = None  # look-ahead step: (state arrays it was computed for, x of the next iteration)
         self._zspare = None
         self._plan = self._fused_plan(mst["x"]) if fused else None
+        if self._plan is not None:
+            # the fused steps never write a tensor they have published as x while anything else references it (new
+            # or recycled buffers, reuse guarded by the reference count): stop criteria may keep references instead
+            # of copies (RelError: no 4-byte-per-voxel copy of x at every check)
+            mst["__immutable__"] = frozenset({"x"})
 
     _FUSED_ALGO = None  # pxa_pds_step algo code of the subclass (0 PD3O, 1 CondatVu), None: no fused step
 
