@@ -97,8 +97,8 @@ if [ "$S" = "c3prof" ]; then
   step fetchc3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetchc3 -o run --output-format csv -- $B3
   step writec3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/writec3 -o run --output-format csv -- $B3
   for k in "pds_plane_kernel<float, 6, 0>:pds_plane_kernel_pd3o@1024^3" "pds_plane_kernel<float, 6, 2>:pds_plane_kernel_cv@1024^3" \
-           "pds_march_kernel<float, 6, 1, true, false, true, true>:pds_march_kernel_pd3o@1024^3" \
-           "pds_march_kernel<float, 6, 1, false, false, true, true>:pds_march_kernel_cv@1024^3"; do
+           "pds_march_kernel<float, 6, 1, true, false, true, true, false, 1>:pds_march_kernel_pd3o@1024^3" \
+           "pds_march_kernel<float, 6, 1, false, false, true, true, false, 1>:pds_march_kernel_cv@1024^3"; do
     python3 scripts/pmc_traffic.py $P/fetchc3 $P/writec3 "${k%%:*}" "${k##*:}" $P/traffic_c3.json $T || true
   done
   K42="python3 bench.py --only k4 --k4-which 2d"
